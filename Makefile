@@ -1,0 +1,50 @@
+# Top-level build: the HIP product library, the `sahara` CLI and the oracle.
+# gfx950 (MI355X) only. `make -j8` here cross-compiles without a GPU.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall
+LIBDIR   := sahara_amd/lib
+OBJDIR   := build/obj
+CSRC     := sahara_amd/csrc
+LIB      := $(LIBDIR)/libsahara_hip.so
+CLI      := bin/sahara
+HDRS     := $(wildcard $(CSRC)/*.h) include/sahara_hip.h
+
+OBJS := $(OBJDIR)/index_build.o $(OBJDIR)/search.o $(OBJDIR)/capi.o $(OBJDIR)/host_util.o $(OBJDIR)/scheme.o
+
+all: $(LIB) oracle $(if $(wildcard sahara_amd/cli/*.cpp),$(CLI),)
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/capi.o: $(CSRC)/capi.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/scheme.o: $(CSRC)/scheme.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/host_util.o: $(CSRC)/host_util.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ -lpthread
+
+CLI_SRC := $(wildcard sahara_amd/cli/*.cpp)
+$(CLI): $(CLI_SRC) $(wildcard sahara_amd/cli/*.h) include/sahara_hip.h $(LIB)
+	@mkdir -p bin
+	g++ $(CXXFLAGS) -Iinclude $(CLI_SRC) -o $@ -L$(LIBDIR) -lsahara_hip -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIBDIR) bin
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

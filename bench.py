@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""bench.py — reads/s of sahara's search hot path on MI355X (BASELINE.json metric).
+
+A "step" is one pass of the hot path (search-scheme DFS + locate + canonical
+sort) over the whole batch of synthetic reads of the configured workload,
+with the reads (and their reverse complements, search.cpp:121-123) already
+resident in HBM. Default workload = BASELINE.json configs[2] (C3): k=2
+Levenshtein, 10M x 100 bp reads vs a 3 Gbp, 24-record synthetic reference
+(record lengths proportional to GRCh38 chromosomes), default
+generator h2-k2.
+
+Multi-GPU (torchrun, one process per GPU): every rank builds the full index
+on its own GPU (replicated, as SURVEY §8(e) prescribes), searches its own
+shard of 10M reads (weak scaling), and the per-rank hit counts and digests
+are all-gathered over RCCL. No collective sits on the data path.
+
+Rank 0 at N=1 also times the CPU restatement (oracle/, the reference's
+algorithm restated in C++) on a bounded sample of the same reads on the host
+cores, and checks GPU == CPU hits on that sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GRCH38 = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973, 145138636,
+          138394717, 133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345,
+          83257441, 80373285, 58617616, 64444167, 46709983, 50818468, 156040895, 57227415]
+
+CONFIGS = {
+    # name: (ref_len, n_records, reads per GPU, read_len, errors, edit, generator)
+    "c1": (1_000_000, 1, 1_000, 32, 0, True, "h2-k2"),
+    "c2": (100_000_000, 1, 1_000_000, 100, 1, False, "h2-k2"),
+    "c3": (3_000_000_000, 24, 10_000_000, 100, 2, True, "h2-k2"),
+    "c5": (3_000_000_000, 24, 1_000_000, 250, 3, True, "h2-k2"),
+}
+
+METRIC = "reads/s at k=2 edit, 10M×100bp vs 3Gbp index; achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def record_lengths(total, n):
+    if n == 1:
+        return np.array([total], np.uint64)
+    w = np.array(GRCH38[:n], np.float64)
+    lens = np.floor(w / w.sum() * total).astype(np.uint64)
+    lens[0] += np.uint64(total - int(lens.sum()))
+    return lens
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads():
+    # the GPU box grants 16 host cores per GPU (OMP_NUM_THREADS is set to it)
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if n <= 0:
+        n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return max(1, min(n, 16))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--reads", type=int, default=0, help="override reads per GPU")
+    ap.add_argument("--ref-len", type=int, default=0, help="override reference length")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch  # plumbing only: device sync + torch.distributed (RCCL)
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import sahara_amd as sa
+
+    ref_len, nrec, nreads, rlen, k, edit, gen = CONFIGS[args.config]
+    if args.ref_len:
+        ref_len = args.ref_len
+    if args.reads:
+        nreads = args.reads
+    sigma = 6
+
+    lens = record_lengths(ref_len, nrec)
+    t = time.time()
+    flat, lens = sa.synth_reference(lens, sigma=sigma, seed=42)
+    log(f"rank {rank}: reference {ref_len/1e9:.3f} Gbp in {len(lens)} records ({time.time()-t:.1f}s)")
+    t = time.time()
+    idx = sa.BiFMIndex.build_flat(flat, lens, sigma=sigma, sampling_rate=16, device=local)
+    build_s = time.time() - t
+    info = idx.info()
+    log(f"rank {rank}: GPU index built in {build_s:.1f}s, {info['device_bytes']/1e9:.2f} GB resident")
+
+    t = time.time()
+    reads = sa.synth_reads(flat, lens, nreads, rlen, k, sigma=sigma, seed=7 + 1000003 * rank)
+    pats = sa.interleave_rc(reads, sigma)
+    scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
+    idx.stage(pats, scheme, edit=edit)
+    log(f"rank {rank}: {nreads} reads (+RC) simulated and staged in HBM ({time.time()-t:.1f}s), "
+        f"{scheme[0].shape[0]} searches")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        t = time.time()
+        idx.run()
+        log(f"rank {rank}: warmup {i} {time.time()-t:.2f}s")
+
+    barrier()
+    t0 = time.perf_counter()
+    search_ms = locate_ms = sort_ms = 0.0
+    launches = 0
+    for i in range(args.steps):
+        nh = idx.run()
+        st = idx.stats()
+        search_ms += st["search_ms"]
+        locate_ms += st["locate_ms"]
+        sort_ms += st["sort_ms"]
+        launches += st["search_launches"]
+    barrier()
+    elapsed = time.perf_counter() - t0
+    digest = idx.digest()
+
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        rec = torch.tensor([nh, digest & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64, device="cuda")
+        allrec = [torch.zeros_like(rec) for _ in range(world)]
+        dist.all_gather(allrec, rec)  # RCCL over xGMI: per-rank hit counts + digests
+        total_hits = int(sum(int(r[0]) for r in allrec))
+    else:
+        total_hits = nh
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    reads_per_s = nreads * world * args.steps / elapsed
+
+    # instrumented run (untimed): deterministic work counters -> algorithmic bytes
+    cnt = None
+    if not args.no_count:
+        idx.run(count=True)
+        cnt = idx.stats()
+    search_ms_step = search_ms / args.steps
+    roofline = None
+    extra = {}
+    if cnt:
+        search_bytes = 64.0 * cnt["ext_lines"] + pats.size  # Occ lines + pattern bytes
+        locate_bytes = 64.0 * (cnt["lf_steps"] + 2 * cnt["hits"])  # LF lines + final line + sample
+        achieved = search_bytes / (search_ms_step / 1e3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
+        extra = {"bytes_per_read": round((search_bytes + locate_bytes) / nreads, 1),
+                 "nodes_per_read": round(cnt["nodes"] / nreads, 1),
+                 "ext_lines_per_read": round(cnt["ext_lines"] / nreads, 1),
+                 "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
+                 "search_ms": round(search_ms_step, 2), "locate_ms": round(locate_ms / args.steps, 2),
+                 "sort_ms": round(sort_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
+                 "search_grid": cnt["search_grid"],
+                 "locate_achieved_GBs": round(locate_bytes / (locate_ms / args.steps / 1e3) / 1e9, 1)
+                 if locate_ms > 0 else None}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(sa, idx, pats, scheme, edit, nreads, args.cpu_seconds)
+
+    out = {
+        "metric": METRIC,
+        "value": round(reads_per_s, 1),
+        "unit": "reads/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": f"{args.config.upper()}: k={k} {'lev' if edit else 'ham'}, {nreads}x{rlen}bp reads "
+                               f"(+RC) per GPU vs {ref_len/1e9:g} Gbp {len(lens)}-record index, {gen}",
+                   "reads_per_gpu": nreads, "read_len": rlen, "errors": k, "ref_len": ref_len,
+                   "records": int(len(lens)), "generator": gen, "searches": int(scheme[0].shape[0]),
+                   "parallelism": f"replicated-index x{world} (query shards)", "index_build_s": round(build_s, 1),
+                   "hits_total": total_hits, **extra},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    if cpu and cpu.get("value"):
+        out["config"]["gpu_over_cpu"] = round(reads_per_s / cpu["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):
+    """Time the CPU restatement on a bounded sample; check GPU == CPU on it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    t = time.time()
+    ex = idx.export()
+    ref = O.Index.from_parts(ex["sigma"], ex["n"], ex["rec_lens"], ex["rate"], ex["bwt_f"], ex["bwt_r"],
+                             ex["sampled"], ex["samples"])
+    del ex
+    log(f"cpu baseline: oracle index loaded ({time.time()-t:.1f}s)")
+    threads = host_threads()
+    # calibrate on a small sample, then scale to ~target_s
+    n = min(200, nreads)
+    t = time.perf_counter()
+    ref.search(pats[: 2 * n], scheme, edit=edit, nthreads=threads)
+    dt = time.perf_counter() - t
+    n2 = int(min(nreads, max(n, n * target_s / max(dt, 1e-3))))
+    t = time.perf_counter()
+    hits, _ = ref.search(pats[: 2 * n2], scheme, edit=edit, nthreads=threads)
+    dt = time.perf_counter() - t
+    rate = n2 / dt
+    # single-thread figure (the reference's execution model, search.cpp:221-241)
+    n1 = max(20, min(n2, int(n2 / threads / 4)))
+    t = time.perf_counter()
+    ref.search(pats[: 2 * n1], scheme, edit=edit, nthreads=1)
+    rate1 = n1 / (time.perf_counter() - t)
+    # parity on the sample
+    gpu_hits = sa.search(idx, pats[: 2 * n2], scheme, edit=edit)
+    from_gpu = np.stack([gpu_hits["qid"], gpu_hits["seq_id"], gpu_hits["pos"], gpu_hits["err"]], 1).astype(np.uint64)
+    h = np.asarray(hits, np.uint64)
+    order = np.lexsort((h[:, 3], h[:, 2], h[:, 1], h[:, 0]))
+    parity = bool(len(h) == len(from_gpu) and np.array_equal(h[order], from_gpu))
+    log(f"cpu baseline: {n2} reads in {dt:.1f}s on {threads} threads = {rate:.0f} reads/s "
+        f"(1 thread: {rate1:.0f} reads/s); GPU==CPU on sample: {parity}")
+    return {"value": round(rate, 1), "unit": "reads/s", "cores": threads, "kind": "port",
+            "sample": f"first {n2} reads (+RC) of the same workload, {dt:.1f}s; "
+                      f"1-thread rate {rate1:.1f} reads/s on {n1} reads; host CPU: {cpu_model()}",
+            "single_thread_value": round(rate1, 1), "parity_on_sample": parity}
+
+
+if __name__ == "__main__":
+    main()

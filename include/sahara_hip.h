@@ -1,0 +1,159 @@
+/*
+ * sahara_hip.h — C ABI of libsahara_hip.so, the MI355X (gfx950) drop-in for
+ * sahara's search hot path.
+ *
+ * Reference interfaces this ABI replaces (paths under /root/reference):
+ *   - fmc::BiFMIndex<Sigma, InterleavedBitvector16> load
+ *       src/sahara/search.cpp:162-169           -> sahara_gpu_open / sahara_gpu_open_file
+ *   - fmc::BiFMIndex{ref, samplingRate, threadNbr} construction + cereal save
+ *       src/sahara/index.cpp:87-100             -> sahara_gpu_build / sahara_gpu_save
+ *   - fmc::search_ng24::search<Edit>(index, queries, scheme, res_cb)
+ *       src/sahara/search.cpp:218-231           -> sahara_gpu_search (search half)
+ *   - fmc::LocateLinear{index, cursor}
+ *       src/sahara/search.cpp:244-250           -> sahara_gpu_search (locate half)
+ *   - search_n (--max_hits)  src/sahara/search.cpp:228,231 -> max_hits argument (reserved, must be 0 this round)
+ *
+ * Conventions: plain C types only; 0 on success, negative on error with a
+ * thread-local message from sahara_gpu_last_error(); no exceptions cross the
+ * boundary. The caller owns every input buffer; the library owns `*hits`
+ * until sahara_gpu_free. One context per device, used from one host thread.
+ * Patterns are rank-encoded (ivsigma d_dna4/d_dna5 codes, 1..sigma-1), all of
+ * the same length `len` (search.cpp:187 assumes this too), laid out
+ * back-to-back. Qid i is the i-th pattern, exactly as in the reference's
+ * `queries` vector (reverse complements interleaved by the caller,
+ * search.cpp:121-123).
+ *
+ * Hits come back in canonical order: sorted by (qid, seq_id, pos, err). The
+ * multiset equals the reference restatement's (one record per reported
+ * cursor per located SA row; duplicates kept).
+ */
+#ifndef SAHARA_HIP_H
+#define SAHARA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One located hit: query id, record id, 0-based position in the record,
+ * number of errors of the reported alignment (search.cpp:246-248). 24 B. */
+typedef struct sahara_hit {
+    uint64_t qid;
+    uint32_t seq_id;
+    uint32_t err;
+    uint64_t pos;
+} sahara_hit;
+
+typedef struct sahara_index_info {
+    uint32_t sigma;          /* 5 (d_dna4) or 6 (d_dna5) */
+    uint32_t sampling_rate;  /* SA sampling rate (16 in index.cpp:87) */
+    uint64_t n;              /* text length incl. one delimiter per record */
+    uint64_t n_records;
+    uint64_t n_samples;
+    uint64_t device_bytes;   /* HBM held by the resident index */
+} sahara_index_info;
+
+/* Per-run statistics of the last sahara_gpu_search / sahara_gpu_run call. */
+typedef struct sahara_stats {
+    uint64_t patterns;
+    uint64_t batches;
+    uint64_t cursors;        /* reported (qid, cursor, e) records */
+    uint64_t hits;           /* located rows = hit records */
+    double   search_ms;      /* device time of the search kernels (HIP events) */
+    double   locate_ms;      /* device time of locate (incl. row-offset scan) */
+    double   sort_ms;        /* device time of the canonical sort + decode */
+    double   total_ms;       /* wall time of the whole call */
+    /* Filled only by sahara_gpu_run(..., count=1): algorithmic work counters. */
+    uint64_t nodes;          /* DFS nodes expanded */
+    uint64_t rank_nodes;     /* nodes that ranked (M/S/D allowed) */
+    uint64_t ext_lines;      /* distinct 64-position Occ lines those ranks touched */
+    uint64_t lf_steps;       /* LF steps in locate */
+    uint32_t search_launches;
+    uint32_t search_grid;    /* workgroups per search launch */
+} sahara_stats;
+
+const char* sahara_gpu_last_error(void);
+int  sahara_gpu_device_count(void);
+
+/* --- index residency (replaces the cereal load at search.cpp:162-169) --- */
+/* idx_image: the bytes of a `.idx` file as written by `sahara index`. */
+int  sahara_gpu_open(int device, const void* idx_image, size_t idx_bytes, void** ctx);
+int  sahara_gpu_open_file(int device, const char* idx_path, void** ctx);
+/* GPU index construction (replaces index.cpp:87): ranks = records
+ * concatenated without delimiters, rec_lens[n_records]. */
+int  sahara_gpu_build(int device, const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records,
+                      uint32_t sigma, uint32_t sampling_rate, void** ctx);
+int  sahara_gpu_save(void* ctx, const char* path);          /* .idx writer (index.cpp:92-100) */
+int  sahara_gpu_index_info(void* ctx, sahara_index_info* info);
+/* Copy out the index parts (any pointer may be NULL): BWT of the text and of
+ * the per-record reversed text (n bytes each), sampled-row bitvector
+ * (n/64+1 words), SA samples (n_samples u32 text positions, row order),
+ * C array (sigma+1 u64) and record lengths (n_records u64). */
+int  sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* sampled_bits,
+                       uint32_t* samples, uint64_t* C, uint64_t* rec_lens);
+/* Full suffix array of the last sahara_gpu_build (test hook; n u32). */
+int  sahara_gpu_export_sa(void* ctx, uint32_t* sa);
+
+/* --- search + locate (replaces search.cpp:218-250) ---
+ * pi/l/u: the expanded search scheme, n_searches rows of len entries each
+ * (fmc::search_scheme::expand output, search.cpp:191; limitToHamming already
+ * applied by the caller for edit == 0, search.cpp:226). */
+int  sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len,
+                       const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,
+                       int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits);
+
+/* Device-resident form of the same path for benchmarking: stage patterns and
+ * scheme once, run search+locate+sort with results left in HBM, fetch later. */
+int  sahara_gpu_stage(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len,
+                      const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,
+                      int edit);
+int  sahara_gpu_run(void* ctx, int count, uint64_t* n_hits);
+int  sahara_gpu_fetch(void* ctx, sahara_hit* out, uint64_t capacity, uint64_t* n_hits);
+/* Order-independent digest of the last run's hits (sum of a 64-bit mix of
+ * each record) computed on the device. */
+int  sahara_gpu_digest(void* ctx, uint64_t* digest);
+int  sahara_gpu_stats(void* ctx, sahara_stats* stats);
+
+void sahara_gpu_free(void* p);
+void sahara_gpu_close(void* ctx);
+
+/* --- search schemes (replaces generator::all / expand / limitToHamming,
+ * search.cpp:174-212, :226) --- */
+/* Registered generator names/descriptions; returns the count. */
+int  sahara_scheme_generators(const char** names, const char** descs, int cap);
+/* Expanded scheme for `len`-long patterns: n_searches rows of len entries in
+ * pi/l/u (pass pi == NULL to get the number of searches). hamming != 0 applies
+ * limitToHamming. Returns the number of searches, -1 unknown generator/k,
+ * -2 capacity, -3 len shorter than the number of parts. */
+int  sahara_scheme(const char* generator, int min_k, int max_k, uint32_t len, int hamming,
+                   uint32_t* pi, uint32_t* l, uint32_t* u, int max_searches);
+/* Part-level (unexpanded) scheme: *parts = number of parts P; n_searches*P
+ * entries per array. Returns the number of searches. */
+int  sahara_scheme_parts(const char* generator, int min_k, int max_k, int* parts, int* pi, int* l, int* u,
+                         int max_entries);
+/* Node count / weighted node count of an expanded scheme (search.cpp:197-198). */
+int  sahara_scheme_counts(const uint32_t* l, const uint32_t* u, uint32_t n_searches, uint32_t len, int edit,
+                          int sigma, double text_len, double* node_count, double* weighted_node_count);
+
+/* --- synthetic inputs (host-side generators, BASELINE.md §2 / SURVEY §8(d)) --- */
+/* Uniform i.i.d. ACGT records (ranks 1,2,3 and 4 (dna4) / 5 (dna5) for T),
+ * std::mt19937_64(seed), 32 bases per draw. */
+int  sahara_synth_reference(uint64_t seed, uint32_t sigma, const uint64_t* rec_lens, uint64_t n_records,
+                            uint8_t* out_ranks);
+/* read_simulator.cpp:119-240 restated: n_reads reads of exactly `len`
+ * symbols sampled from the records with exactly `errors` transcript errors of
+ * uniformly chosen type S/I/D each; read origin (record, pos) written to
+ * origin[2*i], origin[2*i+1] when origin != NULL. */
+int  sahara_synth_reads(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
+                        uint64_t n_reads, uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out,
+                        uint64_t* origin);
+/* Reverse complement interleave of search.cpp:121-123: out[2i] = read i,
+ * out[2i+1] = its reverse complement (A<->T, C<->G, N->N). */
+int  sahara_interleave_rc(const uint8_t* reads, uint64_t n_reads, uint32_t len, uint32_t sigma, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAHARA_HIP_H */

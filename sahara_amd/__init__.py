@@ -1,0 +1,369 @@
+"""sahara_amd — MI355X-native drop-in for sahara's search hot path.
+
+Python mirror of the reference's operator interface for that path
+(/root/reference/src/sahara/search.cpp:104-274), over the C ABI of
+``sahara_amd/lib/libsahara_hip.so`` (include/sahara_hip.h):
+
+    idx    = BiFMIndex.build(records, sigma=6)       # index.cpp:87  (GPU construction)
+    idx    = BiFMIndex.load("ref.fa.idx")             # search.cpp:162-169
+    scheme = search_scheme("h2-k2", 0, k, len)        # search.cpp:174-212 (+ :226 for ham)
+    hits   = search(idx, queries, scheme, edit=True)  # search.cpp:218-250
+
+There is no CPU fallback: every entry point runs the HIP kernels and fails
+loudly when the extension or the GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = [
+    "BiFMIndex", "HIT_DTYPE", "search", "search_scheme", "scheme_parts", "scheme_generators",
+    "scheme_counts", "synth_reference", "synth_reads", "interleave_rc", "load_fasta",
+    "library_path", "lib", "SaharaError", "DNA5", "DNA4",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+# ivsigma delimited alphabets: rank 0 is the delimiter '$'.
+DNA5 = {"sigma": 6, "chars": "$ACGNT"}
+DNA4 = {"sigma": 5, "chars": "$ACGT"}
+
+HIT_DTYPE = np.dtype([("qid", "<u8"), ("seq_id", "<u4"), ("err", "<u4"), ("pos", "<u8")])
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+
+
+class SaharaError(RuntimeError):
+    pass
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [("sigma", C.c_uint32), ("sampling_rate", C.c_uint32), ("n", C.c_uint64),
+                ("n_records", C.c_uint64), ("n_samples", C.c_uint64), ("device_bytes", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("patterns", C.c_uint64), ("batches", C.c_uint64), ("cursors", C.c_uint64),
+                ("hits", C.c_uint64), ("search_ms", C.c_double), ("locate_ms", C.c_double),
+                ("sort_ms", C.c_double), ("total_ms", C.c_double), ("nodes", C.c_uint64),
+                ("rank_nodes", C.c_uint64), ("ext_lines", C.c_uint64), ("lf_steps", C.c_uint64),
+                ("search_launches", C.c_uint32), ("search_grid", C.c_uint32)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+EXPORTED = {
+    # name: (restype, argtypes)
+    "sahara_gpu_last_error": (C.c_char_p, []),
+    "sahara_gpu_device_count": (C.c_int, []),
+    "sahara_gpu_open": (C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "sahara_gpu_open_file": (C.c_int, [C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "sahara_gpu_build": (C.c_int, [C.c_int, u8p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                   C.POINTER(C.c_void_p)]),
+    "sahara_gpu_save": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "sahara_gpu_index_info": (C.c_int, [C.c_void_p, C.POINTER(IndexInfo)]),
+    "sahara_gpu_export": (C.c_int, [C.c_void_p, u8p, u8p, u64p, u32p, u64p, u64p]),
+    "sahara_gpu_export_sa": (C.c_int, [C.c_void_p, u32p]),
+    "sahara_gpu_search": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
+                                    C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
+                                    C.POINTER(C.c_uint64)]),
+    "sahara_gpu_stage": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
+                                   C.c_uint32, C.c_int]),
+    "sahara_gpu_run": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
+    "sahara_gpu_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "sahara_gpu_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "sahara_gpu_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "sahara_gpu_free": (None, [C.c_void_p]),
+    "sahara_gpu_close": (None, [C.c_void_p]),
+    "sahara_scheme_generators": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int]),
+    "sahara_scheme": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_int, u32p, u32p, u32p,
+                                C.c_int]),
+    "sahara_scheme_parts": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                      C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                      C.c_int]),
+    "sahara_scheme_counts": (C.c_int, [u32p, u32p, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                                       C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "sahara_synth_reference": (C.c_int, [C.c_uint64, C.c_uint32, u64p, C.c_uint64, u8p]),
+    "sahara_synth_reads": (C.c_int, [u8p, u64p, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
+                                     C.c_uint32, C.c_uint64, u8p, u64p]),
+    "sahara_interleave_rc": (C.c_int, [u8p, C.c_uint64, C.c_uint32, C.c_uint32, u8p]),
+}
+
+
+def library_path():
+    return os.path.join(_HERE, "lib", "libsahara_hip.so")
+
+
+def lib():
+    """Load libsahara_hip.so. Raises if it is missing: there is no fallback."""
+    global _LIB
+    if _LIB is None:
+        path = library_path()
+        if not os.path.exists(path):
+            raise ImportError(f"sahara_amd HIP extension missing: {path} (run `make` / "
+                              f"__graft_entry__.build())")
+        L = C.CDLL(path)
+        for name, (res, args) in EXPORTED.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().sahara_gpu_last_error()
+        raise SaharaError(msg.decode() if msg else f"error {rc}")
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+def _records_to_flat(records):
+    recs = [np.ascontiguousarray(r, dtype=np.uint8) for r in records]
+    if not recs:
+        raise SaharaError("reference is empty")
+    flat = np.ascontiguousarray(np.concatenate(recs))
+    lens = np.array([len(r) for r in recs], dtype=np.uint64)
+    return flat, lens
+
+
+class BiFMIndex:
+    """GPU-resident bidirectional FM-index (fmc::BiFMIndex<Sigma, InterleavedBitvector16>)."""
+
+    def __init__(self, handle, device):
+        self._h = C.c_void_p(handle)
+        self.device = device
+
+    @classmethod
+    def build(cls, records, sigma=6, sampling_rate=16, device=0):
+        flat, lens = _records_to_flat(records)
+        h = C.c_void_p()
+        _check(lib().sahara_gpu_build(device, _p(flat, u8p), _p(lens, u64p), len(lens), sigma,
+                                      sampling_rate, C.byref(h)))
+        return cls(h.value, device)
+
+    @classmethod
+    def build_flat(cls, flat, rec_lens, sigma=6, sampling_rate=16, device=0):
+        flat = np.ascontiguousarray(flat, dtype=np.uint8)
+        lens = np.ascontiguousarray(rec_lens, dtype=np.uint64)
+        h = C.c_void_p()
+        _check(lib().sahara_gpu_build(device, _p(flat, u8p), _p(lens, u64p), len(lens), sigma,
+                                      sampling_rate, C.byref(h)))
+        return cls(h.value, device)
+
+    @classmethod
+    def load(cls, path, device=0):
+        h = C.c_void_p()
+        _check(lib().sahara_gpu_open_file(device, str(path).encode(), C.byref(h)))
+        return cls(h.value, device)
+
+    @classmethod
+    def from_bytes(cls, data, device=0):
+        buf = np.frombuffer(data, dtype=np.uint8)
+        h = C.c_void_p()
+        _check(lib().sahara_gpu_open(device, buf.ctypes.data_as(C.c_void_p), buf.nbytes, C.byref(h)))
+        return cls(h.value, device)
+
+    def save(self, path):
+        _check(lib().sahara_gpu_save(self._h, str(path).encode()))
+
+    def info(self):
+        i = IndexInfo()
+        _check(lib().sahara_gpu_index_info(self._h, C.byref(i)))
+        return {n: getattr(i, n) for n, _ in i._fields_}
+
+    @property
+    def sigma(self):
+        return self.info()["sigma"]
+
+    def export(self):
+        inf = self.info()
+        n = inf["n"]
+        bf = np.zeros(n, np.uint8)
+        br = np.zeros(n, np.uint8)
+        sb = np.zeros(n // 64 + 1, np.uint64)
+        smp = np.zeros(max(inf["n_samples"], 1), np.uint32)
+        Cc = np.zeros(8, np.uint64)
+        rl = np.zeros(max(inf["n_records"], 1), np.uint64)
+        _check(lib().sahara_gpu_export(self._h, _p(bf, u8p), _p(br, u8p), _p(sb, u64p),
+                                       _p(smp, u32p), _p(Cc, u64p), _p(rl, u64p)))
+        return dict(bwt_f=bf, bwt_r=br, sampled=sb, samples=smp[: inf["n_samples"]],
+                    C=Cc[: inf["sigma"] + 1], rec_lens=rl[: inf["n_records"]], n=n,
+                    sigma=inf["sigma"], rate=inf["sampling_rate"])
+
+    def export_sa(self):
+        n = self.info()["n"]
+        sa = np.zeros(n, np.uint32)
+        _check(lib().sahara_gpu_export_sa(self._h, _p(sa, u32p)))
+        return sa
+
+    # ---- device-resident path (bench) ----
+    def stage(self, queries, scheme, edit=True):
+        q = np.ascontiguousarray(queries, dtype=np.uint8)
+        pi, l, u = (np.ascontiguousarray(a, dtype=np.uint32) for a in scheme)
+        _check(lib().sahara_gpu_stage(self._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
+                                      _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit)))
+
+    def run(self, count=False):
+        n = C.c_uint64()
+        _check(lib().sahara_gpu_run(self._h, int(count), C.byref(n)))
+        return n.value
+
+    def fetch(self):
+        n = C.c_uint64()
+        st = self.stats()
+        out = np.zeros(max(st["hits"], 1), HIT_DTYPE)
+        _check(lib().sahara_gpu_fetch(self._h, out.ctypes.data_as(C.c_void_p), len(out), C.byref(n)))
+        return out[: n.value]
+
+    def digest(self):
+        d = C.c_uint64()
+        _check(lib().sahara_gpu_digest(self._h, C.byref(d)))
+        return d.value
+
+    def stats(self):
+        s = Stats()
+        _check(lib().sahara_gpu_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def close(self):
+        if self._h and self._h.value:
+            lib().sahara_gpu_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def search(index, queries, scheme, edit=True, max_hits=0):
+    """fmc::search_ng24::search<Edit> + fmc::LocateLinear (search.cpp:218-250).
+
+    queries: (n_patterns, len) uint8 ranks (qid = row); scheme: (pi, l, u),
+    each (n_searches, len). Returns a HIT_DTYPE array sorted by
+    (qid, seq_id, pos, err)."""
+    q = np.ascontiguousarray(queries, dtype=np.uint8)
+    if q.ndim != 2 or q.shape[0] == 0:
+        raise SaharaError("queries must be a non-empty (n_patterns, len) array")
+    pi, l, u = (np.ascontiguousarray(a, dtype=np.uint32) for a in scheme)
+    out = C.c_void_p()
+    n = C.c_uint64()
+    _check(lib().sahara_gpu_search(index._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
+                                   _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit), max_hits,
+                                   C.byref(out), C.byref(n)))
+    try:
+        if n.value == 0:
+            return np.zeros(0, HIT_DTYPE)
+        raw = (C.c_uint8 * (n.value * HIT_DTYPE.itemsize)).from_address(out.value)
+        return np.frombuffer(raw, dtype=HIT_DTYPE).copy()
+    finally:
+        lib().sahara_gpu_free(out)
+
+
+def scheme_generators():
+    n = lib().sahara_scheme_generators(None, None, 0)
+    names = (C.c_char_p * n)()
+    descs = (C.c_char_p * n)()
+    lib().sahara_scheme_generators(names, descs, n)
+    return {names[i].decode(): descs[i].decode() for i in range(n)}
+
+
+def search_scheme(generator, min_k, max_k, length, hamming=False):
+    """generator::all[name](minK, maxK) -> expand(len) [-> limitToHamming] (search.cpp:186-212, :226)."""
+    L = lib()
+    n = L.sahara_scheme(generator.encode(), min_k, max_k, length, int(hamming), None, None, None, 0)
+    if n < 0:
+        names = ", ".join(scheme_generators())
+        raise SaharaError(f'unknown search scheme generetaror "{generator}", valid generators are: {names}')
+    pi = np.zeros((n, length), np.uint32)
+    l = np.zeros((n, length), np.uint32)
+    u = np.zeros((n, length), np.uint32)
+    rc = L.sahara_scheme(generator.encode(), min_k, max_k, length, int(hamming), _p(pi, u32p),
+                         _p(l, u32p), _p(u, u32p), n)
+    if rc != n:
+        raise SaharaError(f"cannot expand scheme {generator} to length {length} (rc={rc})")
+    return pi, l, u
+
+
+def scheme_parts(generator, min_k, max_k):
+    P = C.c_int()
+    n = lib().sahara_scheme_parts(generator.encode(), min_k, max_k, C.byref(P), None, None, None, 0)
+    if n < 0:
+        raise SaharaError(f"unknown generator {generator}")
+    cap = n * P.value
+    pi = (C.c_int * cap)()
+    l = (C.c_int * cap)()
+    u = (C.c_int * cap)()
+    lib().sahara_scheme_parts(generator.encode(), min_k, max_k, C.byref(P), pi, l, u, cap)
+    sh = (n, P.value)
+    return (np.array(pi[:], np.int64).reshape(sh), np.array(l[:], np.int64).reshape(sh),
+            np.array(u[:], np.int64).reshape(sh))
+
+
+def scheme_counts(scheme, edit, sigma, text_len):
+    pi, l, u = (np.ascontiguousarray(a, dtype=np.uint32) for a in scheme)
+    a, b = C.c_double(), C.c_double()
+    lib().sahara_scheme_counts(_p(l, u32p), _p(u, u32p), pi.shape[0], pi.shape[1], int(edit), sigma,
+                               float(text_len), C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def synth_reference(lengths, sigma=6, seed=42):
+    lens = np.ascontiguousarray(lengths, dtype=np.uint64)
+    out = np.zeros(int(lens.sum()), np.uint8)
+    _check(lib().sahara_synth_reference(seed, sigma, _p(lens, u64p), len(lens), _p(out, u8p)))
+    return out, lens
+
+
+def synth_reads(flat, rec_lens, n_reads, length, errors, sigma=6, seed=7, with_origin=False):
+    flat = np.ascontiguousarray(flat, dtype=np.uint8)
+    lens = np.ascontiguousarray(rec_lens, dtype=np.uint64)
+    out = np.zeros((n_reads, length), np.uint8)
+    origin = np.zeros((n_reads, 2), np.uint64) if with_origin else None
+    _check(lib().sahara_synth_reads(_p(flat, u8p), _p(lens, u64p), len(lens), sigma, n_reads, length,
+                                    errors, seed, _p(out, u8p), _p(origin, u64p)))
+    return (out, origin) if with_origin else out
+
+
+def interleave_rc(reads, sigma=6):
+    """search.cpp:121-123: qid 2i = read i, 2i+1 = its reverse complement."""
+    r = np.ascontiguousarray(reads, dtype=np.uint8)
+    out = np.zeros((2 * r.shape[0], r.shape[1]), np.uint8)
+    _check(lib().sahara_interleave_rc(_p(r, u8p), r.shape[0], r.shape[1], sigma, _p(out, u8p)))
+    return out
+
+
+def load_fasta(path, sigma=6):
+    """Minimal FASTA reader -> list of (id, ranks) (ivio::fasta::reader + convert_char_to_rank)."""
+    table = np.full(256, 255, np.uint8)
+    chars = DNA5["chars"] if sigma == 6 else DNA4["chars"]
+    for r, ch in enumerate(chars):
+        if r == 0:
+            continue
+        table[ord(ch)] = r
+        table[ord(ch.lower())] = r
+    recs, name, seq = [], None, []
+    with open(path, "rb") as f:
+        for line in f:
+            line = line.rstrip(b"\r\n")
+            if line.startswith(b">"):
+                if name is not None:
+                    recs.append((name, table[np.frombuffer(b"".join(seq), np.uint8)]))
+                name, seq = line[1:].decode(), []
+            elif line:
+                seq.append(line)
+    if name is not None:
+        recs.append((name, table[np.frombuffer(b"".join(seq), np.uint8)]))
+    return recs

@@ -1,0 +1,498 @@
+// capi.cpp — the C ABI of libsahara_hip.so (include/sahara_hip.h).
+//
+// The drop-in boundary for sahara's hot path: index residency
+// (search.cpp:162-169), GPU index construction (index.cpp:87-100), and
+// search + locate (search.cpp:218-250). No C++ types or exceptions cross it.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sahara_hip.h"
+#include "device_index.h"
+#include "idx_format.h"
+#include "search.h"
+
+using namespace sahara;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Ctx {
+    int device = 0;
+    hipStream_t st = nullptr;
+    int numCU = 0;
+    DeviceIndex I;
+
+    // staged inputs
+    DevBuf<uint8_t> pats;
+    uint64_t npat = 0;
+    uint32_t m = 0;
+    DevBuf<uint32_t> scheme;
+    uint32_t nsearch = 0;
+    uint32_t maxErr = 0;
+    bool edit = true;
+    bool staged = false;
+
+    // work buffers
+    DevBuf<uint4> stack, hits;
+    DevBuf<uint32_t> small;               // work, hitCount, flags
+    DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest
+    DevBuf<uint64_t> rowOff, k0, k1;
+    DevBuf<char> tmp;
+    DevBuf<sahara_hit> out;
+    uint64_t nout = 0;
+    uint32_t hitCap = 0;
+    sahara_stats stats{};
+    hipEvent_t ev[6] = {};
+
+    ~Ctx() {
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+    } catch (...) {
+        g_err = "unknown error";
+    }
+    return -1;
+}
+
+Ctx* newCtx(int device) {
+    int n = 0;
+    SH_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n)
+        throw Error("no HIP device " + std::to_string(device) + " (found " + std::to_string(n) + ")");
+    SH_HIP(hipSetDevice(device));
+    auto c = std::make_unique<Ctx>();
+    c->device = device;
+    hipDeviceProp_t prop;
+    SH_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
+    c->numCU = prop.multiProcessorCount;
+    SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
+    c->small.reserve(4);
+    c->counters.reserve(8);
+    return c.release();
+}
+
+Ctx* ctxOf(void* p) {
+    if (!p) throw Error("null context");
+    Ctx* c = static_cast<Ctx*>(p);
+    SH_HIP(hipSetDevice(c->device));
+    return c;
+}
+
+void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
+                std::vector<uint32_t>& out, uint32_t& maxErr) {
+    if (ns == 0) throw Error("empty search scheme");
+    if (m == 0 || m > kMaxPatternLen) throw Error("pattern length out of range");
+    out.resize((size_t)ns * m);
+    maxErr = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+        const uint32_t* P = pi + (size_t)s * m;
+        uint32_t lo = P[0], hi = P[0];
+        if (P[0] >= m) throw Error("scheme pi out of range");
+        for (uint32_t p = 0; p < m; ++p) {
+            const uint32_t L = l[(size_t)s * m + p], U = u[(size_t)s * m + p];
+            if (L > U || U > kMaxErrors) throw Error("scheme bounds must satisfy l <= u <= 15");
+            if (p > 0) {
+                if (P[p] == hi + 1) hi = P[p];
+                else if (lo > 0 && P[p] == lo - 1) lo = P[p];
+                else throw Error("scheme pi is not a connected order (search.cpp:191 expand)");
+            }
+            maxErr = std::max(maxErr, U);
+        }
+        for (uint32_t p = 0; p < m; ++p) {
+            uint32_t right;
+            if (p > 0) right = P[p] > P[p - 1];
+            else right = m > 1 ? (P[1] > P[0]) : 1u;
+            out[(size_t)s * m + p] = packScheme(P[p], l[(size_t)s * m + p], u[(size_t)s * m + p], right);
+        }
+    }
+}
+
+void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l,
+           const uint32_t* u, uint32_t ns, int edit) {
+    if (npat == 0) throw Error("no patterns");
+    std::vector<uint32_t> packed;
+    packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);
+    if ((size_t)ns * m * 4 > 60 * 1024) throw Error("scheme too large for LDS (searches * len > 15360)");
+    for (uint64_t i = 0; i < npat * m; ++i)
+        if (ranks[i] == 0 || ranks[i] >= c->I.sigma) throw Error("pattern rank out of range for this index");
+    c->pats.reserve(npat * m);
+    SH_HIP(hipMemcpyAsync(c->pats.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
+    c->scheme.reserve(packed.size());
+    SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
+    SH_HIP(hipStreamSynchronize(c->st));
+    c->npat = npat;
+    c->m = m;
+    c->nsearch = ns;
+    c->edit = edit != 0;
+    c->staged = true;
+}
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    SH_HIP(hipEventElapsedTime(&ms, a, b));
+    return ms;
+}
+
+void run(Ctx* c, bool count) {
+    if (!c->staged) throw Error("sahara_gpu_run: nothing staged");
+    auto t0 = std::chrono::steady_clock::now();
+    sahara_stats S{};
+    S.patterns = c->npat;
+    const uint32_t sigma = c->I.sigma;
+    const size_t lds = (size_t)c->nsearch * c->m * 4;
+    const int bpc = searchBlocksPerCU(sigma, c->edit, lds);
+    const uint32_t blocks = (uint32_t)(c->numCU * bpc);
+    const uint64_t T = (uint64_t)blocks * 256;
+    const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
+    c->stack.reserve(stackCap * T);
+    S.search_grid = blocks;
+
+    const uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
+    if (c->hitCap == 0) {
+        c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (const char* e = std::getenv("SAHARA_HITCAP")) c->hitCap = (uint32_t)std::max(1L, std::atol(e));
+    }
+    c->hits.reserve((size_t)c->hitCap + 1);
+    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 8 * sizeof(unsigned long long), c->st));
+    c->nout = 0;
+
+    for (uint64_t q0 = 0; q0 < c->npat; q0 += maxBatch) {
+        const uint64_t nb = std::min<uint64_t>(maxBatch, c->npat - q0);
+        ++S.batches;
+        uint32_t hostSmall[3];
+        for (;;) {
+            SH_HIP(hipMemsetAsync(c->small.ptr, 0, 4 * sizeof(uint32_t), c->st));
+            SearchArgs a{};
+            a.occF = c->I.occF.ptr;
+            a.occR = c->I.occR.ptr;
+            for (int i = 0; i < 8; ++i) a.C[i] = (uint32_t)c->I.C[i];
+            a.n = (uint32_t)c->I.n;
+            a.pats = c->pats.ptr + q0 * c->m;
+            a.m = c->m;
+            a.nsearch = c->nsearch;
+            a.nitems = (uint32_t)(nb * c->nsearch);
+            a.scheme = c->scheme.ptr;
+            a.work = c->small.ptr;
+            a.hitCount = c->small.ptr + 1;
+            a.flags = c->small.ptr + 2;
+            a.stack = c->stack.ptr;
+            a.stackCap = stackCap;
+            a.hits = c->hits.ptr;
+            a.hitCap = c->hitCap;
+            a.counters = c->counters.ptr;
+            SH_HIP(hipEventRecord(c->ev[0], c->st));
+            launchSearch(a, sigma, c->edit, count, blocks, lds, c->st);
+            SH_HIP(hipEventRecord(c->ev[1], c->st));
+            SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+            SH_HIP(hipStreamSynchronize(c->st));
+            S.search_ms += elapsed(c->ev[0], c->ev[1]);
+            ++S.search_launches;
+            if (hostSmall[2] & 1u) throw Error("search stack overflow (internal bound violated)");
+            if ((hostSmall[2] & 2u) || hostSmall[1] > c->hitCap) {
+                // hit buffer too small for this batch: grow and re-run it
+                const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
+                if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
+                c->hitCap = (uint32_t)want;
+                c->hits.reserve((size_t)c->hitCap + 1);
+                continue;
+            }
+            break;
+        }
+        const uint64_t nh = hostSmall[1];
+        S.cursors += nh;
+
+        // locate: row offsets (exclusive scan of len), LF walks, canonical sort, decode
+        SH_HIP(hipEventRecord(c->ev[2], c->st));
+        SH_HIP(hipMemsetAsync(c->hits.ptr + nh, 0, sizeof(uint4), c->st));
+        c->rowOff.reserve(nh + 1);
+        const size_t scanBytes = rowOffsetsTempBytes(nh);
+        c->tmp.reserve(scanBytes + 256);
+        rowOffsets(c->hits.ptr, nh, c->rowOff.ptr, c->tmp.ptr, c->tmp.cap, c->st);
+        uint64_t rows = 0;
+        SH_HIP(hipMemcpyAsync(&rows, c->rowOff.ptr + nh, 8, hipMemcpyDeviceToHost, c->st));
+        SH_HIP(hipStreamSynchronize(c->st));
+        c->k0.reserve(std::max<uint64_t>(rows, 1));
+        c->k1.reserve(std::max<uint64_t>(rows, 1));
+        LocateArgs la{};
+        la.hits = c->hits.ptr;
+        la.nhits = nh;
+        la.rowOff = c->rowOff.ptr;
+        la.occF = c->I.occF.ptr;
+        for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
+        la.samples = c->I.samples.ptr;
+        la.rate = c->I.rate;
+        la.keys = c->k0.ptr;
+        la.flags = c->small.ptr + 2;
+        la.counters = c->counters.ptr + 3;
+        launchLocate(la, count, c->st);
+        SH_HIP(hipEventRecord(c->ev[3], c->st));
+        unsigned endBit = 36;
+        while ((1ull << (endBit - 36)) < nb) ++endBit;
+        const size_t sb = sortTempBytes(rows);
+        c->tmp.reserve(sb + 256);
+        uint64_t* sorted = sortKeys(c->k0.ptr, c->k1.ptr, rows, std::min(endBit, 64u), c->tmp.ptr, c->tmp.cap, c->st);
+        // grow the output (device-resident) and decode
+        if (c->nout + rows > c->out.cap) {
+            const size_t want = std::max<size_t>((c->nout + rows) + (c->nout + rows) / 2, 1024);
+            sahara_hit* np = nullptr;
+            SH_HIP(hipMalloc(&np, want * sizeof(sahara_hit)));
+            if (c->nout)
+                SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, c->st));
+            SH_HIP(hipStreamSynchronize(c->st));
+            c->out.release();
+            c->out.ptr = np;
+            c->out.cap = want;
+        }
+        launchDecode(sorted, rows, q0, c->I.dRecStarts.ptr, (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout,
+                     c->st);
+        SH_HIP(hipEventRecord(c->ev[4], c->st));
+        SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+        SH_HIP(hipStreamSynchronize(c->st));
+        if (hostSmall[2] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
+        S.locate_ms += elapsed(c->ev[2], c->ev[3]);
+        S.sort_ms += elapsed(c->ev[3], c->ev[4]);
+        c->nout += rows;
+        S.hits += rows;
+    }
+    if (count) {
+        unsigned long long h[4];
+        SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, c->st));
+        SH_HIP(hipStreamSynchronize(c->st));
+        S.nodes = h[0];
+        S.rank_nodes = h[1];
+        S.ext_lines = h[2];
+        S.lf_steps = h[3];
+    }
+    S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->stats = S;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sahara_gpu_last_error(void) { return g_err.c_str(); }
+
+int sahara_gpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int sahara_gpu_build(int device, const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
+                     uint32_t sampling_rate, void** ctx) {
+    return guarded([&] {
+        std::unique_ptr<Ctx> c(newCtx(device));
+        buildFromText(c->I, ranks, rec_lens, n_records, sigma, sampling_rate, true, c->st);
+        *ctx = c.release();
+    });
+}
+
+int sahara_gpu_open(int device, const void* idx_image, size_t idx_bytes, void** ctx) {
+    return guarded([&] {
+        IdxParts P = parseIdx(static_cast<const uint8_t*>(idx_image), idx_bytes);
+        std::unique_ptr<Ctx> c(newCtx(device));
+        buildFromParts(c->I, P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF, P.bwtR, P.sampled,
+                       P.samples, P.nsamples, c->st);
+        *ctx = c.release();
+    });
+}
+
+int sahara_gpu_open_file(int device, const char* path, void** ctx) {
+    return guarded([&] {
+        std::vector<uint8_t> buf = readFile(path);
+        IdxParts P = parseIdx(buf.data(), buf.size());
+        std::unique_ptr<Ctx> c(newCtx(device));
+        buildFromParts(c->I, P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF, P.bwtR, P.sampled,
+                       P.samples, P.nsamples, c->st);
+        *ctx = c.release();
+    });
+}
+
+int sahara_gpu_index_info(void* ctx, sahara_index_info* info) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        info->sigma = c->I.sigma;
+        info->sampling_rate = c->I.rate;
+        info->n = c->I.n;
+        info->n_records = c->I.recLens.size();
+        info->n_samples = c->I.nsamples;
+        info->device_bytes = c->I.deviceBytes();
+    });
+}
+
+int sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* sampled_bits, uint32_t* samples,
+                      uint64_t* C, uint64_t* rec_lens) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        exportParts(c->I, bwt_f, bwt_r, sampled_bits, samples, c->st);
+        if (C) std::memcpy(C, c->I.C, (c->I.sigma + 1) * 8);
+        if (rec_lens) std::memcpy(rec_lens, c->I.recLens.data(), c->I.recLens.size() * 8);
+    });
+}
+
+int sahara_gpu_export_sa(void* ctx, uint32_t* sa) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (!c->I.sa.ptr) throw Error("suffix array not kept (only available after sahara_gpu_build)");
+        SH_HIP(hipMemcpy(sa, c->I.sa.ptr, c->I.n * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+int sahara_gpu_save(void* ctx, const char* path) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        const uint64_t n = c->I.n;
+        std::vector<uint8_t> bf(n), br(n);
+        std::vector<uint64_t> sb(n / 64 + 1);
+        std::vector<uint32_t> smp(c->I.nsamples);
+        exportParts(c->I, bf.data(), br.data(), sb.data(), smp.data(), c->st);
+        IdxParts P;
+        P.sigma = c->I.sigma;
+        P.n = n;
+        P.rate = c->I.rate;
+        std::copy(c->I.C, c->I.C + 8, P.C);
+        P.recLens = c->I.recLens;
+        P.bwtF = bf.data();
+        P.bwtR = br.data();
+        P.sampled = sb.data();
+        P.samples = smp.data();
+        P.nsamples = smp.size();
+        writeIdx(path, P);
+    });
+}
+
+int sahara_gpu_stage(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,
+                     const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit) {
+    return guarded([&] { stage(ctxOf(ctx), ranks, n_patterns, len, pi, l, u, n_searches, edit); });
+}
+
+int sahara_gpu_run(void* ctx, int count, uint64_t* n_hits) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        run(c, count != 0);
+        if (n_hits) *n_hits = c->nout;
+    });
+}
+
+int sahara_gpu_fetch(void* ctx, sahara_hit* out, uint64_t capacity, uint64_t* n_hits) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (n_hits) *n_hits = c->nout;
+        if (capacity < c->nout) throw Error("sahara_gpu_fetch: capacity too small");
+        if (c->nout) SH_HIP(hipMemcpy(out, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
+    });
+}
+
+int sahara_gpu_digest(void* ctx, uint64_t* digest) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 4, 0, 8, c->st));
+        launchDigest(c->out.ptr, c->nout, c->counters.ptr + 4, c->st);
+        unsigned long long d = 0;
+        SH_HIP(hipMemcpyAsync(&d, c->counters.ptr + 4, 8, hipMemcpyDeviceToHost, c->st));
+        SH_HIP(hipStreamSynchronize(c->st));
+        *digest = d;
+    });
+}
+
+int sahara_gpu_stats(void* ctx, sahara_stats* stats) {
+    return guarded([&] { *stats = ctxOf(ctx)->stats; });
+}
+
+int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,
+                      const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit, uint32_t max_hits,
+                      sahara_hit** hits, uint64_t* n_hits) {
+    return guarded([&] {
+        if (max_hits != 0) throw Error("--max_hits (search_n) is not implemented in this build yet");
+        Ctx* c = ctxOf(ctx);
+        stage(c, ranks, n_patterns, len, pi, l, u, n_searches, edit);
+        run(c, false);
+        auto* buf = static_cast<sahara_hit*>(std::malloc(std::max<uint64_t>(c->nout, 1) * sizeof(sahara_hit)));
+        if (!buf) throw Error("out of host memory for hits");
+        if (c->nout) SH_HIP(hipMemcpy(buf, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
+        *hits = buf;
+        *n_hits = c->nout;
+    });
+}
+
+void sahara_gpu_free(void* p) { std::free(p); }
+
+void sahara_gpu_close(void* ctx) {
+    if (!ctx) return;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    (void)hipSetDevice(c->device);
+    delete c;
+}
+
+// ------------------------------------------------------------ synthetic ----
+
+int sahara_synth_reference(uint64_t seed, uint32_t sigma, const uint64_t* rec_lens, uint64_t n_records,
+                           uint8_t* out) {
+    return guarded([&] {
+        if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 or 6");
+        const uint8_t code[4] = {1, 2, 3, (uint8_t)(sigma == 6 ? 5 : 4)};
+        uint64_t total = 0;
+        for (uint64_t r = 0; r < n_records; ++r) total += rec_lens[r];
+        std::mt19937_64 gen(seed);
+        uint64_t i = 0;
+        for (; i + 32 <= total; i += 32) {
+            uint64_t x = gen();
+            for (int j = 0; j < 32; ++j) out[i + j] = code[(x >> (2 * j)) & 3u];
+        }
+        if (i < total) {
+            uint64_t x = gen();
+            for (int j = 0; i < total; ++i, ++j) out[i] = code[(x >> (2 * j)) & 3u];
+        }
+    });
+}
+
+int sahara_synth_reads(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
+                       uint64_t n_reads, uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out,
+                       uint64_t* origin) {
+    return guarded([&] { synthReads(ranks, rec_lens, n_records, sigma, n_reads, len, errors, seed, out, origin); });
+}
+
+int sahara_interleave_rc(const uint8_t* reads, uint64_t n_reads, uint32_t len, uint32_t sigma, uint8_t* out) {
+    return guarded([&] {
+        if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 or 6");
+        uint8_t comp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (sigma == 6) { comp[1] = 5; comp[2] = 3; comp[3] = 2; comp[4] = 4; comp[5] = 1; }
+        else            { comp[1] = 4; comp[2] = 3; comp[3] = 2; comp[4] = 1; }
+        for (uint64_t i = 0; i < n_reads; ++i) {
+            const uint8_t* r = reads + i * len;
+            uint8_t* f = out + (2 * i) * len;
+            uint8_t* b = out + (2 * i + 1) * len;
+            std::memcpy(f, r, len);
+            for (uint32_t j = 0; j < len; ++j) b[j] = comp[r[len - 1 - j] & 7];
+        }
+    });
+}
+
+}  // extern "C"

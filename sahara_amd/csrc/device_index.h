@@ -1,0 +1,74 @@
+// device_index.h — host-side handle of a GPU-resident bidirectional FM-index.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fm_layout.h"
+
+namespace sahara {
+
+struct Error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define SH_HIP(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            throw ::sahara::Error(std::string("HIP error '") + hipGetErrorString(_e) +       \
+                                  "' at " __FILE__ ":" + std::to_string(__LINE__) + ": " #expr); \
+    } while (0)
+
+template <typename T>
+struct DevBuf {  // minimal owning device buffer that only ever grows
+    T* ptr = nullptr;
+    size_t cap = 0;
+    void reserve(size_t n) {
+        if (n <= cap) return;
+        release();
+        if (n) SH_HIP(hipMalloc(&ptr, n * sizeof(T)));
+        cap = n;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+    ~DevBuf() { release(); }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+};
+
+struct DeviceIndex {
+    int device = 0;
+    uint32_t sigma = 6;
+    uint32_t rate = 16;
+    uint64_t n = 0;                 // text length incl. delimiters
+    std::vector<uint64_t> recLens;
+    std::vector<uint64_t> recStarts;
+    uint64_t C[8] = {0};
+    DevBuf<OccLine> occF, occR;     // n/64 + 1 lines each
+    DevBuf<uint32_t> samples;       // text position per sampled row, row order
+    uint64_t nsamples = 0;
+    DevBuf<uint64_t> dRecStarts;
+    DevBuf<uint32_t> sa;            // kept only when requested (test export)
+    uint64_t deviceBytes() const {
+        return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8;
+    }
+};
+
+// index_build.hip
+void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec,
+                   uint32_t sigma, uint32_t rate, bool keepSA, hipStream_t st);
+void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec,
+                    uint32_t rate, const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits,
+                    const uint32_t* samples, uint64_t nsamples, hipStream_t st);
+void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits,
+                 uint32_t* samples, hipStream_t st);
+
+}  // namespace sahara

@@ -1,0 +1,194 @@
+// host_util.cpp — .idx I/O and the synthetic read generator (host side).
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <thread>
+
+#include "device_index.h"
+#include "idx_format.h"
+
+namespace sahara {
+
+std::vector<uint8_t> readFile(const std::string& path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) throw Error("no valid index path at " + path);
+    const std::streamsize sz = f.tellg();
+    f.seekg(0);
+    std::vector<uint8_t> buf((size_t)sz);
+    if (sz && !f.read(reinterpret_cast<char*>(buf.data()), sz)) throw Error("cannot read " + path);
+    return buf;
+}
+
+namespace {
+struct Reader {
+    const uint8_t* p;
+    const uint8_t* end;
+    template <typename T> T get() {
+        if ((size_t)(end - p) < sizeof(T)) throw Error("truncated .idx file");
+        T v;
+        std::memcpy(&v, p, sizeof(T));
+        p += sizeof(T);
+        return v;
+    }
+    template <typename T> const T* vec(uint64_t& n) {
+        n = get<uint64_t>();
+        if (n > (uint64_t)(end - p) / sizeof(T)) throw Error("truncated .idx file");
+        const T* r = reinterpret_cast<const T*>(p);
+        p += n * sizeof(T);
+        return r;
+    }
+};
+}  // namespace
+
+IdxParts parseIdx(const uint8_t* buf, size_t bytes) {
+    Reader r{buf, buf + bytes};
+    IdxParts P;
+    const uint64_t sigma = r.get<uint64_t>();
+    if (sigma != 5 && sigma != 6) throw Error("unknown index with " + std::to_string(sigma) + " letters");
+    if (r.get<uint64_t>() != kIdxMagic) throw Error("not a sahara-amd .idx file (payload magic mismatch)");
+    P.sigma = (uint32_t)sigma;
+    P.n = r.get<uint64_t>();
+    for (uint64_t c = 0; c <= sigma; ++c) P.C[c] = r.get<uint64_t>();
+    uint64_t nrec = 0, nf = 0, nr = 0, ns = 0;
+    const uint64_t* rl = r.vec<uint64_t>(nrec);
+    P.recLens.assign(rl, rl + nrec);
+    P.rate = (uint32_t)r.get<uint64_t>();
+    P.bwtF = r.vec<uint8_t>(nf);
+    P.bwtR = r.vec<uint8_t>(nr);
+    // the u64/u32 vectors are 8/4-aligned only if the preceding byte vectors
+    // keep alignment; copy-free access requires it, so check
+    P.sampled = r.vec<uint64_t>(ns);
+    P.samples = r.vec<uint32_t>(P.nsamples);
+    if (nf != P.n || nr != P.n || ns != P.n / 64 + 1) throw Error("inconsistent .idx payload sizes");
+    uint64_t tot = 0;
+    for (uint64_t x : P.recLens) tot += x + 1;
+    if (tot != P.n) throw Error("record lengths do not match index size");
+    return P;
+}
+
+void writeIdx(const std::string& path, const IdxParts& P) {
+    std::ofstream o(path, std::ios::binary);
+    if (!o) throw Error("cannot write " + path);
+    auto put = [&](uint64_t v) { o.write(reinterpret_cast<const char*>(&v), 8); };
+    put(P.sigma);
+    put(kIdxMagic);
+    put(P.n);
+    for (uint32_t c = 0; c <= P.sigma; ++c) put(P.C[c]);
+    put(P.recLens.size());
+    o.write(reinterpret_cast<const char*>(P.recLens.data()), (std::streamsize)(P.recLens.size() * 8));
+    put(P.rate);
+    put(P.n);
+    o.write(reinterpret_cast<const char*>(P.bwtF), (std::streamsize)P.n);
+    put(P.n);
+    o.write(reinterpret_cast<const char*>(P.bwtR), (std::streamsize)P.n);
+    put(P.n / 64 + 1);
+    o.write(reinterpret_cast<const char*>(P.sampled), (std::streamsize)((P.n / 64 + 1) * 8));
+    put(P.nsamples);
+    o.write(reinterpret_cast<const char*>(P.samples), (std::streamsize)(P.nsamples * 4));
+    if (!o) throw Error("write failed: " + path);
+}
+
+uint64_t readIdxSigma(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw Error("no valid index path at " + path);
+    uint64_t s = 0;
+    f.read(reinterpret_cast<char*>(&s), 8);
+    if (!f) throw Error("cannot read " + path);
+    return s;
+}
+
+// --------------------------------------------------------------- reads ----
+// read_simulator.cpp:119-240 restated with a counter-based generator so reads
+// can be produced in parallel and still depend only on (seed, read index):
+//   per error, the type is S/I/D with probability 1/3 each (:258-267);
+//   S turns a random 'M' of the transcript into 'S' (:129-136), I turns a
+//   random 'M' into 'I' (:138-145), D inserts a 'D' at a random slot (:147-150);
+//   the reference span (len - #I + #D) is sampled uniformly inside one record;
+//   S writes one of the three other bases, I a random base, D skips a
+//   reference base (:204-240). Reads therefore always have exactly `len` bases.
+namespace {
+struct Xoshiro {
+    uint64_t s[4];
+    static uint64_t splitmix(uint64_t& x) {
+        uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        return z ^ (z >> 31);
+    }
+    explicit Xoshiro(uint64_t seed) {
+        for (auto& v : s) v = splitmix(seed);
+    }
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t operator()() {
+        const uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+        s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3]; s[2] ^= t; s[3] = rotl(s[3], 45);
+        return r;
+    }
+    uint64_t below(uint64_t n) { return n ? (*this)() % n : 0; }
+};
+}  // namespace
+
+void synthReads(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma, uint64_t nreads,
+                uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out, uint64_t* origin) {
+    if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 or 6");
+    if (len == 0) throw Error("read length must be > 0");
+    const uint8_t code[4] = {1, 2, 3, (uint8_t)(sigma == 6 ? 5 : 4)};
+    auto toIdx = [&](uint8_t r) -> int { return r == 1 ? 0 : r == 2 ? 1 : r == 3 ? 2 : 3; };
+    std::vector<uint64_t> starts(nrec + 1, 0);
+    for (uint64_t r = 0; r < nrec; ++r) starts[r + 1] = starts[r] + recLens[r];
+    const uint64_t total = starts[nrec];
+    if (total == 0) throw Error("empty reference");
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    std::vector<std::string> errs(nth);
+    for (unsigned t = 0; t < nth; ++t) {
+        th.emplace_back([&, t] {
+            std::vector<char> tr;
+            for (uint64_t i = nreads * t / nth; i < nreads * (t + 1) / nth; ++i) {
+                Xoshiro g(seed * 0x100000001b3ull + i);
+                uint32_t ns = 0, ni = 0, nd = 0;
+                for (uint32_t e = 0; e < errors; ++e) {
+                    const uint64_t k = g.below(3);
+                    ns += k == 0; ni += k == 1; nd += k == 2;
+                }
+                if (ns + ni > len) { errs[t] = "more substitutions+insertions than read length"; return; }
+                tr.assign(len, 'M');
+                auto pickM = [&](char to) {
+                    for (;;) {
+                        const uint64_t p = g.below(tr.size());
+                        if (tr[p] == 'M') { tr[p] = to; return; }
+                    }
+                };
+                for (uint32_t k = 0; k < ns; ++k) pickM('S');
+                for (uint32_t k = 0; k < ni; ++k) pickM('I');
+                for (uint32_t k = 0; k < nd; ++k) tr.insert(tr.begin() + (long)g.below(tr.size() + 1), 'D');
+                const uint64_t span = (uint64_t)len - ni + nd;
+                uint64_t rec = 0, pos = 0;
+                for (int tries = 0;; ++tries) {
+                    if (tries > 1000000) { errs[t] = "no record long enough for the reads"; return; }
+                    const uint64_t gp = g.below(total);
+                    rec = (uint64_t)(std::upper_bound(starts.begin(), starts.end(), gp) - starts.begin()) - 1;
+                    pos = gp - starts[rec];
+                    if (pos + span <= recLens[rec]) break;
+                }
+                const uint8_t* ref = ranks + starts[rec] + pos;
+                uint8_t* o = out + i * len;
+                uint64_t p = 0, w = 0;
+                for (char c : tr) {
+                    switch (c) {
+                        case 'M': o[w++] = ref[p++]; break;
+                        case 'S': o[w++] = code[(toIdx(ref[p++]) + 1 + (int)g.below(3)) % 4]; break;
+                        case 'I': o[w++] = code[g.below(4)]; break;
+                        default: ++p; break;  // 'D'
+                    }
+                }
+                if (origin) { origin[2 * i] = rec; origin[2 * i + 1] = pos; }
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    for (auto& e : errs)
+        if (!e.empty()) throw Error(e);
+}
+
+}  // namespace sahara

@@ -1,0 +1,443 @@
+// index_build.hip — GPU construction of the bidirectional FM-index (gfx950).
+//
+// Restates `sahara index` (/root/reference/src/sahara/index.cpp:41-112): the
+// records are concatenated with one '$' (rank 0) after each, a suffix array
+// is built for the text and for the per-record reversed text, and from it the
+// two BWTs, the C array and the SA samples (samplingRate 16, index.cpp:87).
+// Upstream does this on one CPU thread with libsais (fmindex-collection
+// v1.1.0, absent here); this build uses GPU prefix doubling instead:
+//   round 0: sort suffixes by their first 21 symbols packed 3 bits each,
+//   round r: sort by (rank of the 2^r*21-prefix at i, rank at i + 2^r*21),
+// with rocPRIM's onesweep radix sort (u64 keys, u32 suffix ids), until every
+// rank group is a singleton. Random text finishes after 2 sorts at 3 Gbp.
+// Sampling: row i is sampled iff the position of
+// SA[i] inside its record is a multiple of the rate, so every record start
+// is sampled and LF walks never cross a delimiter.
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include <algorithm>
+#include <rocprim/rocprim.hpp>
+
+#include "device_index.h"
+
+namespace sahara {
+namespace {
+
+constexpr int kTB = 256;
+
+inline unsigned gridFor(uint64_t n, unsigned cap = 65535u * 4u) {
+    uint64_t g = (n + kTB - 1) / kTB;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, cap));
+}
+
+__device__ inline uint32_t recordOf(const uint64_t* starts, uint32_t nrec, uint64_t p) {
+    uint32_t lo = 0, hi = nrec;  // last start <= p
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (starts[mid] <= p) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void kInitKeys(const uint8_t* __restrict__ T, uint64_t N, uint64_t* __restrict__ keys,
+                          uint32_t* __restrict__ vals) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t k = 0;
+#pragma unroll
+        for (int j = 0; j < 21; ++j) {
+            const uint64_t p = i + j;
+            const uint64_t c = p < N ? (uint64_t)T[p] + 1u : 0u;
+            k = (k << 3) | c;
+        }
+        keys[i] = k;
+        vals[i] = (uint32_t)i;
+    }
+}
+
+// g[i] = i at the head of a group of equal keys, 0 otherwise; counts heads.
+__global__ void kHeads(const uint64_t* __restrict__ keys, uint64_t N, uint32_t* __restrict__ g,
+                       unsigned long long* __restrict__ nheads) {
+    uint32_t local = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const bool head = (i == 0) || keys[i] != keys[i - 1];
+        g[i] = head ? (uint32_t)i : 0u;
+        local += head;
+    }
+    // wave reduction then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(nheads, (unsigned long long)local);
+}
+
+__global__ void kScatterRank(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ g, uint64_t N,
+                             uint32_t* __restrict__ isa) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        isa[vals[i]] = g[i];
+}
+
+__global__ void kPairKeys(const uint32_t* __restrict__ isa, uint64_t N, uint64_t h, uint64_t* __restrict__ keys,
+                          uint32_t* __restrict__ vals) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t hi = isa[i];
+        const uint64_t lo = (i + h < N) ? (uint64_t)isa[i + h] + 1u : 0u;
+        keys[i] = (hi << 32) | lo;
+        vals[i] = (uint32_t)i;
+    }
+}
+
+__global__ void kReverseRecords(const uint8_t* __restrict__ T, uint64_t N, const uint64_t* __restrict__ starts,
+                                const uint64_t* __restrict__ lens, uint32_t nrec, uint8_t* __restrict__ R) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = recordOf(starts, nrec, i);
+        const uint64_t off = i - starts[r];
+        R[i] = off < lens[r] ? T[starts[r] + lens[r] - 1 - off] : (uint8_t)0;
+    }
+}
+
+__global__ void kBwt(const uint8_t* __restrict__ T, const uint32_t* __restrict__ sa, uint64_t N,
+                     uint8_t* __restrict__ bwt) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = sa[i];
+        bwt[i] = T[p ? p - 1 : N - 1];
+    }
+}
+
+// One thread per 64-row block: sampled-row word.
+__global__ void kSampledBits(const uint32_t* __restrict__ sa, uint64_t N, const uint64_t* __restrict__ starts,
+                             uint32_t nrec, uint32_t rate, uint64_t* __restrict__ bits) {
+    const uint64_t nb = N / 64 + 1;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nb;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t w = 0;
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint64_t i = b * 64 + j;
+            if (i >= N) break;
+            const uint64_t p = sa[i];
+            const uint32_t r = recordOf(starts, nrec, p);
+            if ((p - starts[r]) % rate == 0) w |= 1ull << j;
+        }
+        bits[b] = w;
+    }
+}
+
+struct Cnt6 {
+    uint32_t c[6];  // symbols 1..5, then sampled rows
+};
+struct Cnt6Plus {
+    __host__ __device__ Cnt6 operator()(const Cnt6& a, const Cnt6& b) const {
+        Cnt6 r;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) r.c[i] = a.c[i] + b.c[i];
+        return r;
+    }
+};
+
+// One thread per 64-position block: local symbol counts + bit planes.
+__global__ void kLinesLocal(const uint8_t* __restrict__ bwt, uint64_t N, const uint64_t* __restrict__ sampled,
+                            OccLine* __restrict__ lines, Cnt6* __restrict__ counts) {
+    const uint64_t nb = N / 64 + 1;
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nb;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t p0 = 0, p1 = 0, p2 = 0;
+        Cnt6 c = {{0, 0, 0, 0, 0, 0}};
+        const uint64_t base = b * 64;
+        if (base + 64 <= N) {
+            const uint4* src = reinterpret_cast<const uint4*>(bwt + base);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint4 q = src[v];
+                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const uint32_t s = (w[t >> 2] >> ((t & 3) * 8)) & 0xffu;
+                    const int j = v * 16 + t;
+                    p0 |= (uint64_t)(s & 1u) << j;
+                    p1 |= (uint64_t)((s >> 1) & 1u) << j;
+                    p2 |= (uint64_t)((s >> 2) & 1u) << j;
+                }
+            }
+        } else {
+            for (uint64_t j = 0; j < 64 && base + j < N; ++j) {
+                const uint32_t s = bwt[base + j];
+                p0 |= (uint64_t)(s & 1u) << j;
+                p1 |= (uint64_t)((s >> 1) & 1u) << j;
+                p2 |= (uint64_t)((s >> 2) & 1u) << j;
+            }
+        }
+        const uint64_t valid = (base + 64 <= N) ? ~0ull : lowMask((uint32_t)(N - base));
+        const uint64_t pl[3] = {p0, p1, p2};
+#pragma unroll
+        for (uint32_t s = 1; s <= 5; ++s) c.c[s - 1] = (uint32_t)__popcll(symMask(pl, s) & valid);
+        const uint64_t sw = sampled ? sampled[b] : 0ull;
+        c.c[5] = (uint32_t)__popcll(sw);
+        OccLine L;
+        L.plane[0] = p0;
+        L.plane[1] = p1;
+        L.plane[2] = p2;
+        L.sampled = sw;
+        L.reserved = 0;
+        lines[b] = L;  // counts filled after the scan
+        counts[b] = c;
+    }
+}
+
+__global__ void kLinesCounts(OccLine* __restrict__ lines, const Cnt6* __restrict__ scanned, uint64_t nb) {
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nb;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const Cnt6 c = scanned[b];
+#pragma unroll
+        for (int s = 0; s < 5; ++s) lines[b].cnt[s] = c.c[s];
+        lines[b].srank = c.c[5];
+    }
+}
+
+__global__ void kSamples(const uint32_t* __restrict__ sa, uint64_t N, const OccLine* __restrict__ lines,
+                         uint32_t* __restrict__ samples) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const OccLine& L = lines[i >> 6];
+        const uint32_t o = (uint32_t)(i & 63);
+        if ((L.sampled >> o) & 1ull) samples[L.srank + __popcll(L.sampled & lowMask(o))] = sa[i];
+    }
+}
+
+__global__ void kDecodeBwt(const OccLine* __restrict__ lines, uint64_t N, uint8_t* __restrict__ bwt) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        bwt[i] = (uint8_t)symAt(lines[i >> 6].plane, (uint32_t)(i & 63));
+}
+
+__global__ void kSampledWords(const OccLine* __restrict__ lines, uint64_t nb, uint64_t* __restrict__ w) {
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nb;
+         b += (uint64_t)gridDim.x * blockDim.x)
+        w[b] = lines[b].sampled;
+}
+
+// Builds the suffix array of the device text T[0, N) into `sa`.
+void suffixArray(const uint8_t* dT, uint64_t N, uint32_t* dSA, hipStream_t st) {
+    DevBuf<uint64_t> k0, k1;
+    DevBuf<uint32_t> v1, g, isa;
+    k0.reserve(N);
+    k1.reserve(N);
+    v1.reserve(N);
+    g.reserve(N);
+    isa.reserve(N);
+    DevBuf<unsigned long long> cnt;
+    cnt.reserve(1);
+    DevBuf<char> tmp;
+    const unsigned grid = gridFor(N);
+
+    hipLaunchKernelGGL(kInitKeys, dim3(grid), dim3(kTB), 0, st, dT, N, k0.ptr, dSA);
+    SH_HIP(hipGetLastError());
+    rocprim::double_buffer<uint64_t> kb(k0.ptr, k1.ptr);
+    rocprim::double_buffer<uint32_t> vb(dSA, v1.ptr);
+    size_t tmpBytes = 0;
+    SH_HIP(rocprim::radix_sort_pairs(nullptr, tmpBytes, kb, vb, (size_t)N, 0, 64, st));
+    size_t scanBytes = 0;
+    SH_HIP(rocprim::inclusive_scan(nullptr, scanBytes, g.ptr, g.ptr, (size_t)N, rocprim::maximum<uint32_t>(), st));
+    tmp.reserve(std::max(tmpBytes, scanBytes) + 256);
+    size_t tb = tmp.cap;
+    SH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, kb, vb, (size_t)N, 0, 63, st));
+
+    uint64_t h = 21;
+    for (int round = 0;; ++round) {
+        SH_HIP(hipMemsetAsync(cnt.ptr, 0, sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(kHeads, dim3(grid), dim3(kTB), 0, st, kb.current(), N, g.ptr, cnt.ptr);
+        SH_HIP(hipGetLastError());
+        unsigned long long heads = 0;
+        SH_HIP(hipMemcpyAsync(&heads, cnt.ptr, sizeof(heads), hipMemcpyDeviceToHost, st));
+        SH_HIP(hipStreamSynchronize(st));
+        if (heads == N) break;
+        if (round > 40) throw Error("suffix array construction did not converge");
+        tb = tmp.cap;
+        SH_HIP(rocprim::inclusive_scan(tmp.ptr, tb, g.ptr, g.ptr, (size_t)N, rocprim::maximum<uint32_t>(), st));
+        hipLaunchKernelGGL(kScatterRank, dim3(grid), dim3(kTB), 0, st, vb.current(), g.ptr, N, isa.ptr);
+        hipLaunchKernelGGL(kPairKeys, dim3(grid), dim3(kTB), 0, st, isa.ptr, N, h, kb.current(), vb.current());
+        SH_HIP(hipGetLastError());
+        tb = tmp.cap;
+        SH_HIP(rocprim::radix_sort_pairs(tmp.ptr, tb, kb, vb, (size_t)N, 0, 64, st));
+        h *= 2;
+    }
+    if (vb.current() != dSA)
+        SH_HIP(hipMemcpyAsync(dSA, vb.current(), N * 4, hipMemcpyDeviceToDevice, st));
+    SH_HIP(hipStreamSynchronize(st));
+}
+
+// BWT bytes (+ optional sampled words) -> Occ lines with prefix counts.
+void buildLines(const uint8_t* dBwt, uint64_t N, const uint64_t* dSampled, DevBuf<OccLine>& lines,
+                uint64_t totals[6], hipStream_t st) {
+    const uint64_t nb = N / 64 + 1;
+    lines.reserve(nb);
+    DevBuf<Cnt6> counts;
+    counts.reserve(nb + 1);
+    const unsigned grid = gridFor(nb);
+    hipLaunchKernelGGL(kLinesLocal, dim3(grid), dim3(kTB), 0, st, dBwt, N, dSampled, lines.ptr, counts.ptr);
+    SH_HIP(hipGetLastError());
+    SH_HIP(hipMemsetAsync(counts.ptr + nb, 0, sizeof(Cnt6), st));
+    size_t tb = 0;
+    Cnt6 zero = {{0, 0, 0, 0, 0, 0}};
+    SH_HIP(rocprim::exclusive_scan(nullptr, tb, counts.ptr, counts.ptr, zero, (size_t)nb + 1, Cnt6Plus(), st));
+    DevBuf<char> tmp;
+    tmp.reserve(tb + 256);
+    tb = tmp.cap;
+    SH_HIP(rocprim::exclusive_scan(tmp.ptr, tb, counts.ptr, counts.ptr, zero, (size_t)nb + 1, Cnt6Plus(), st));
+    hipLaunchKernelGGL(kLinesCounts, dim3(grid), dim3(kTB), 0, st, lines.ptr, counts.ptr, nb);
+    SH_HIP(hipGetLastError());
+    Cnt6 tot;
+    SH_HIP(hipMemcpyAsync(&tot, counts.ptr + nb, sizeof(Cnt6), hipMemcpyDeviceToHost, st));
+    SH_HIP(hipStreamSynchronize(st));
+    for (int i = 0; i < 6; ++i) totals[i] = tot.c[i];
+}
+
+void setCommon(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec, uint32_t rate,
+               hipStream_t st) {
+    I.sigma = sigma;
+    I.n = n;
+    I.rate = rate;
+    I.recLens.assign(recLens, recLens + nrec);
+    I.recStarts.resize(nrec);
+    uint64_t s = 0;
+    for (uint64_t r = 0; r < nrec; ++r) { I.recStarts[r] = s; s += recLens[r] + 1; }
+    I.dRecStarts.reserve(nrec);
+    SH_HIP(hipMemcpyAsync(I.dRecStarts.ptr, I.recStarts.data(), nrec * 8, hipMemcpyHostToDevice, st));
+}
+
+void setC(DeviceIndex& I, const uint64_t totals[6], uint64_t nrec) {
+    uint64_t cnt[8] = {0};
+    cnt[0] = nrec;  // one '$' per record
+    for (uint32_t c = 1; c < I.sigma; ++c) cnt[c] = totals[c - 1];
+    I.C[0] = 0;
+    for (uint32_t c = 1; c <= I.sigma; ++c) I.C[c] = I.C[c - 1] + cnt[c - 1];
+}
+
+}  // namespace
+
+void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma,
+                   uint32_t rate, bool keepSA, hipStream_t st) {
+    if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
+    if (nrec == 0) throw Error("reference is empty");
+    if (rate == 0) throw Error("sampling rate must be > 0");
+    uint64_t N = 0;
+    for (uint64_t r = 0; r < nrec; ++r) N += recLens[r] + 1;
+    if (N >= 0xFFFFFFFEull) throw Error("text too long for 32-bit rows (n must be < 2^32 - 2)");
+    for (uint64_t i = 0, tot = N - nrec; i < tot; ++i)
+        if (hostRanks[i] == 0 || hostRanks[i] >= sigma) throw Error("reference rank out of range");
+    setCommon(I, sigma, N, recLens, nrec, rate, st);
+
+    // text with delimiters, on device
+    DevBuf<uint8_t> T, R, bwt;
+    DevBuf<uint64_t> dLens;
+    T.reserve(N + 16);
+    R.reserve(N + 16);
+    dLens.reserve(nrec);
+    SH_HIP(hipMemcpyAsync(dLens.ptr, recLens, nrec * 8, hipMemcpyHostToDevice, st));
+    SH_HIP(hipMemsetAsync(T.ptr, 0, N + 16, st));
+    for (uint64_t r = 0, off = 0; r < nrec; ++r) {
+        SH_HIP(hipMemcpyAsync(T.ptr + I.recStarts[r], hostRanks + off, recLens[r], hipMemcpyHostToDevice, st));
+        off += recLens[r];
+    }
+    const unsigned grid = gridFor(N);
+    hipLaunchKernelGGL(kReverseRecords, dim3(grid), dim3(kTB), 0, st, T.ptr, N, I.dRecStarts.ptr, dLens.ptr,
+                       (uint32_t)nrec, R.ptr);
+    SH_HIP(hipGetLastError());
+
+    DevBuf<uint32_t> sa;
+    sa.reserve(N);
+    DevBuf<uint64_t> sampled;
+    const uint64_t nb = N / 64 + 1;
+    sampled.reserve(nb);
+    bwt.reserve(N + 64);
+    uint64_t totals[6];
+
+    // forward direction: SA, BWT, sampling, lines, samples
+    suffixArray(T.ptr, N, sa.ptr, st);
+    hipLaunchKernelGGL(kBwt, dim3(grid), dim3(kTB), 0, st, T.ptr, sa.ptr, N, bwt.ptr);
+    hipLaunchKernelGGL(kSampledBits, dim3(gridFor(nb)), dim3(kTB), 0, st, sa.ptr, N, I.dRecStarts.ptr,
+                       (uint32_t)nrec, rate, sampled.ptr);
+    SH_HIP(hipGetLastError());
+    buildLines(bwt.ptr, N, sampled.ptr, I.occF, totals, st);
+    setC(I, totals, nrec);
+    I.nsamples = totals[5];
+    I.samples.reserve(std::max<uint64_t>(I.nsamples, 1));
+    hipLaunchKernelGGL(kSamples, dim3(grid), dim3(kTB), 0, st, sa.ptr, N, I.occF.ptr, I.samples.ptr);
+    SH_HIP(hipGetLastError());
+    if (keepSA) {
+        I.sa.reserve(N);
+        SH_HIP(hipMemcpyAsync(I.sa.ptr, sa.ptr, N * 4, hipMemcpyDeviceToDevice, st));
+    }
+
+    // reverse direction: SA, BWT, lines (no sampling)
+    suffixArray(R.ptr, N, sa.ptr, st);
+    hipLaunchKernelGGL(kBwt, dim3(grid), dim3(kTB), 0, st, R.ptr, sa.ptr, N, bwt.ptr);
+    SH_HIP(hipGetLastError());
+    uint64_t totalsR[6];
+    buildLines(bwt.ptr, N, nullptr, I.occR, totalsR, st);
+    for (int c = 0; c < 5; ++c)
+        if (totalsR[c] != totals[c]) throw Error("forward/reverse symbol counts differ");
+    SH_HIP(hipStreamSynchronize(st));
+}
+
+void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec, uint32_t rate,
+                    const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits, const uint32_t* samples,
+                    uint64_t nsamples, hipStream_t st) {
+    if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
+    if (n >= 0xFFFFFFFEull) throw Error("text too long for 32-bit rows");
+    setCommon(I, sigma, n, recLens, nrec, rate, st);
+    const uint64_t nb = n / 64 + 1;
+    DevBuf<uint8_t> bwt;
+    DevBuf<uint64_t> sampled;
+    bwt.reserve(n + 64);
+    sampled.reserve(nb);
+    uint64_t totals[6], totalsR[6];
+    SH_HIP(hipMemcpyAsync(sampled.ptr, sampledBits, nb * 8, hipMemcpyHostToDevice, st));
+    SH_HIP(hipMemcpyAsync(bwt.ptr, bwtF, n, hipMemcpyHostToDevice, st));
+    buildLines(bwt.ptr, n, sampled.ptr, I.occF, totals, st);
+    if (totals[5] != nsamples) throw Error("sampled bitvector and sample count disagree");
+    setC(I, totals, nrec);
+    I.nsamples = nsamples;
+    I.samples.reserve(std::max<uint64_t>(nsamples, 1));
+    SH_HIP(hipMemcpyAsync(I.samples.ptr, samples, nsamples * 4, hipMemcpyHostToDevice, st));
+    SH_HIP(hipMemcpyAsync(bwt.ptr, bwtR, n, hipMemcpyHostToDevice, st));
+    buildLines(bwt.ptr, n, nullptr, I.occR, totalsR, st);
+    for (int c = 0; c < 5; ++c)
+        if (totalsR[c] != totals[c]) throw Error("forward/reverse BWT symbol counts differ");
+    SH_HIP(hipStreamSynchronize(st));
+}
+
+void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits, uint32_t* samples,
+                 hipStream_t st) {
+    const uint64_t N = I.n, nb = N / 64 + 1;
+    DevBuf<uint8_t> bwt;
+    bwt.reserve(N + 64);
+    const unsigned grid = gridFor(N);
+    if (bwtF) {
+        hipLaunchKernelGGL(kDecodeBwt, dim3(grid), dim3(kTB), 0, st, I.occF.ptr, N, bwt.ptr);
+        SH_HIP(hipMemcpyAsync(bwtF, bwt.ptr, N, hipMemcpyDeviceToHost, st));
+        SH_HIP(hipStreamSynchronize(st));
+    }
+    if (bwtR) {
+        hipLaunchKernelGGL(kDecodeBwt, dim3(grid), dim3(kTB), 0, st, I.occR.ptr, N, bwt.ptr);
+        SH_HIP(hipMemcpyAsync(bwtR, bwt.ptr, N, hipMemcpyDeviceToHost, st));
+        SH_HIP(hipStreamSynchronize(st));
+    }
+    if (sampledBits) {
+        DevBuf<uint64_t> w;
+        w.reserve(nb);
+        hipLaunchKernelGGL(kSampledWords, dim3(gridFor(nb)), dim3(kTB), 0, st, I.occF.ptr, nb, w.ptr);
+        SH_HIP(hipMemcpyAsync(sampledBits, w.ptr, nb * 8, hipMemcpyDeviceToHost, st));
+        SH_HIP(hipStreamSynchronize(st));
+    }
+    if (samples && I.nsamples)
+        SH_HIP(hipMemcpyAsync(samples, I.samples.ptr, I.nsamples * 4, hipMemcpyDeviceToHost, st));
+    SH_HIP(hipStreamSynchronize(st));
+}
+
+}  // namespace sahara

@@ -1,0 +1,278 @@
+// scheme.cpp — search-scheme generation for the product (host side).
+//
+// Restates what sahara's `loadSearchScheme` needs from fmindex-collection
+// (/root/reference/src/sahara/search.cpp:174-212, :226):
+//   generator::all[name](minK, maxK, sigma, N)   part-level {pi, l, u}
+//   expand(oss, len)                            per-position bounds
+//   limitToHamming(scheme)                      Hamming tightening
+//   nodeCount / weightedNodeCount               printed by search.cpp:197-198
+// The upstream generator tables are not in the container,
+// so the generators are this build's own, each complete for every error
+// distribution in [minK, maxK] (tests/test_scheme.py checks that, and checks
+// this file against the oracle's independent restatement).
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct Part {
+    std::vector<int> pi, l, u;
+};
+
+// connected orders starting at part `start`
+std::vector<int> connected(int P, int start, bool rightFirst) {
+    std::vector<int> o;
+    o.reserve(P);
+    o.push_back(start);
+    int lo = start, hi = start;
+    while ((int)o.size() < P) {
+        const bool canR = hi + 1 < P, canL = lo > 0;
+        if (canR && (rightFirst || !canL)) o.push_back(++hi);
+        else o.push_back(--lo);
+    }
+    return o;
+}
+
+void distributions(int P, int minK, int maxK, std::vector<std::vector<int>>& out) {
+    std::vector<int> d(P, 0);
+    for (;;) {
+        int s = 0;
+        for (int v : d) s += v;
+        if (s >= minK && s <= maxK) out.push_back(d);
+        int i = P - 1;  // odometer over [0, maxK]^P, pruned by the sum
+        while (i >= 0) {
+            ++d[i];
+            int t = 0;
+            for (int v : d) t += v;
+            if (t <= maxK) break;
+            d[i] = 0;
+            --i;
+        }
+        if (i < 0) break;
+    }
+}
+
+// "h2" family: greedy box construction over connected candidate searches.
+std::vector<Part> boxScheme(int P, int minK, int maxK) {
+    std::vector<std::vector<int>> cand;
+    for (int s = 0; s < P; ++s)
+        for (bool rf : {true, false}) {
+            auto o = connected(P, s, rf);
+            if (std::find(cand.begin(), cand.end(), o) == cand.end()) cand.push_back(o);
+        }
+    std::vector<std::vector<int>> dist;
+    distributions(P, minK, maxK, dist);
+    const int INF = 1 << 20;
+    std::vector<Part> box(cand.size());
+    std::vector<char> used(cand.size(), 0);
+    for (size_t c = 0; c < cand.size(); ++c) {
+        box[c].pi = cand[c];
+        box[c].l.assign(P, INF);
+        box[c].u.assign(P, -1);
+    }
+    for (const auto& d : dist) {
+        int best = -1;
+        long bestCost = 0;
+        for (size_t c = 0; c < cand.size(); ++c) {
+            if (P > maxK && d[cand[c][0]] != 0) continue;  // first part error-free
+            long cost = 0, acc = 0;
+            for (int i = 0; i < P; ++i) cost += (acc += d[cand[c][i]]);
+            if (best < 0 || cost < bestCost) { best = (int)c; bestCost = cost; }
+        }
+        long acc = 0;
+        for (int i = 0; i < P; ++i) {
+            acc += d[cand[best][i]];
+            box[best].l[i] = std::min<int>(box[best].l[i], (int)acc);
+            box[best].u[i] = std::max<int>(box[best].u[i], (int)acc);
+        }
+        used[best] = 1;
+    }
+    std::vector<Part> out;
+    for (size_t c = 0; c < cand.size(); ++c)
+        if (used[c]) out.push_back(box[c]);
+    return out;
+}
+
+bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& out) {
+    if (minK < 0 || maxK < minK || maxK > 15) return false;
+    if (name == "backtracking") {
+        out = {Part{{0}, {minK}, {maxK}}};
+        return true;
+    }
+    if (name == "pigeon") {
+        out.clear();
+        const int P = maxK + 1;
+        for (int s = 0; s < P; ++s) {
+            Part p;
+            p.pi = connected(P, s, true);
+            p.l.assign(P, 0);
+            p.l[P - 1] = minK;
+            p.u.assign(P, maxK);
+            p.u[0] = 0;
+            out.push_back(p);
+        }
+        return true;
+    }
+    if (name.size() == 5 && name.compare(0, 4, "h2-k") == 0 && name[4] >= '1' && name[4] <= '3') {
+        out = boxScheme(maxK + (name[4] - '0'), minK, maxK);
+        return true;
+    }
+    return false;
+}
+
+const char* kNames[] = {"backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3"};
+const char* kDescs[] = {"single part, errors anywhere",
+                        "k+1 parts, one exact part per search (pigeonhole)",
+                        "k+1 parts, greedy-box optimum-style scheme",
+                        "k+2 parts, greedy-box optimum-style scheme (default)",
+                        "k+3 parts, greedy-box optimum-style scheme"};
+
+// expand(oss, len): parts of len/P (+1 for the first len%P parts); inside a
+// part the order follows the search direction; upper bounds hold for the
+// whole part, lower bounds apply at the part's last position.
+bool expand(const Part& s, unsigned len, std::vector<unsigned>& pi, std::vector<unsigned>& l,
+            std::vector<unsigned>& u) {
+    const unsigned P = (unsigned)s.pi.size();
+    if (len < P) return false;
+    std::vector<unsigned> first(P + 1, 0);
+    for (unsigned t = 0; t < P; ++t) first[t + 1] = first[t] + len / P + (t < len % P ? 1u : 0u);
+    pi.clear(); l.clear(); u.clear();
+    for (unsigned i = 0; i < P; ++i) {
+        const unsigned t = (unsigned)s.pi[i];
+        const bool asc = i == 0 ? (P == 1 || s.pi[1] > s.pi[0]) : (s.pi[i] > s.pi[i - 1]);
+        const unsigned a = first[t], b = first[t + 1];
+        for (unsigned j = a; j < b; ++j) {
+            pi.push_back(asc ? j : a + b - 1 - j);
+            u.push_back((unsigned)s.u[i]);
+            l.push_back(j + 1 == b ? (unsigned)s.l[i] : (i ? (unsigned)s.l[i - 1] : 0u));
+        }
+    }
+    return true;
+}
+
+void toHamming(std::vector<unsigned>& l, std::vector<unsigned>& u) {
+    const size_t m = l.size();
+    for (size_t p = 0; p < m; ++p) u[p] = std::min<unsigned>(u[p], (unsigned)p + 1);
+    for (size_t p = m - 1; p-- > 0;)
+        if (l[p + 1] > 0) l[p] = std::max(l[p], l[p + 1] - 1);
+}
+
+// Tree size of one expanded search when every symbol exists (the reference
+// prints nodeCount<Edit>(oss, sigma), search.cpp:197): DP over (pos, e) with
+// (sigma-1) M/S edges, and for Edit one I edge and (sigma-1) D edges.
+// weightedNodeCount additionally weights a node at text depth d by
+// min(1, N / (sigma-1)^d), its expected number of occurrences in N random
+// symbols (search.cpp:198).
+void counts(const std::vector<unsigned>& l, const std::vector<unsigned>& u, bool edit, int sigma, double N,
+            double& nodes, double& weighted) {
+    const size_t m = l.size();
+    const int A = std::max(1, sigma - 1);
+    const unsigned K = 16;
+    // f[pos][e][depth] would be large; depth only matters through the weight,
+    // so track weighted and unweighted sums per (e, depth) on the fly.
+    const size_t D = m + 16;
+    std::vector<double> cur(K * D, 0.0), nxt(K * D, 0.0);
+    cur[0] = 1.0;  // root: pos 0, e 0, depth 0
+    nodes = 0;
+    weighted = 0;
+    auto w = [&](size_t d) { return std::min(1.0, N / std::pow((double)A, (double)d)); };
+    for (size_t pos = 0; pos < m; ++pos) {
+        // deletions stay at pos: propagate within the layer in increasing e
+        if (edit) {
+            for (unsigned e = 0; e + 1 <= u[pos] && e + 1 < K; ++e)
+                for (size_t d = 0; d + 1 < D; ++d)
+                    if (cur[e * D + d] > 0 && pos > 0) cur[(e + 1) * D + d + 1] += cur[e * D + d] * A;
+        }
+        std::fill(nxt.begin(), nxt.end(), 0.0);
+        for (unsigned e = 0; e < K; ++e)
+            for (size_t d = 0; d < D; ++d) {
+                const double c = cur[e * D + d];
+                if (c == 0) continue;
+                nodes += c;
+                weighted += c * w(d);
+                if (d + 1 < D) {
+                    if (l[pos] <= e && e <= u[pos]) nxt[e * D + d + 1] += c;               // M
+                    if (l[pos] <= e + 1 && e + 1 <= u[pos] && e + 1 < K) {
+                        nxt[(e + 1) * D + d + 1] += c * (A - 1);                         // S
+                        if (edit) nxt[(e + 1) * D + d] += c;                             // I
+                    }
+                }
+            }
+        cur.swap(nxt);
+    }
+    for (double c : cur) nodes += c;  // leaves
+}
+
+}  // namespace
+
+extern "C" {
+
+int sahara_scheme_generators(const char** names, const char** descs, int cap) {
+    const int n = (int)(sizeof(kNames) / sizeof(kNames[0]));
+    for (int i = 0; i < n && i < cap; ++i) {
+        if (names) names[i] = kNames[i];
+        if (descs) descs[i] = kDescs[i];
+    }
+    return n;
+}
+
+int sahara_scheme(const char* generator, int min_k, int max_k, uint32_t len, int hamming, uint32_t* pi,
+                  uint32_t* l, uint32_t* u, int max_searches) {
+    std::vector<Part> parts;
+    if (!generator || !generate(generator, min_k, max_k, parts)) return -1;
+    if (!pi) return (int)parts.size();
+    if ((int)parts.size() > max_searches) return -2;
+    std::vector<unsigned> P, L, U;
+    for (size_t s = 0; s < parts.size(); ++s) {
+        if (!expand(parts[s], len, P, L, U)) return -3;
+        if (hamming) toHamming(L, U);
+        for (uint32_t j = 0; j < len; ++j) {
+            pi[s * len + j] = P[j];
+            l[s * len + j] = L[j];
+            u[s * len + j] = U[j];
+        }
+    }
+    return (int)parts.size();
+}
+
+int sahara_scheme_parts(const char* generator, int min_k, int max_k, int* parts_out, int* pi, int* l, int* u,
+                        int max_entries) {
+    std::vector<Part> parts;
+    if (!generator || !generate(generator, min_k, max_k, parts)) return -1;
+    const int P = (int)parts[0].pi.size();
+    if (parts_out) *parts_out = P;
+    if (pi) {
+        if ((int)parts.size() * P > max_entries) return -2;
+        for (size_t s = 0; s < parts.size(); ++s)
+            for (int i = 0; i < P; ++i) {
+                pi[s * P + i] = parts[s].pi[i];
+                l[s * P + i] = parts[s].l[i];
+                u[s * P + i] = parts[s].u[i];
+            }
+    }
+    return (int)parts.size();
+}
+
+int sahara_scheme_counts(const uint32_t* l, const uint32_t* u, uint32_t n_searches, uint32_t len, int edit,
+                         int sigma, double text_len, double* node_count, double* weighted_node_count) {
+    double nc = 0, wc = 0;
+    for (uint32_t s = 0; s < n_searches; ++s) {
+        std::vector<unsigned> L(l + (size_t)s * len, l + (size_t)(s + 1) * len),
+            U(u + (size_t)s * len, u + (size_t)(s + 1) * len);
+        double a = 0, b = 0;
+        counts(L, U, edit != 0, sigma, text_len, a, b);
+        nc += a;
+        wc += b;
+    }
+    *node_count = nc;
+    *weighted_node_count = wc;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,392 @@
+// search.hip — search-scheme DFS + locate on the GPU-resident FM-index (gfx950).
+//
+// Replaces fmc::search_ng24::search<Edit> (/root/reference/src/sahara/search.cpp:227,230)
+// and fmc::LocateLinear (search.cpp:244-250) — semantics policy P0,
+// docs/semantics.md; CPU restatement in oracle/oracle.cpp (Searcher::visit).
+//
+// Execution model (one lane = one DFS, the wave shares the work queue):
+//   * Work items are (pattern, search) pairs. A lane with nothing to do takes
+//     the next item; all idle lanes of a wave are served by ONE atomic on the
+//     item counter (ballot + mbcnt prefix compaction).
+//   * Each lane walks its search tree depth-first. The node being expanded
+//     stays in registers; at every expansion the match child is pushed first
+//     and all error children above it, and one error child continues in
+//     registers. Hence the stack only holds siblings of error edges on the
+//     current path: at most k * (2*sigma - 2) entries (k <= 15), independent
+//     of the pattern length. Stacks live in HBM interleaved [depth][lane] so a
+//     wave's pushes/pops at equal depth coalesce; the hot top sits in L2.
+//   * An expansion ranks all sigma-1 symbols at lo and lo+len on the BWT of
+//     the extension side: one 64-B Occ line per distinct 64-row block (1 or 2
+//     lines), coalesced 16-B loads, popcount arithmetic — no LDS, no MFMA.
+//   * Leaves (pos == len) are compacted to the hit buffer with a wave ballot
+//     + one atomic per wave. Overflow of the hit buffer is flagged and the
+//     host re-runs the batch with a larger buffer; nothing is truncated.
+// Locate: one lane per reported cursor walks LF (<= rate-1 steps) on the
+// forward lines to a sampled row; each step is one 64-B line. Records are
+// packed into u64 keys (qid, text position, e) and radix-sorted for the
+// canonical (qid, seq_id, pos, e) order.
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "search.h"
+
+namespace sahara {
+namespace {
+
+__device__ __forceinline__ void loadRankPart(const OccLine* L, uint32_t b, uint32_t cnt[5], uint64_t p[3]) {
+    const uint4* q = reinterpret_cast<const uint4*>(L + b);
+    const uint4 a0 = q[0], a1 = q[1], a2 = q[2];
+    cnt[0] = a0.x; cnt[1] = a0.y; cnt[2] = a0.z; cnt[3] = a0.w; cnt[4] = a1.x;
+    p[0] = (uint64_t)a1.z | ((uint64_t)a1.w << 32);
+    p[1] = (uint64_t)a2.x | ((uint64_t)a2.y << 32);
+    p[2] = (uint64_t)a2.z | ((uint64_t)a2.w << 32);
+}
+
+__device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
+    uint32_t r = v[0];
+    r = i == 1 ? v[1] : r;
+    r = i == 2 ? v[2] : r;
+    r = i == 3 ? v[3] : r;
+    r = i == 4 ? v[4] : r;
+    return r;
+}
+
+template <int SIGMA, bool EDIT, bool COUNT>
+__global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
+    extern __shared__ uint32_t sch[];
+    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) sch[i] = a.scheme[i];
+    __syncthreads();
+
+    const uint32_t T = gridDim.x * blockDim.x;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t ltMask = (1ull << lane) - 1ull;
+    uint4* stk = a.stack + gtid;
+
+    uint32_t sp = 0, pid = 0, sOff = 0;
+    bool have = false, exhausted = false;
+    uint4 cur = make_uint4(0, 0, 0, 0);
+    uint64_t cNodes = 0, cRank = 0, cLines = 0;
+
+    for (;;) {
+        // ---- refill idle lanes from the item queue (one atomic per wave)
+        const bool need = !have && sp == 0 && !exhausted;
+        const uint64_t nm = __ballot(need);
+        if (nm) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)nm) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.work, (uint32_t)__popcll(nm));
+            base = __shfl(base, (int)leader);
+            if (need) {
+                const uint32_t item = base + (uint32_t)__popcll(nm & ltMask);
+                if (item < a.nitems) {
+                    pid = item / a.nsearch;
+                    sOff = (item - pid * a.nsearch) * a.m;
+                    cur = make_uint4(0u, 0u, a.n, 0u);
+                    have = true;
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (!have && sp > 0) {
+            --sp;
+            cur = stk[(size_t)sp * T];
+            have = true;
+        }
+        if (!__any(have)) break;
+
+        // ---- leaves -> hit buffer (ballot compaction, one atomic per wave)
+        const uint32_t pos = cur.w & 0xFFFFu;
+        const bool leaf = have && pos == a.m;
+        const uint64_t lm = __ballot(leaf);
+        if (lm) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)lm) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.hitCount, (uint32_t)__popcll(lm));
+            base = __shfl(base, (int)leader);
+            if (leaf) {
+                const uint32_t idx = base + (uint32_t)__popcll(lm & ltMask);
+                if (idx < a.hitCap) a.hits[idx] = make_uint4(pid, cur.x, cur.z, (cur.w >> 16) & 0xFu);
+                else atomicOr(a.flags, 2u);
+                have = false;
+            }
+        }
+        if (have) {
+        // ---- expand one node
+        const uint32_t e = (cur.w >> 16) & 0xFu;
+        const uint32_t lastL = (cur.w >> 20) & 3u, lastR = (cur.w >> 22) & 3u;
+        const uint32_t se = sch[sOff + pos];
+        const uint32_t q = se & 0xFFFFu, lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
+        const bool right = (se >> 24) & 1u;
+        const uint32_t cq = a.pats[(size_t)pid * a.m + q];
+        const uint32_t side = right ? lastR : lastL;
+        const bool matchOK = lb <= e && e <= ub;
+        const bool misOK = lb <= e + 1 && e + 1 <= ub;
+        const bool delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
+        const bool insOK = EDIT && misOK && side != OP_D;
+        auto meta = [&](uint32_t npos, uint32_t ne, uint32_t op) -> uint32_t {
+            const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
+            const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
+            return packMeta(npos, ne, nl, nr);
+        };
+        if (COUNT) ++cNodes;
+
+        uint32_t occ[SIGMA], nlo[SIGMA], noth[SIGMA];
+#pragma unroll
+        for (int c = 0; c < SIGMA; ++c) occ[c] = nlo[c] = noth[c] = 0;
+        if (matchOK || misOK || delOK) {
+            const OccLine* L = right ? a.occR : a.occF;
+            const uint32_t lo = right ? cur.y : cur.x;
+            const uint32_t hi = lo + cur.z;
+            uint32_t ca[5], cb[5];
+            uint64_t pa[3], pb[3];
+            loadRankPart(L, lo >> 6, ca, pa);
+            const bool two = (hi >> 6) != (lo >> 6);
+            if (two) {
+                loadRankPart(L, hi >> 6, cb, pb);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) cb[i] = ca[i];
+                pb[0] = pa[0]; pb[1] = pa[1]; pb[2] = pa[2];
+            }
+            if (COUNT) { ++cRank; cLines += two ? 2 : 1; }
+            const uint64_t ml = lowMask(lo & 63u), mh = lowMask(hi & 63u);
+            uint32_t sum = 0;
+#pragma unroll
+            for (int c = 1; c < SIGMA; ++c) {
+                const uint32_t rl = ca[c - 1] + (uint32_t)__popcll(symMask(pa, c) & ml);
+                const uint32_t rh = cb[c - 1] + (uint32_t)__popcll(symMask(pb, c) & mh);
+                occ[c] = rh - rl;
+                nlo[c] = a.C[c] + rl;
+                sum += occ[c];
+            }
+            uint32_t acc = (right ? cur.x : cur.y) + (cur.z - sum);
+#pragma unroll
+            for (int c = 1; c < SIGMA; ++c) { noth[c] = acc; acc += occ[c]; }
+        }
+        auto child = [&](int c, uint32_t m) -> uint4 {
+            return right ? make_uint4(noth[c], nlo[c], occ[c], m) : make_uint4(nlo[c], noth[c], occ[c], m);
+        };
+
+        // count error children; find the match child
+        uint32_t nErr = insOK ? 1u : 0u;
+        bool hasM = false;
+        uint4 mChild = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int c = 1; c < SIGMA; ++c) {
+            if (occ[c]) {
+                if ((uint32_t)c == cq) {
+                    hasM = matchOK;
+                    mChild = child(c, meta(pos + 1, e, OP_MS));
+                } else {
+                    nErr += misOK ? 1u : 0u;
+                }
+                nErr += delOK ? 1u : 0u;
+            }
+        }
+        bool kept = false;
+        uint4 next = make_uint4(0, 0, 0, 0);
+        auto push = [&](const uint4& v) {
+            if (sp < a.stackCap) {
+                stk[(size_t)sp * T] = v;
+                ++sp;
+            } else {
+                atomicOr(a.flags, 1u);
+            }
+        };
+        auto emit = [&](const uint4& v) {
+            if (!kept) { next = v; kept = true; }
+            else push(v);
+        };
+        if (hasM && nErr) push(mChild);  // match child below all its error siblings
+        if (insOK) emit(make_uint4(cur.x, cur.y, cur.z, meta(pos + 1, e + 1, OP_I)));
+#pragma unroll
+        for (int c = 1; c < SIGMA; ++c) {
+            if (occ[c]) {
+                if ((uint32_t)c != cq && misOK) emit(child(c, meta(pos + 1, e + 1, OP_MS)));
+                if (delOK) emit(child(c, meta(pos, e + 1, OP_D)));
+            }
+        }
+        if (!kept && hasM) { next = mChild; kept = true; }
+        have = kept;
+        cur = next;
+        }  // have
+    }
+    if (COUNT) {
+        atomicAdd(a.counters + 0, (unsigned long long)cNodes);
+        atomicAdd(a.counters + 1, (unsigned long long)cRank);
+        atomicAdd(a.counters + 2, (unsigned long long)cLines);
+    }
+}
+
+// One lane per reported cursor: locate every row of [lb, lb+len).
+template <bool COUNT>
+__global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
+    uint64_t steps = 0;
+    for (uint64_t h = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; h < a.nhits;
+         h += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 hit = a.hits[h];
+        const uint64_t out = a.rowOff[h];
+        for (uint32_t j = 0; j < hit.z; ++j) {
+            uint32_t row = hit.y + j;
+            uint32_t st = 0;
+            uint64_t gpos = 0;
+            for (;;) {
+                const uint4* q = reinterpret_cast<const uint4*>(a.occF + (row >> 6));
+                const uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+                const uint32_t o = row & 63u;
+                const uint64_t sampled = (uint64_t)a3.x | ((uint64_t)a3.y << 32);
+                if ((sampled >> o) & 1ull) {
+                    const uint32_t k = a1.y + (uint32_t)__popcll(sampled & lowMask(o));
+                    gpos = (uint64_t)a.samples[k] + st;
+                    break;
+                }
+                const uint64_t p[3] = {(uint64_t)a1.z | ((uint64_t)a1.w << 32),
+                                       (uint64_t)a2.x | ((uint64_t)a2.y << 32),
+                                       (uint64_t)a2.z | ((uint64_t)a2.w << 32)};
+                const uint32_t c = symAt(p, o);
+                if (c == 0 || st >= a.rate) {  // cannot happen on a well-formed index
+                    atomicOr(a.flags, 4u);
+                    break;
+                }
+                const uint32_t cnt[5] = {a0.x, a0.y, a0.z, a0.w, a1.x};
+                row = a.C[c] + pick5(cnt, c - 1) + (uint32_t)__popcll(symMask(p, c) & lowMask(o));
+                ++st;
+            }
+            if (COUNT) steps += st;
+            a.keys[out + j] = ((uint64_t)hit.x << 36) | (gpos << 4) | (uint64_t)hit.w;
+        }
+    }
+    if (COUNT && steps) atomicAdd(a.counters, (unsigned long long)steps);
+}
+
+__global__ void kDecode(const uint64_t* __restrict__ keys, uint64_t n, uint64_t qidBase,
+                        const uint64_t* __restrict__ starts, uint32_t nrec, sahara_hit* __restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        const uint64_t gpos = (k >> 4) & 0xFFFFFFFFull;
+        uint32_t lo = 0, hi = nrec;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (starts[mid] <= gpos) lo = mid; else hi = mid;
+        }
+        sahara_hit h;
+        h.qid = qidBase + (k >> 36);
+        h.seq_id = lo;
+        h.err = (uint32_t)(k & 15u);
+        h.pos = gpos - starts[lo];
+        out[i] = h;
+    }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+__global__ void kDigest(const sahara_hit* __restrict__ h, uint64_t n, unsigned long long* out) {
+    uint64_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        acc += mix64(h[i].qid * 0x9E3779B97F4A7C15ull ^ mix64(((uint64_t)h[i].seq_id << 40) ^ (h[i].pos << 4) ^ h[i].err));
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, (unsigned long long)acc);
+}
+
+struct HitLen {
+    __host__ __device__ uint64_t operator()(const uint4& h) const { return (uint64_t)h.z; }
+};
+
+template <int SIGMA>
+void launchSearchT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
+    if (edit) {
+        if (count) hipLaunchKernelGGL((kSearch<SIGMA, true, true>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearch<SIGMA, true, false>), grid, dim3(256), lds, st, a);
+    } else {
+        if (count) hipLaunchKernelGGL((kSearch<SIGMA, false, true>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearch<SIGMA, false, false>), grid, dim3(256), lds, st, a);
+    }
+}
+
+}  // namespace
+
+int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
+    int b = 0;
+    const void* f;
+    if (sigma == 5) f = edit ? (const void*)kSearch<5, true, false> : (const void*)kSearch<5, false, false>;
+    else            f = edit ? (const void*)kSearch<6, true, false> : (const void*)kSearch<6, false, false>;
+    SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
+    return b < 1 ? 1 : b;
+}
+
+void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
+                  hipStream_t st) {
+    if (sigma == 5) launchSearchT<5>(a, edit, count, dim3(blocks), lds, st);
+    else            launchSearchT<6>(a, edit, count, dim3(blocks), lds, st);
+    SH_HIP(hipGetLastError());
+}
+
+size_t rowOffsetsTempBytes(uint64_t nhits) {
+    size_t tb = 0;
+    rocprim::transform_iterator<const uint4*, HitLen, uint64_t> it(nullptr, HitLen());
+    SH_HIP(rocprim::exclusive_scan(nullptr, tb, it, (uint64_t*)nullptr, (uint64_t)0, (size_t)nhits + 1,
+                                   rocprim::plus<uint64_t>(), (hipStream_t)0));
+    return tb;
+}
+
+void rowOffsets(const uint4* hits, uint64_t nhits, uint64_t* off, void* tmp, size_t tmpBytes, hipStream_t st) {
+    // off[nhits] = total rows (hits[nhits] must be readable: caller zeroes it)
+    rocprim::transform_iterator<const uint4*, HitLen, uint64_t> it(hits, HitLen());
+    size_t tb = tmpBytes;
+    SH_HIP(rocprim::exclusive_scan(tmp, tb, it, off, (uint64_t)0, (size_t)nhits + 1, rocprim::plus<uint64_t>(),
+                                   st));
+}
+
+void launchLocate(const LocateArgs& a, bool count, hipStream_t st) {
+    if (a.nhits == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((a.nhits + 255) / 256, 65536);
+    if (count) hipLaunchKernelGGL(kLocate<true>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else       hipLaunchKernelGGL(kLocate<false>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    SH_HIP(hipGetLastError());
+}
+
+size_t sortTempBytes(uint64_t n) {
+    size_t tb = 0;
+    rocprim::double_buffer<uint64_t> kb(nullptr, nullptr);
+    SH_HIP(rocprim::radix_sort_keys(nullptr, tb, kb, (size_t)n, 0, 64, (hipStream_t)0));
+    return tb;
+}
+
+uint64_t* sortKeys(uint64_t* k0, uint64_t* k1, uint64_t n, unsigned endBit, void* tmp, size_t tmpBytes,
+                   hipStream_t st) {
+    if (n == 0) return k0;
+    rocprim::double_buffer<uint64_t> kb(k0, k1);
+    size_t tb = tmpBytes;
+    SH_HIP(rocprim::radix_sort_keys(tmp, tb, kb, (size_t)n, 0, endBit, st));
+    return kb.current();
+}
+
+void launchDecode(const uint64_t* keys, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint32_t nrec,
+                  sahara_hit* out, hipStream_t st) {
+    if (n == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 65536);
+    hipLaunchKernelGGL(kDecode, dim3((unsigned)blocks), dim3(256), 0, st, keys, n, qidBase, starts, nrec, out);
+    SH_HIP(hipGetLastError());
+}
+
+void launchDigest(const sahara_hit* h, uint64_t n, unsigned long long* out, hipStream_t st) {
+    if (n == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(kDigest, dim3((unsigned)blocks), dim3(256), 0, st, h, n, out);
+    SH_HIP(hipGetLastError());
+}
+
+}  // namespace sahara

@@ -1,0 +1,22 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
+    config.addinivalue_line("markers", "slow: larger CPU cases")
+
+
+@pytest.fixture(scope="session")
+def gpu_device():
+    import sahara_amd as sa
+    n = sa.lib().sahara_gpu_device_count()
+    if n < 1:
+        pytest.fail("no HIP device visible; gpu-marked tests need an MI355X")
+    return 0

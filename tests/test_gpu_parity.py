@@ -1,0 +1,175 @@
+"""GPU (HIP, gfx950) vs the CPU restatement: bit-exact multisets.
+
+Every test runs through the C ABI of sahara_amd/lib/libsahara_hip.so.
+Parity bar: the multiset of (qid, seq_id, pos, e) records is identical to the
+oracle's (oracle/oracle.cpp), and the GPU-built index (SA, both BWTs, C,
+samples) equals the oracle's construction byte for byte.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import sahara_amd as sa
+from helpers import hits_as_rows, mutate_reads, pset, random_records
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sigma", [5, 6])
+@pytest.mark.parametrize("shape", ["multi", "repeats", "tiny"])
+def test_gpu_index_equals_oracle(gpu_device, sigma, shape):
+    rng = np.random.default_rng(hash((sigma, shape)) % 2**32)
+    if shape == "multi":
+        recs = random_records(rng, [5000, 1, 130, 4096, 63, 64, 65], sigma, with_n=True)
+    elif shape == "repeats":
+        recs = random_records(rng, [6000, 3000], sigma, repeats=True)
+        recs[0][100:1100] = recs[0][0]  # long homopolymer: many doubling rounds
+    else:
+        recs = [np.array([1], np.uint8)]
+    ref = O.Index.build(recs, sigma, 16)
+    gpu = sa.BiFMIndex.build(recs, sigma=sigma, sampling_rate=16, device=gpu_device)
+    a = ref.export()
+    b = gpu.export()
+    assert np.array_equal(gpu.export_sa(), a["sa"])
+    for key in ("bwt_f", "bwt_r", "sampled", "samples"):
+        assert np.array_equal(a[key], b[key]), key
+    assert np.array_equal(a["C"][: sigma + 1], b["C"])
+
+
+CASES = [  # sigma, edit, k, m, gen, with_n, repeats
+    (6, True, 0, 32, "h2-k2", False, False),
+    (6, True, 1, 40, "h2-k2", True, False),
+    (6, True, 2, 50, "h2-k2", False, True),
+    (6, True, 2, 50, "pigeon", False, False),
+    (6, True, 2, 30, "backtracking", True, False),
+    (6, True, 3, 60, "h2-k3", False, True),
+    (6, True, 3, 60, "h2-k1", False, False),
+    (5, True, 2, 50, "h2-k2", False, False),
+    (5, True, 3, 40, "h2-k2", False, True),
+    (6, False, 1, 40, "h2-k2", False, False),
+    (6, False, 2, 50, "h2-k2", True, True),
+    (5, False, 3, 60, "pigeon", False, False),
+]
+
+
+@pytest.mark.parametrize("sigma,edit,k,m,gen,with_n,repeats", CASES)
+def test_gpu_search_multiset_equals_oracle(gpu_device, sigma, edit, k, m, gen, with_n, repeats):
+    rng = np.random.default_rng(7 * k + m + sigma + (1 if edit else 0))
+    recs = random_records(rng, [20000, 7000, 3000], sigma, with_n=with_n, repeats=repeats)
+    reads = mutate_reads(rng, recs, 300, m, k, sigma)
+    pats = sa.interleave_rc(reads, sigma)
+    scheme = sa.search_scheme(gen, 0, k, m, hamming=not edit)
+    ref = O.Index.build(recs, sigma, 16)
+    want, _ = ref.search(pats, scheme, edit=edit, nthreads=8)
+    gpu = sa.BiFMIndex.build(recs, sigma=sigma, device=gpu_device)
+    got = sa.search(gpu, pats, scheme, edit=edit)
+    assert len(got) == len(want)
+    # canonical order out of the ABI
+    rows = hits_as_rows(got)
+    raw = np.stack([got["qid"], got["seq_id"], got["pos"], got["err"]], 1).astype(np.uint64)
+    assert np.array_equal(rows, raw)
+    assert np.array_equal(rows, hits_as_rows(want))
+
+
+def test_gpu_pset_equals_bruteforce(gpu_device):
+    rng = np.random.default_rng(77)
+    recs = random_records(rng, [900, 400], 6, with_n=True, repeats=True)
+    reads = mutate_reads(rng, recs, 40, 24, 2)
+    scheme = sa.search_scheme("h2-k2", 0, 2, 24)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    got = sa.search(gpu, reads, scheme, edit=True)
+    bf = O.bruteforce(recs, reads, 2, edit=True)
+    assert pset(hits_as_rows(got)) == pset(hits_as_rows(bf))
+
+
+def test_idx_files_cross_load(gpu_device, tmp_path):
+    rng = np.random.default_rng(5)
+    recs = random_records(rng, [3000, 500], 6, with_n=True)
+    ref = O.Index.build(recs, 6, 16)
+    p1 = tmp_path / "oracle.idx"
+    ref.write(p1)
+    g1 = sa.BiFMIndex.load(p1, device=gpu_device)          # oracle-written -> GPU
+    g2 = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    p2 = tmp_path / "gpu.idx"
+    g2.save(p2)
+    r2 = O.Index.read(p2)                                    # GPU-written -> oracle
+    a, b = ref.export(with_sa=False), r2.export(with_sa=False)
+    for key in ("bwt_f", "bwt_r", "sampled", "samples", "C"):
+        assert np.array_equal(a[key], b[key]), key
+    assert open(p1, "rb").read() == open(p2, "rb").read()     # byte-identical files
+    g3 = sa.BiFMIndex.from_bytes(open(p2, "rb").read(), device=gpu_device)
+    reads = mutate_reads(rng, recs, 50, 30, 2)
+    sch = sa.search_scheme("h2-k2", 0, 2, 30)
+    want = hits_as_rows(ref.search(reads, sch)[0])
+    for g in (g1, g2, g3):
+        assert np.array_equal(hits_as_rows(sa.search(g, reads, sch)), want)
+
+
+def test_hit_buffer_overflow_reruns(gpu_device, monkeypatch):
+    rng = np.random.default_rng(8)
+    recs = random_records(rng, [4000], 6, repeats=True)
+    recs[0][:500] = 1  # poly-A: huge intervals, many cursors
+    reads = np.vstack([np.full((20, 20), 1, np.uint8), mutate_reads(rng, recs, 30, 20, 1)])
+    sch = sa.search_scheme("h2-k2", 0, 1, 20)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(reads, sch)[0])
+    monkeypatch.setenv("SAHARA_HITCAP", "7")
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    got = sa.search(gpu, reads, sch)
+    assert np.array_equal(hits_as_rows(got), want)
+
+
+def test_no_hits_and_device_resident_path(gpu_device):
+    rng = np.random.default_rng(9)
+    recs = random_records(rng, [5000], 6)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    sch = sa.search_scheme("h2-k2", 0, 1, 40)
+    junk = np.array(rng.integers(1, 4, size=(10, 40)), np.uint8)  # random 40-mers: absent from 5 kbp
+    assert len(sa.search(gpu, junk, sch)) == 0
+    reads = mutate_reads(rng, recs, 100, 40, 1)
+    direct = sa.search(gpu, reads, sch)
+    gpu.stage(reads, sch, edit=True)
+    n = gpu.run(count=True)
+    st = gpu.stats()
+    assert n == len(direct) == st["hits"]
+    assert np.array_equal(gpu.fetch(), direct)
+    d1 = gpu.digest()
+    gpu.run(count=False)
+    assert gpu.digest() == d1
+    # counters agree with the oracle's deterministic work counts
+    ref = O.Index.build(recs, 6, 16)
+    _, cnt = ref.search(reads, sch, edit=True)
+    assert st["nodes"] == cnt["nodes"]
+    assert st["rank_nodes"] == cnt["rank_nodes"]
+    assert st["ext_lines"] == cnt["ext_lines"]
+    assert st["lf_steps"] == cnt["lf_steps"]
+    assert st["cursors"] == cnt["leaves"]
+
+
+def test_errors_are_loud(gpu_device):
+    rng = np.random.default_rng(10)
+    recs = random_records(rng, [500], 6)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    bad = np.zeros((2, 10), np.uint8)  # rank 0 ('$') is not a query symbol
+    with pytest.raises(sa.SaharaError, match="rank out of range"):
+        sa.search(gpu, bad, sa.search_scheme("h2-k2", 0, 1, 10))
+    with pytest.raises(sa.SaharaError, match="max_hits"):
+        sa.search(gpu, np.ones((1, 10), np.uint8), sa.search_scheme("h2-k2", 0, 1, 10), max_hits=3)
+
+
+@pytest.mark.parametrize("k,m,nreads,ref_len", [(2, 100, 20000, 2_000_000), (3, 150, 3000, 1_000_000)])
+def test_medium_scale_parity(gpu_device, k, m, nreads, ref_len):
+    flat, lens = sa.synth_reference([ref_len // 2, ref_len // 3, ref_len - ref_len // 2 - ref_len // 3],
+                                    sigma=6, seed=42)
+    reads = sa.synth_reads(flat, lens, nreads, m, k, sigma=6, seed=7)
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme("h2-k2", 0, k, m)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    got = sa.search(gpu, pats, sch)
+    ex = gpu.export()
+    ref = O.Index.from_parts(6, ex["n"], lens, 16, ex["bwt_f"], ex["bwt_r"], ex["sampled"], ex["samples"])
+    want, _ = ref.search(pats, sch, edit=True, nthreads=8)
+    assert np.array_equal(hits_as_rows(got), hits_as_rows(want))
+    # every simulated read is found (forward strand) with <= k errors
+    found = np.zeros(nreads, bool)
+    found[(got["qid"][got["qid"] % 2 == 0] // 2).astype(np.int64)] = True
+    assert found.all()

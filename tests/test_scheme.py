@@ -1,0 +1,87 @@
+"""Search schemes: completeness, validity, and product == oracle restatement
+(search.cpp:174-212 generator/expand, :226 limitToHamming)."""
+import numpy as np
+import pytest
+
+import oracle as O
+import sahara_amd as sa
+
+GENS = ["backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3"]
+
+
+def covers(pi, l, u, d):
+    acc = 0
+    for i, part in enumerate(pi):
+        acc += d[part]
+        if acc < l[i] or acc > u[i]:
+            return False
+    return True
+
+
+def dists(P, lo, hi):
+    out = []
+
+    def rec(cur):
+        if len(cur) == P:
+            if lo <= sum(cur) <= hi:
+                out.append(list(cur))
+            return
+        for e in range(0, hi - sum(cur) + 1):
+            rec(cur + [e])
+    rec([])
+    return out
+
+
+@pytest.mark.parametrize("gen", GENS)
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 4])
+def test_complete_and_valid(gen, k):
+    for mink in range(0, k + 1):
+        pi, l, u = sa.scheme_parts(gen, mink, k)
+        P = pi.shape[1]
+        for s in range(pi.shape[0]):
+            assert sorted(pi[s].tolist()) == list(range(P))
+            lo = hi = pi[s][0]
+            for x in pi[s][1:]:
+                assert x in (lo - 1, hi + 1)
+                lo, hi = min(lo, x), max(hi, x)
+            assert all(l[s][i] <= u[s][i] for i in range(P))
+            assert all(l[s][i] <= l[s][i + 1] and u[s][i] <= u[s][i + 1] for i in range(P - 1))
+        for d in dists(P, mink, k):
+            assert any(covers(pi[s], l[s], u[s], d) for s in range(pi.shape[0])), (d, gen, mink, k)
+        assert O.scheme_complete(gen, mink, k)
+
+
+@pytest.mark.parametrize("gen", GENS)
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+@pytest.mark.parametrize("length", [7, 32, 100, 101, 250])
+@pytest.mark.parametrize("ham", [False, True])
+def test_product_scheme_equals_oracle(gen, k, length, ham):
+    a = sa.search_scheme(gen, 0, k, length, hamming=ham)
+    b = O.scheme(gen, 0, k, length, hamming=ham)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    pi = a[0]
+    for s in range(pi.shape[0]):
+        assert sorted(pi[s].tolist()) == list(range(length))
+
+
+def test_default_generator_shape():
+    # h2-k2 at k=2: 4 parts, every search starts with an exact part
+    pi, l, u = sa.scheme_parts("h2-k2", 0, 2)
+    assert pi.shape[1] == 4
+    assert all(u[s][0] == 0 for s in range(pi.shape[0]))
+
+
+def test_unknown_generator_and_short_pattern():
+    with pytest.raises(sa.SaharaError, match="valid generators are"):
+        sa.search_scheme("nope", 0, 2, 50)
+    with pytest.raises(sa.SaharaError):
+        sa.search_scheme("h2-k2", 0, 2, 3)  # 4 parts do not fit 3 positions
+
+
+def test_counts_monotone_in_k():
+    prev = 0
+    for k in range(0, 4):
+        nc, wnc = sa.scheme_counts(sa.search_scheme("h2-k2", 0, k, 100), True, 6, 3e9)
+        assert nc > prev and wnc > 0
+        prev = nc
