@@ -238,11 +238,15 @@ def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):
     del ex
     log(f"cpu baseline: oracle index loaded ({time.time()-t:.1f}s)")
     threads = host_threads()
-    # calibrate on a small sample, then scale to ~target_s
-    n = min(200, nreads)
-    t = time.perf_counter()
-    ref.search(pats[: 2 * n], scheme, edit=edit, nthreads=threads)
-    dt = time.perf_counter() - t
+    # calibrate: grow the sample until it runs >= 1 s, then scale to ~target_s
+    n = min(1000, nreads)
+    while True:
+        t = time.perf_counter()
+        ref.search(pats[: 2 * n], scheme, edit=edit, nthreads=threads)
+        dt = time.perf_counter() - t
+        if dt >= 1.0 or n >= nreads:
+            break
+        n = min(nreads, n * 4)
     n2 = int(min(nreads, max(n, n * target_s / max(dt, 1e-3))))
     t = time.perf_counter()
     hits, _ = ref.search(pats[: 2 * n2], scheme, edit=edit, nthreads=threads)

@@ -170,7 +170,7 @@ void run(Ctx* c, bool count) {
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     const uint64_t T = (uint64_t)blocks * 256;
     const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
-    c->stack.reserve(stackCap * T);
+    c->stack.reserve((size_t)std::max<uint32_t>(stackCap, 5) * T);  // levels beyond the LDS part (bounded by stackCap)
     S.search_grid = blocks;
 
     const uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
@@ -185,7 +185,7 @@ void run(Ctx* c, bool count) {
     for (uint64_t q0 = 0; q0 < c->npat; q0 += maxBatch) {
         const uint64_t nb = std::min<uint64_t>(maxBatch, c->npat - q0);
         ++S.batches;
-        uint32_t hostSmall[3];
+        uint32_t hostSmall[4];
         for (;;) {
             SH_HIP(hipMemsetAsync(c->small.ptr, 0, 4 * sizeof(uint32_t), c->st));
             SearchArgs a{};
@@ -201,6 +201,7 @@ void run(Ctx* c, bool count) {
             a.work = c->small.ptr;
             a.hitCount = c->small.ptr + 1;
             a.flags = c->small.ptr + 2;
+            a.filled = c->small.ptr + 3;
             a.stack = c->stack.ptr;
             a.stackCap = stackCap;
             a.hits = c->hits.ptr;
@@ -209,12 +210,12 @@ void run(Ctx* c, bool count) {
             SH_HIP(hipEventRecord(c->ev[0], c->st));
             launchSearch(a, sigma, c->edit, count, blocks, lds, c->st);
             SH_HIP(hipEventRecord(c->ev[1], c->st));
-            SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+            SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
             SH_HIP(hipStreamSynchronize(c->st));
             S.search_ms += elapsed(c->ev[0], c->ev[1]);
             ++S.search_launches;
             if (hostSmall[2] & 1u) throw Error("search stack overflow (internal bound violated)");
-            if ((hostSmall[2] & 2u) || hostSmall[1] > c->hitCap) {
+            if (hostSmall[2] & 2u) {
                 // hit buffer too small for this batch: grow and re-run it
                 const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
                 if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
@@ -224,8 +225,10 @@ void run(Ctx* c, bool count) {
             }
             break;
         }
-        const uint64_t nh = hostSmall[1];
-        S.cursors += nh;
+        // reserved slots incl. len-0 holes; a wave's last range may reach past
+        // the capacity without having written there (no overflow flag)
+        const uint64_t nh = std::min<uint64_t>(hostSmall[1], c->hitCap);
+        S.cursors += hostSmall[3];
 
         // locate: row offsets (exclusive scan of len), LF walks, canonical sort, decode
         SH_HIP(hipEventRecord(c->ev[2], c->st));
@@ -272,7 +275,7 @@ void run(Ctx* c, bool count) {
         launchDecode(sorted, rows, q0, c->I.dRecStarts.ptr, (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout,
                      c->st);
         SH_HIP(hipEventRecord(c->ev[4], c->st));
-        SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+        SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
         SH_HIP(hipStreamSynchronize(c->st));
         if (hostSmall[2] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
         S.locate_ms += elapsed(c->ev[2], c->ev[3]);

@@ -20,11 +20,12 @@ struct SearchArgs {
     uint32_t nitems;         // npat * nsearch
     const uint32_t* scheme;  // nsearch * m packed entries (packScheme)
     uint32_t* work;          // item counter
-    uint4* stack;            // stackCap * (grid threads) nodes, [depth][lane]
+    uint4* stack;            // (stackCap - 4) * (grid threads) spilled nodes, [depth][lane]
     uint32_t stackCap;
     uint4* hits;             // (qid, lb, len, e)
     uint32_t hitCap;
-    uint32_t* hitCount;
+    uint32_t* hitCount;      // reserved slots (waves reserve ranges; unused slots have len 0)
+    uint32_t* filled;        // cursors actually written
     uint32_t* flags;         // 1 = stack overflow, 2 = hit-buffer overflow, 4 = corrupt locate
     unsigned long long* counters;  // nodes, rank nodes, lines
 };

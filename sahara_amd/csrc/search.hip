@@ -37,13 +37,49 @@
 namespace sahara {
 namespace {
 
-__device__ __forceinline__ void loadRankPart(const OccLine* L, uint32_t b, uint32_t cnt[5], uint64_t p[3]) {
-    const uint4* q = reinterpret_cast<const uint4*>(L + b);
-    const uint4 a0 = q[0], a1 = q[1], a2 = q[2];
-    cnt[0] = a0.x; cnt[1] = a0.y; cnt[2] = a0.z; cnt[3] = a0.w; cnt[4] = a1.x;
-    p[0] = (uint64_t)a1.z | ((uint64_t)a1.w << 32);
-    p[1] = (uint64_t)a2.x | ((uint64_t)a2.y << 32);
-    p[2] = (uint64_t)a2.z | ((uint64_t)a2.w << 32);
+// Swap a dword with the neighbour lane of the pair (DPP quad_perm [1,0,3,2]).
+__device__ __forceinline__ uint32_t pairSwap(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint4 pairSwap4(const uint4& v) {
+    return make_uint4(pairSwap(v.x), pairSwap(v.y), pairSwap(v.z), pairSwap(v.w));
+}
+__device__ __forceinline__ uint64_t pairSwap64(uint64_t v) {
+    return (uint64_t)pairSwap((uint32_t)v) | ((uint64_t)pairSwap((uint32_t)(v >> 32)) << 32);
+}
+
+// Pair-cooperative fetch of the rank part (bytes 0..47) of one 64-B Occ line
+// per lane. Must be called by all 64 lanes (wave-uniform control flow):
+// for the pair (E = even lane's line, O = odd lane's line) four loads run
+//   #1 E bytes 0-15 | 16-31   #2 E bytes 32-47 | 48-63
+//   #3 O bytes 0-15 | 16-31   #4 O bytes 32-47 | 48-63
+// (even | odd lane), so each wave instruction touches <= 32 distinct lines;
+// two DPP swaps then hand each lane the chunks of its own line.
+__device__ __forceinline__ void fetchLinePair(uint64_t own, bool need, bool odd, uint32_t cnt[5], uint64_t p[3]) {
+    const uint64_t other = pairSwap64(own);
+    const bool otherNeed = pairSwap(need ? 1u : 0u) != 0u;
+    const uint64_t addrE = odd ? other : own, addrO = odd ? own : other;
+    const bool needE = odd ? otherNeed : need, needO = odd ? need : otherNeed;
+    const uint32_t half = odd ? 16u : 0u;
+    uint4 r1 = make_uint4(0, 0, 0, 0), r2 = r1, r3 = r1, r4 = r1;
+    if (needE) {
+        r1 = *reinterpret_cast<const uint4*>(addrE + half);
+        r2 = *reinterpret_cast<const uint4*>(addrE + 32 + half);
+    }
+    if (needO) {
+        r3 = *reinterpret_cast<const uint4*>(addrO + half);
+        r4 = *reinterpret_cast<const uint4*>(addrO + 32 + half);
+    }
+    // even: r1 = E0, r2 = E2, r3 = O0, r4 = O2 ; odd: r1 = E1, r2 = E3, r3 = O1, r4 = O3
+    const uint4 g1 = pairSwap4(odd ? r1 : r3);  // even <- E1, odd <- O0
+    const uint4 g2 = pairSwap4(r4);             // odd <- O2 (even receives O3, unused)
+    const uint4 c0 = odd ? g1 : r1;
+    const uint4 c1 = odd ? r3 : g1;
+    const uint4 c2 = odd ? g2 : r2;
+    cnt[0] = c0.x; cnt[1] = c0.y; cnt[2] = c0.z; cnt[3] = c0.w; cnt[4] = c1.x;
+    p[0] = (uint64_t)c1.z | ((uint64_t)c1.w << 32);
+    p[1] = (uint64_t)c2.x | ((uint64_t)c2.y << 32);
+    p[2] = (uint64_t)c2.z | ((uint64_t)c2.w << 32);
 }
 
 __device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
@@ -55,6 +91,10 @@ __device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
     return r;
 }
 
+constexpr uint32_t kWorkChunk = 256;  // items a wave takes per atomic
+constexpr uint32_t kHitChunk = 64;    // hit slots a wave reserves per atomic
+constexpr uint32_t kLdsDepth = 4;     // DFS stack levels kept in LDS (16 KB per block)
+
 template <int SIGMA, bool EDIT, bool COUNT>
 __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
     extern __shared__ uint32_t sch[];
@@ -65,70 +105,128 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t ltMask = (1ull << lane) - 1ull;
+    const bool odd = lane & 1u;
+    // DFS stack: the bottom kLdsDepth levels live in LDS ([level][thread],
+    // conflict-free 16-B rows when lanes sit at equal depth), deeper levels
+    // spill to HBM ([level][grid thread]). Typical depth stays in LDS.
+    __shared__ uint4 lstk[kLdsDepth][256];
     uint4* stk = a.stack + gtid;
+    auto spush = [&](uint32_t d, const uint4& v) {
+        if (d < kLdsDepth) lstk[d][threadIdx.x] = v;
+        else stk[(size_t)(d - kLdsDepth) * T] = v;
+    };
+    auto spop = [&](uint32_t d) -> uint4 {
+        return d < kLdsDepth ? lstk[d][threadIdx.x] : stk[(size_t)(d - kLdsDepth) * T];
+    };
 
     uint32_t sp = 0, pid = 0, sOff = 0;
     bool have = false, exhausted = false;
+    uint32_t qNext = 0, qEnd = 0, hNext = 0, hEnd = 0, filled = 0;  // wave-uniform
+    bool qDone = false;
     uint4 cur = make_uint4(0, 0, 0, 0);
     uint64_t cNodes = 0, cRank = 0, cLines = 0;
 
     for (;;) {
-        // ---- refill idle lanes from the item queue (one atomic per wave)
+        // ---- refill idle lanes from the wave's private item range; the wave
+        // takes kWorkChunk items per atomic on the global counter, so one
+        // counter word serves the whole grid without saturating
         const bool need = !have && sp == 0 && !exhausted;
-        const uint64_t nm = __ballot(need);
-        if (nm) {
-            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)nm) - 1u;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.work, (uint32_t)__popcll(nm));
-            base = __shfl(base, (int)leader);
-            if (need) {
-                const uint32_t item = base + (uint32_t)__popcll(nm & ltMask);
-                if (item < a.nitems) {
-                    pid = item / a.nsearch;
-                    sOff = (item - pid * a.nsearch) * a.m;
-                    cur = make_uint4(0u, 0u, a.n, 0u);
-                    have = true;
-                } else {
-                    exhausted = true;
-                }
+        uint64_t pending = __ballot(need);
+        while (pending) {  // wave-uniform
+            if (qNext >= qEnd) {
+                if (qDone) break;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(a.work, kWorkChunk);
+                base = __shfl(base, 0);
+                if (base >= a.nitems) { qDone = true; break; }
+                qNext = base;
+                qEnd = min(base + kWorkChunk, a.nitems);
             }
+            const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
+            const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
+            const bool mine = ((pending >> lane) & 1ull) && rank < take;
+            if (mine) {
+                const uint32_t item = qNext + rank;
+                pid = item / a.nsearch;
+                sOff = (item - pid * a.nsearch) * a.m;
+                cur = make_uint4(0u, 0u, a.n, 0u);
+                have = true;
+            }
+            pending &= ~__ballot(mine);
+            qNext += take;
         }
+        if (qDone && need && !have) exhausted = true;
         if (!have && sp > 0) {
             --sp;
-            cur = stk[(size_t)sp * T];
+            cur = spop(sp);
             have = true;
         }
         if (!__any(have)) break;
 
-        // ---- leaves -> hit buffer (ballot compaction, one atomic per wave)
+        // ---- leaves -> hit buffer: ballot + prefix compaction into the wave's
+        // reserved slot range; a new range of kHitChunk slots costs one atomic
         const uint32_t pos = cur.w & 0xFFFFu;
         const bool leaf = have && pos == a.m;
         const uint64_t lm = __ballot(leaf);
         if (lm) {
-            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)lm) - 1u;
+            const uint32_t cnt = (uint32_t)__popcll(lm);
+            const uint32_t rank = (uint32_t)__popcll(lm & ltMask);
+            const uint32_t avail = hEnd - hNext;
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.hitCount, (uint32_t)__popcll(lm));
-            base = __shfl(base, (int)leader);
+            if (cnt > avail) {
+                if (lane == 0) base = atomicAdd(a.hitCount, kHitChunk);
+                base = __shfl(base, 0);
+            }
             if (leaf) {
-                const uint32_t idx = base + (uint32_t)__popcll(lm & ltMask);
+                const uint32_t idx = rank < avail ? hNext + rank : base + (rank - avail);
                 if (idx < a.hitCap) a.hits[idx] = make_uint4(pid, cur.x, cur.z, (cur.w >> 16) & 0xFu);
                 else atomicOr(a.flags, 2u);
                 have = false;
             }
+            if (cnt > avail) { hNext = base + (cnt - avail); hEnd = base + kHitChunk; }
+            else hNext += cnt;
+            filled += cnt;
         }
+        // ---- decode the node (per lane)
+        uint32_t e = 0, lastL = 0, lastR = 0, cq = 0, lb = 0, ub = 0;
+        bool right = false, matchOK = false, misOK = false, delOK = false, insOK = false;
+        uint32_t lo = 0, hi = 0;
+        bool needA = false, needB = false;
+        if (have) {
+            e = (cur.w >> 16) & 0xFu;
+            lastL = (cur.w >> 20) & 3u;
+            lastR = (cur.w >> 22) & 3u;
+            const uint32_t se = sch[sOff + pos];
+            const uint32_t q = se & 0xFFFFu;
+            lb = (se >> 16) & 0xFu;
+            ub = (se >> 20) & 0xFu;
+            right = (se >> 24) & 1u;
+            cq = a.pats[(size_t)pid * a.m + q];
+            const uint32_t side = right ? lastR : lastL;
+            matchOK = lb <= e && e <= ub;
+            misOK = lb <= e + 1 && e + 1 <= ub;
+            delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
+            insOK = EDIT && misOK && side != OP_D;
+            lo = right ? cur.y : cur.x;
+            hi = lo + cur.z;
+            needA = matchOK || misOK || delOK;
+            needB = needA && (hi >> 6) != (lo >> 6);
+        }
+
+        // ---- pair-cooperative Occ line fetch (wave-uniform). Lanes 2i, 2i+1
+        // fetch each other's lines together: every load instruction touches
+        // at most 32 distinct 64-B lines (two lanes per line), which keeps
+        // address translation off the critical path on a multi-GB index
+        // (tools/gather_bench: 49.8 vs 21.7 Glines/s at 7 GB).
+        const uint64_t ownA = (uint64_t)(right ? a.occR : a.occF) + (uint64_t)(lo >> 6) * 64u;
+        const uint64_t ownB = (uint64_t)(right ? a.occR : a.occF) + (uint64_t)(hi >> 6) * 64u;
+        uint32_t ca[5], cb[5];
+        uint64_t pa[3], pb[3];
+        fetchLinePair(ownA, needA, odd, ca, pa);
+        fetchLinePair(ownB, needB, odd, cb, pb);
+
         if (have) {
         // ---- expand one node
-        const uint32_t e = (cur.w >> 16) & 0xFu;
-        const uint32_t lastL = (cur.w >> 20) & 3u, lastR = (cur.w >> 22) & 3u;
-        const uint32_t se = sch[sOff + pos];
-        const uint32_t q = se & 0xFFFFu, lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
-        const bool right = (se >> 24) & 1u;
-        const uint32_t cq = a.pats[(size_t)pid * a.m + q];
-        const uint32_t side = right ? lastR : lastL;
-        const bool matchOK = lb <= e && e <= ub;
-        const bool misOK = lb <= e + 1 && e + 1 <= ub;
-        const bool delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
-        const bool insOK = EDIT && misOK && side != OP_D;
         auto meta = [&](uint32_t npos, uint32_t ne, uint32_t op) -> uint32_t {
             const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
             const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
@@ -139,22 +237,13 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         uint32_t occ[SIGMA], nlo[SIGMA], noth[SIGMA];
 #pragma unroll
         for (int c = 0; c < SIGMA; ++c) occ[c] = nlo[c] = noth[c] = 0;
-        if (matchOK || misOK || delOK) {
-            const OccLine* L = right ? a.occR : a.occF;
-            const uint32_t lo = right ? cur.y : cur.x;
-            const uint32_t hi = lo + cur.z;
-            uint32_t ca[5], cb[5];
-            uint64_t pa[3], pb[3];
-            loadRankPart(L, lo >> 6, ca, pa);
-            const bool two = (hi >> 6) != (lo >> 6);
-            if (two) {
-                loadRankPart(L, hi >> 6, cb, pb);
-            } else {
+        if (needA) {
+            if (!needB) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) cb[i] = ca[i];
                 pb[0] = pa[0]; pb[1] = pa[1]; pb[2] = pa[2];
             }
-            if (COUNT) { ++cRank; cLines += two ? 2 : 1; }
+            if (COUNT) { ++cRank; cLines += needB ? 2 : 1; }
             const uint64_t ml = lowMask(lo & 63u), mh = lowMask(hi & 63u);
             uint32_t sum = 0;
 #pragma unroll
@@ -193,7 +282,7 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         uint4 next = make_uint4(0, 0, 0, 0);
         auto push = [&](const uint4& v) {
             if (sp < a.stackCap) {
-                stk[(size_t)sp * T] = v;
+                spush(sp, v);
                 ++sp;
             } else {
                 atomicOr(a.flags, 1u);
@@ -217,6 +306,10 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         cur = next;
         }  // have
     }
+    // unused tail of the wave's last slot range: empty cursors (len 0)
+    for (uint32_t i = hNext + lane; i < hEnd; i += 64)
+        if (i < a.hitCap) a.hits[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (lane == 0 && filled) atomicAdd(a.filled, filled);
     if (COUNT) {
         atomicAdd(a.counters + 0, (unsigned long long)cNodes);
         atomicAdd(a.counters + 1, (unsigned long long)cRank);
