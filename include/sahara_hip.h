@@ -72,6 +72,8 @@ typedef struct sahara_stats {
     uint64_t lf_steps;       /* LF steps in locate */
     uint32_t search_launches;
     uint32_t search_grid;    /* workgroups per search launch */
+    uint64_t text_nodes;     /* nodes expanded against the resident text (verify mode) */
+    uint64_t conversions;    /* singleton intervals resolved through the full SA */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);
@@ -93,8 +95,18 @@ int  sahara_gpu_index_info(void* ctx, sahara_index_info* info);
  * C array (sigma+1 u64) and record lengths (n_records u64). */
 int  sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* sampled_bits,
                        uint32_t* samples, uint64_t* C, uint64_t* rec_lens);
-/* Full suffix array of the last sahara_gpu_build (test hook; n u32). */
+/* Full suffix array and text (one symbol per byte, n entries) resident on the
+ * device: built with the index or densified from the .idx samples (test hooks). */
 int  sahara_gpu_export_sa(void* ctx, uint32_t* sa);
+int  sahara_gpu_export_text(void* ctx, uint8_t* text);
+/* Execution mode of the search (default verify = 1, locate_sa = 1):
+ *   verify    1: once a DFS node's interval is a single row, resolve its text
+ *             position through the resident SA and continue the identical DFS
+ *             against the resident text; 0: rank every node on the FM-index.
+ *   locate_sa 1: locate rows by one read of the resident SA; 0: LF walk to
+ *             the SA samples (fmc::LocateLinear, search.cpp:246).
+ * The multiset of hits is the same in every mode. */
+int  sahara_gpu_set_mode(void* ctx, int verify, int locate_sa);
 
 /* --- search + locate (replaces search.cpp:218-250) ---
  * pi/l/u: the expanded search scheme, n_searches rows of len entries each

@@ -53,7 +53,8 @@ class Stats(C.Structure):
                 ("hits", C.c_uint64), ("search_ms", C.c_double), ("locate_ms", C.c_double),
                 ("sort_ms", C.c_double), ("total_ms", C.c_double), ("nodes", C.c_uint64),
                 ("rank_nodes", C.c_uint64), ("ext_lines", C.c_uint64), ("lf_steps", C.c_uint64),
-                ("search_launches", C.c_uint32), ("search_grid", C.c_uint32)]
+                ("search_launches", C.c_uint32), ("search_grid", C.c_uint32),
+                ("text_nodes", C.c_uint64), ("conversions", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -71,6 +72,8 @@ EXPORTED = {
     "sahara_gpu_index_info": (C.c_int, [C.c_void_p, C.POINTER(IndexInfo)]),
     "sahara_gpu_export": (C.c_int, [C.c_void_p, u8p, u8p, u64p, u32p, u64p, u64p]),
     "sahara_gpu_export_sa": (C.c_int, [C.c_void_p, u32p]),
+    "sahara_gpu_export_text": (C.c_int, [C.c_void_p, u8p]),
+    "sahara_gpu_set_mode": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "sahara_gpu_search": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                     C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_uint64)]),
@@ -206,6 +209,17 @@ class BiFMIndex:
         sa = np.zeros(n, np.uint32)
         _check(lib().sahara_gpu_export_sa(self._h, _p(sa, u32p)))
         return sa
+
+    def export_text(self):
+        n = self.info()["n"]
+        t = np.zeros(n, np.uint8)
+        _check(lib().sahara_gpu_export_text(self._h, _p(t, u8p)))
+        return t
+
+    def set_mode(self, verify=True, locate_sa=True):
+        """verify: continue singleton intervals against the resident text;
+        locate_sa: locate through the resident full SA (else LF walks)."""
+        _check(lib().sahara_gpu_set_mode(self._h, int(verify), int(locate_sa)))
 
     # ---- device-resident path (bench) ----
     def stage(self, queries, scheme, edit=True):

@@ -44,6 +44,8 @@ struct Ctx {
     uint32_t maxErr = 0;
     bool edit = true;
     bool staged = false;
+    bool verify = true;
+    bool locateSA = true;
 
     // work buffers
     DevBuf<uint4> stack, hits;
@@ -94,6 +96,7 @@ Ctx* newCtx(int device) {
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
     c->small.reserve(4);
     c->counters.reserve(8);
+    SH_HIP(hipMemset(c->counters.ptr, 0, 8 * sizeof(unsigned long long)));
     return c.release();
 }
 
@@ -207,6 +210,9 @@ void run(Ctx* c, bool count) {
             a.hits = c->hits.ptr;
             a.hitCap = c->hitCap;
             a.counters = c->counters.ptr;
+            a.sa = c->I.saFull.ptr;
+            a.text4 = c->I.text4.ptr;
+            a.verify = c->verify ? 1u : 0u;
             SH_HIP(hipEventRecord(c->ev[0], c->st));
             launchSearch(a, sigma, c->edit, count, blocks, lds, c->st);
             SH_HIP(hipEventRecord(c->ev[1], c->st));
@@ -253,6 +259,8 @@ void run(Ctx* c, bool count) {
         la.keys = c->k0.ptr;
         la.flags = c->small.ptr + 2;
         la.counters = c->counters.ptr + 3;
+        la.sa = c->I.saFull.ptr;
+        la.useSA = c->locateSA ? 1u : 0u;
         launchLocate(la, count, c->st);
         SH_HIP(hipEventRecord(c->ev[3], c->st));
         unsigned endBit = 36;
@@ -284,13 +292,15 @@ void run(Ctx* c, bool count) {
         S.hits += rows;
     }
     if (count) {
-        unsigned long long h[4];
+        unsigned long long h[8];
         SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, c->st));
         SH_HIP(hipStreamSynchronize(c->st));
         S.nodes = h[0];
         S.rank_nodes = h[1];
         S.ext_lines = h[2];
         S.lf_steps = h[3];
+        S.text_nodes = h[5];
+        S.conversions = h[6];
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->stats = S;
@@ -312,7 +322,7 @@ int sahara_gpu_build(int device, const uint8_t* ranks, const uint64_t* rec_lens,
                      uint32_t sampling_rate, void** ctx) {
     return guarded([&] {
         std::unique_ptr<Ctx> c(newCtx(device));
-        buildFromText(c->I, ranks, rec_lens, n_records, sigma, sampling_rate, true, c->st);
+        buildFromText(c->I, ranks, rec_lens, n_records, sigma, sampling_rate, c->st);
         *ctx = c.release();
     });
 }
@@ -363,8 +373,24 @@ int sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* sampl
 int sahara_gpu_export_sa(void* ctx, uint32_t* sa) {
     return guarded([&] {
         Ctx* c = ctxOf(ctx);
-        if (!c->I.sa.ptr) throw Error("suffix array not kept (only available after sahara_gpu_build)");
-        SH_HIP(hipMemcpy(sa, c->I.sa.ptr, c->I.n * 4, hipMemcpyDeviceToHost));
+        SH_HIP(hipMemcpy(sa, c->I.saFull.ptr, c->I.n * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+int sahara_gpu_export_text(void* ctx, uint8_t* text) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        std::vector<uint8_t> t4((c->I.n + 1) / 2);
+        SH_HIP(hipMemcpy(t4.data(), c->I.text4.ptr, t4.size(), hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < c->I.n; ++i) text[i] = (t4[i >> 1] >> ((i & 1) * 4)) & 15;
+    });
+}
+
+int sahara_gpu_set_mode(void* ctx, int verify, int locate_sa) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        c->verify = verify != 0;
+        c->locateSA = locate_sa != 0;
     });
 }
 

@@ -56,15 +56,18 @@ struct DeviceIndex {
     DevBuf<uint32_t> samples;       // text position per sampled row, row order
     uint64_t nsamples = 0;
     DevBuf<uint64_t> dRecStarts;
-    DevBuf<uint32_t> sa;            // kept only when requested (test export)
+    // Resident for the search (HBM is 288 GB; at 3 Gbp these are 12 + 1.5 GB):
+    DevBuf<uint32_t> saFull;        // SA[row] for every row: locate = one read
+    DevBuf<uint8_t> text4;          // text, 4 bits per symbol (two per byte), '$' = 0
     uint64_t deviceBytes() const {
-        return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8;
+        return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8 + saFull.cap * 4 +
+               text4.cap;
     }
 };
 
 // index_build.hip
 void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec,
-                   uint32_t sigma, uint32_t rate, bool keepSA, hipStream_t st);
+                   uint32_t sigma, uint32_t rate, hipStream_t st);
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec,
                     uint32_t rate, const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits,
                     const uint32_t* samples, uint64_t nsamples, hipStream_t st);

@@ -50,13 +50,22 @@ SH_HD uint32_t symAt(const uint64_t p[3], uint32_t off) {
 }
 
 // Node of the search-scheme DFS, packed in 16 bytes (uint4 on device):
-//   x = lb (forward SA interval), y = lbRev (reverse SA interval), z = len,
-//   w = pos | e << 16 | lastL << 20 | lastR << 22
+//   FM node:   x = lb (forward SA interval), y = lbRev (reverse), z = len
+//   text node: x = first text position of the matched string t, y = one past
+//              its last, z = 1 (a singleton interval resolved through SA)
+//   w = pos | e << 16 | lastL << 20 | lastR << 22 | text << 24 | (|t| - pos + 16) << 25
+// |t| - pos = #D - #I on the path, in [-15, 15].
 enum : uint32_t { OP_NONE = 0, OP_MS = 1, OP_I = 2, OP_D = 3 };
+constexpr uint32_t kTextBit = 1u << 24;
+constexpr uint32_t kDeltaZero = 16u << 25;
 
 SH_HD uint32_t packMeta(uint32_t pos, uint32_t e, uint32_t lastL, uint32_t lastR) {
-    return pos | (e << 16) | (lastL << 20) | (lastR << 22);
+    return pos | (e << 16) | (lastL << 20) | (lastR << 22) | kDeltaZero;
 }
+SH_HD uint32_t metaDelta(uint32_t w) { return w >> 25; }  // |t| - pos + 16
+
+// Hit record flag: the cursor is already a text position (x), len 1.
+constexpr uint32_t kPosKnown = 1u << 31;
 
 // One expanded scheme position, packed in a u32 for LDS:
 //   pi (16 bits) | l << 16 (4) | u << 20 (4) | dirRight << 24

@@ -221,6 +221,60 @@ __global__ void kSampledWords(const OccLine* __restrict__ lines, uint64_t nb, ui
         w[b] = lines[b].sampled;
 }
 
+
+// text bytes (one symbol per byte) -> 4-bit packed, two symbols per byte
+__global__ void kPackText(const uint8_t* __restrict__ T, uint64_t N, uint8_t* __restrict__ t4) {
+    const uint64_t nb = (N + 1) / 2;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nb;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t a = T[2 * i];
+        const uint8_t b = (2 * i + 1 < N) ? T[2 * i + 1] : 0;
+        t4[i] = (uint8_t)(a | (b << 4));
+    }
+}
+
+__device__ __forceinline__ uint32_t rankAll(const OccLine& L, uint32_t row, uint32_t c) {
+    // occurrences of symbol c in BWT[0, row); '$' (c = 0) by complement
+    const uint32_t o = row & 63u;
+    const uint64_t m = lowMask(o);
+    if (c != 0) return L.cnt[c - 1] + (uint32_t)__popcll(symMask(L.plane, c) & m);
+    uint32_t others = 0;
+#pragma unroll
+    for (uint32_t s = 1; s <= 5; ++s) others += L.cnt[s - 1] + (uint32_t)__popcll(symMask(L.plane, s) & m);
+    return row - others;
+}
+
+// Densify the sampled SA to the full SA and recover the text from the BWT:
+// every sampled row (and row 0, the suffix "$" at n-1) seeds a backward LF
+// walk that stops at the next sampled row, writing SA[row] = pos and
+// T[pos-1] = BWT[row] on the way. Each row is visited by exactly one walk.
+__global__ void kDensify(const OccLine* __restrict__ occ, uint64_t N, const uint32_t* __restrict__ samples,
+                         const uint64_t* __restrict__ C, uint32_t rate, uint32_t* __restrict__ sa,
+                         uint8_t* __restrict__ T, unsigned int* __restrict__ err) {
+    for (uint64_t r0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r0 < N;
+         r0 += (uint64_t)gridDim.x * blockDim.x) {
+        const OccLine& L0 = occ[r0 >> 6];
+        const uint32_t o0 = (uint32_t)(r0 & 63);
+        const bool sampled = (L0.sampled >> o0) & 1ull;
+        if (!sampled && r0 != 0) continue;
+        uint64_t pos = sampled ? samples[L0.srank + __popcll(L0.sampled & lowMask(o0))] : N - 1;
+        uint32_t row = (uint32_t)r0;
+        sa[row] = (uint32_t)pos;
+        for (uint32_t step = 0;; ++step) {
+            if (step > 2 * rate + 2) { atomicOr(err, 1u); break; }
+            const OccLine& L = occ[row >> 6];
+            const uint32_t c = symAt(L.plane, row & 63u);
+            if (pos == 0) break;
+            T[pos - 1] = (uint8_t)c;
+            row = (uint32_t)C[c] + rankAll(L, row, c);
+            --pos;
+            const OccLine& L2 = occ[row >> 6];
+            if ((L2.sampled >> (row & 63u)) & 1ull) break;
+            sa[row] = (uint32_t)pos;
+        }
+    }
+}
+
 // Builds the suffix array of the device text T[0, N) into `sa`.
 void suffixArray(const uint8_t* dT, uint64_t N, uint32_t* dSA, hipStream_t st) {
     DevBuf<uint64_t> k0, k1;
@@ -321,7 +375,7 @@ void setC(DeviceIndex& I, const uint64_t totals[6], uint64_t nrec) {
 }  // namespace
 
 void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma,
-                   uint32_t rate, bool keepSA, hipStream_t st) {
+                   uint32_t rate, hipStream_t st) {
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
     if (nrec == 0) throw Error("reference is empty");
     if (rate == 0) throw Error("sampling rate must be > 0");
@@ -369,10 +423,13 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
     I.samples.reserve(std::max<uint64_t>(I.nsamples, 1));
     hipLaunchKernelGGL(kSamples, dim3(grid), dim3(kTB), 0, st, sa.ptr, N, I.occF.ptr, I.samples.ptr);
     SH_HIP(hipGetLastError());
-    if (keepSA) {
-        I.sa.reserve(N);
-        SH_HIP(hipMemcpyAsync(I.sa.ptr, sa.ptr, N * 4, hipMemcpyDeviceToDevice, st));
-    }
+    // resident full SA + packed text for the search (locate = one read)
+    I.saFull.reserve(N);
+    SH_HIP(hipMemcpyAsync(I.saFull.ptr, sa.ptr, N * 4, hipMemcpyDeviceToDevice, st));
+    I.text4.reserve((N + 1) / 2 + 64);
+    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (N + 1) / 2 + 64, st));
+    hipLaunchKernelGGL(kPackText, dim3(gridFor((N + 1) / 2)), dim3(kTB), 0, st, T.ptr, N, I.text4.ptr);
+    SH_HIP(hipGetLastError());
 
     // reverse direction: SA, BWT, lines (no sampling)
     suffixArray(R.ptr, N, sa.ptr, st);
@@ -409,7 +466,26 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     buildLines(bwt.ptr, n, nullptr, I.occR, totalsR, st);
     for (int c = 0; c < 5; ++c)
         if (totalsR[c] != totals[c]) throw Error("forward/reverse BWT symbol counts differ");
+    // full SA + text from the sampled SA by bounded LF walks
+    I.saFull.reserve(n);
+    DevBuf<uint64_t> dC;
+    dC.reserve(8);
+    SH_HIP(hipMemcpyAsync(dC.ptr, I.C, 8 * 8, hipMemcpyHostToDevice, st));
+    DevBuf<unsigned int> err;
+    err.reserve(1);
+    SH_HIP(hipMemsetAsync(err.ptr, 0, 4, st));
+    SH_HIP(hipMemsetAsync(bwt.ptr, 0, n + 64, st));  // reused as the unpacked text
+    hipLaunchKernelGGL(kDensify, dim3(gridFor(n)), dim3(kTB), 0, st, I.occF.ptr, n, I.samples.ptr, dC.ptr, rate,
+                       I.saFull.ptr, bwt.ptr, err.ptr);
+    SH_HIP(hipGetLastError());
+    I.text4.reserve((n + 1) / 2 + 64);
+    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (n + 1) / 2 + 64, st));
+    hipLaunchKernelGGL(kPackText, dim3(gridFor((n + 1) / 2)), dim3(kTB), 0, st, bwt.ptr, n, I.text4.ptr);
+    SH_HIP(hipGetLastError());
+    unsigned int herr = 0;
+    SH_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, st));
     SH_HIP(hipStreamSynchronize(st));
+    if (herr) throw Error("SA densification walk exceeded its bound (inconsistent .idx samples)");
 }
 
 void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits, uint32_t* samples,

@@ -27,7 +27,10 @@ struct SearchArgs {
     uint32_t* hitCount;      // reserved slots (waves reserve ranges; unused slots have len 0)
     uint32_t* filled;        // cursors actually written
     uint32_t* flags;         // 1 = stack overflow, 2 = hit-buffer overflow, 4 = corrupt locate
-    unsigned long long* counters;  // nodes, rank nodes, lines
+    unsigned long long* counters;  // nodes, rank nodes, lines, -, -, text nodes, conversions
+    const uint32_t* sa;      // full SA (text mode / verify)
+    const uint8_t* text4;    // 4-bit packed text
+    uint32_t verify;         // 1: continue singleton intervals against the text
 };
 
 struct LocateArgs {
@@ -41,6 +44,8 @@ struct LocateArgs {
     uint64_t* keys;
     uint32_t* flags;
     unsigned long long* counters;  // lf steps
+    const uint32_t* sa;            // full SA: locate = one read (when useSA)
+    uint32_t useSA;
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);

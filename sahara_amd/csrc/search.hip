@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
     uint32_t qNext = 0, qEnd = 0, hNext = 0, hEnd = 0, filled = 0;  // wave-uniform
     bool qDone = false;
     uint4 cur = make_uint4(0, 0, 0, 0);
-    uint64_t cNodes = 0, cRank = 0, cLines = 0;
+    uint64_t cNodes = 0, cRank = 0, cLines = 0, cText = 0, cConv = 0;
 
     for (;;) {
         // ---- refill idle lanes from the wave's private item range; the wave
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
                 const uint32_t item = qNext + rank;
                 pid = item / a.nsearch;
                 sOff = (item - pid * a.nsearch) * a.m;
-                cur = make_uint4(0u, 0u, a.n, 0u);
+                cur = make_uint4(0u, 0u, a.n, kDeltaZero);
                 have = true;
             }
             pending &= ~__ballot(mine);
@@ -179,7 +179,9 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
             }
             if (leaf) {
                 const uint32_t idx = rank < avail ? hNext + rank : base + (rank - avail);
-                if (idx < a.hitCap) a.hits[idx] = make_uint4(pid, cur.x, cur.z, (cur.w >> 16) & 0xFu);
+                const bool known = (cur.w & kTextBit) != 0;
+                if (idx < a.hitCap)
+                    a.hits[idx] = make_uint4(pid, cur.x, known ? 1u : cur.z, ((cur.w >> 16) & 0xFu) | (known ? kPosKnown : 0u));
                 else atomicOr(a.flags, 2u);
                 have = false;
             }
@@ -189,8 +191,8 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         }
         // ---- decode the node (per lane)
         uint32_t e = 0, lastL = 0, lastR = 0, cq = 0, lb = 0, ub = 0;
-        bool right = false, matchOK = false, misOK = false, delOK = false, insOK = false;
-        uint32_t lo = 0, hi = 0;
+        bool right = false, matchOK = false, misOK = false, delOK = false, insOK = false, text = false;
+        uint32_t lo = 0, hi = 0, tc = 0;
         bool needA = false, needB = false;
         if (have) {
             e = (cur.w >> 16) & 0xFu;
@@ -207,10 +209,26 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
             misOK = lb <= e + 1 && e + 1 <= ub;
             delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
             insOK = EDIT && misOK && side != OP_D;
-            lo = right ? cur.y : cur.x;
-            hi = lo + cur.z;
-            needA = matchOK || misOK || delOK;
-            needB = needA && (hi >> 6) != (lo >> 6);
+            text = (cur.w & kTextBit) != 0;
+            if (!text && a.verify && cur.z == 1u) {
+                // singleton interval: resolve its text position once (full SA)
+                // and continue the same DFS against the resident text
+                const uint32_t p = a.sa[cur.x];
+                const uint32_t tlen = pos + metaDelta(cur.w) - 16u;
+                cur = make_uint4(p, p + tlen, 1u, cur.w | kTextBit);
+                text = true;
+                if (COUNT) ++cConv;
+            }
+            if (text) {
+                const uint32_t tp = right ? cur.y : cur.x - 1u;  // next text symbol
+                const bool inside = right ? (cur.y < a.n) : (cur.x > 0u);
+                if (inside && (matchOK || misOK || delOK)) tc = (a.text4[tp >> 1] >> ((tp & 1u) * 4u)) & 0xFu;
+            } else {
+                lo = right ? cur.y : cur.x;
+                hi = lo + cur.z;
+                needA = matchOK || misOK || delOK;
+                needB = needA && (hi >> 6) != (lo >> 6);
+            }
         }
 
         // ---- pair-cooperative Occ line fetch (wave-uniform). Lanes 2i, 2i+1
@@ -227,17 +245,31 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
 
         if (have) {
         // ---- expand one node
+        const uint32_t dl = metaDelta(cur.w);
         auto meta = [&](uint32_t npos, uint32_t ne, uint32_t op) -> uint32_t {
             const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
             const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
-            return packMeta(npos, ne, nl, nr);
+            const uint32_t nd = dl + (op == OP_D ? 1u : 0u) - (op == OP_I ? 1u : 0u);
+            return npos | (ne << 16) | (nl << 20) | (nr << 22) | (cur.w & kTextBit) | (nd << 25);
         };
         if (COUNT) ++cNodes;
 
-        uint32_t occ[SIGMA], nlo[SIGMA], noth[SIGMA];
+        // child c = (fx[c], fy[c], occ[c]): forward / reverse lower bounds of an
+        // FM child, or the [start, end) text span of a text child
+        uint32_t occ[SIGMA], fx[SIGMA], fy[SIGMA];
 #pragma unroll
-        for (int c = 0; c < SIGMA; ++c) occ[c] = nlo[c] = noth[c] = 0;
-        if (needA) {
+        for (int c = 0; c < SIGMA; ++c) occ[c] = fx[c] = fy[c] = 0;
+        if (text) {
+            // the only symbol that can extend a singleton is the text's own
+            if (COUNT) ++cText;
+            const uint32_t ns = right ? cur.x : cur.x - 1u, ne = right ? cur.y + 1u : cur.y;
+#pragma unroll
+            for (int c = 1; c < SIGMA; ++c) {  // branch-free: keeps the arrays in registers
+                occ[c] = (uint32_t)c == tc ? 1u : 0u;
+                fx[c] = ns;
+                fy[c] = ne;
+            }
+        } else if (needA) {
             if (!needB) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) cb[i] = ca[i];
@@ -245,23 +277,28 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
             }
             if (COUNT) { ++cRank; cLines += needB ? 2 : 1; }
             const uint64_t ml = lowMask(lo & 63u), mh = lowMask(hi & 63u);
-            uint32_t sum = 0;
+            uint32_t sum = 0, base[SIGMA];
 #pragma unroll
             for (int c = 1; c < SIGMA; ++c) {
                 const uint32_t rl = ca[c - 1] + (uint32_t)__popcll(symMask(pa, c) & ml);
                 const uint32_t rh = cb[c - 1] + (uint32_t)__popcll(symMask(pb, c) & mh);
                 occ[c] = rh - rl;
-                nlo[c] = a.C[c] + rl;
+                base[c] = a.C[c] + rl;
                 sum += occ[c];
             }
+            // bidirectional update: the other side moves by the occurrences of
+            // the smaller symbols, '$' first
             uint32_t acc = (right ? cur.x : cur.y) + (cur.z - sum);
 #pragma unroll
-            for (int c = 1; c < SIGMA; ++c) { noth[c] = acc; acc += occ[c]; }
+            for (int c = 1; c < SIGMA; ++c) {
+                fx[c] = right ? acc : base[c];
+                fy[c] = right ? base[c] : acc;
+                acc += occ[c];
+            }
         }
         auto child = [&](int c, uint32_t m) -> uint4 {
-            return right ? make_uint4(noth[c], nlo[c], occ[c], m) : make_uint4(nlo[c], noth[c], occ[c], m);
+            return make_uint4(fx[c], fy[c], occ[c], m);
         };
-
         // count error children; find the match child
         uint32_t nErr = insOK ? 1u : 0u;
         bool hasM = false;
@@ -314,6 +351,8 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         atomicAdd(a.counters + 0, (unsigned long long)cNodes);
         atomicAdd(a.counters + 1, (unsigned long long)cRank);
         atomicAdd(a.counters + 2, (unsigned long long)cLines);
+        atomicAdd(a.counters + 5, (unsigned long long)cText);
+        atomicAdd(a.counters + 6, (unsigned long long)cConv);
     }
 }
 
@@ -325,6 +364,16 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
          h += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 hit = a.hits[h];
         const uint64_t out = a.rowOff[h];
+        const uint64_t e = hit.w & 0xFu;
+        if (hit.w & kPosKnown) {  // resolved during the search (text mode)
+            a.keys[out] = ((uint64_t)hit.x << 36) | ((uint64_t)hit.y << 4) | e;
+            continue;
+        }
+        if (a.useSA) {  // full SA resident: one read per row
+            for (uint32_t j = 0; j < hit.z; ++j)
+                a.keys[out + j] = ((uint64_t)hit.x << 36) | ((uint64_t)a.sa[hit.y + j] << 4) | e;
+            continue;
+        }
         for (uint32_t j = 0; j < hit.z; ++j) {
             uint32_t row = hit.y + j;
             uint32_t st = 0;
@@ -352,7 +401,7 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
                 ++st;
             }
             if (COUNT) steps += st;
-            a.keys[out + j] = ((uint64_t)hit.x << 36) | (gpos << 4) | (uint64_t)hit.w;
+            a.keys[out + j] = ((uint64_t)hit.x << 36) | (gpos << 4) | e;
         }
     }
     if (COUNT && steps) atomicAdd(a.counters, (unsigned long long)steps);

@@ -31,6 +31,8 @@ def test_gpu_index_equals_oracle(gpu_device, sigma, shape):
     a = ref.export()
     b = gpu.export()
     assert np.array_equal(gpu.export_sa(), a["sa"])
+    text = np.concatenate([np.append(np.asarray(r, np.uint8), 0) for r in recs])
+    assert np.array_equal(gpu.export_text(), text)
     for key in ("bwt_f", "bwt_r", "sampled", "samples"):
         assert np.array_equal(a[key], b[key]), key
     assert np.array_equal(a["C"][: sigma + 1], b["C"])
@@ -52,6 +54,9 @@ CASES = [  # sigma, edit, k, m, gen, with_n, repeats
 ]
 
 
+MODES = [(True, True), (False, False), (True, False), (False, True)]  # (verify, locate_sa)
+
+
 @pytest.mark.parametrize("sigma,edit,k,m,gen,with_n,repeats", CASES)
 def test_gpu_search_multiset_equals_oracle(gpu_device, sigma, edit, k, m, gen, with_n, repeats):
     rng = np.random.default_rng(7 * k + m + sigma + (1 if edit else 0))
@@ -62,13 +67,15 @@ def test_gpu_search_multiset_equals_oracle(gpu_device, sigma, edit, k, m, gen, w
     ref = O.Index.build(recs, sigma, 16)
     want, _ = ref.search(pats, scheme, edit=edit, nthreads=8)
     gpu = sa.BiFMIndex.build(recs, sigma=sigma, device=gpu_device)
-    got = sa.search(gpu, pats, scheme, edit=edit)
-    assert len(got) == len(want)
-    # canonical order out of the ABI
-    rows = hits_as_rows(got)
-    raw = np.stack([got["qid"], got["seq_id"], got["pos"], got["err"]], 1).astype(np.uint64)
-    assert np.array_equal(rows, raw)
-    assert np.array_equal(rows, hits_as_rows(want))
+    for verify, locate_sa in MODES:
+        gpu.set_mode(verify=verify, locate_sa=locate_sa)
+        got = sa.search(gpu, pats, scheme, edit=edit)
+        assert len(got) == len(want), (verify, locate_sa)
+        # canonical order out of the ABI
+        rows = hits_as_rows(got)
+        raw = np.stack([got["qid"], got["seq_id"], got["pos"], got["err"]], 1).astype(np.uint64)
+        assert np.array_equal(rows, raw)
+        assert np.array_equal(rows, hits_as_rows(want)), (verify, locate_sa)
 
 
 def test_gpu_pset_equals_bruteforce(gpu_device):
@@ -89,6 +96,10 @@ def test_idx_files_cross_load(gpu_device, tmp_path):
     p1 = tmp_path / "oracle.idx"
     ref.write(p1)
     g1 = sa.BiFMIndex.load(p1, device=gpu_device)          # oracle-written -> GPU
+    # full SA and text densified from the rate-16 samples on load
+    assert np.array_equal(g1.export_sa(), ref.export()["sa"])
+    text = np.concatenate([np.append(np.asarray(r, np.uint8), 0) for r in recs])
+    assert np.array_equal(g1.export_text(), text)
     g2 = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
     p2 = tmp_path / "gpu.idx"
     g2.save(p2)
@@ -102,7 +113,9 @@ def test_idx_files_cross_load(gpu_device, tmp_path):
     sch = sa.search_scheme("h2-k2", 0, 2, 30)
     want = hits_as_rows(ref.search(reads, sch)[0])
     for g in (g1, g2, g3):
-        assert np.array_equal(hits_as_rows(sa.search(g, reads, sch)), want)
+        for verify, locate_sa in MODES:
+            g.set_mode(verify, locate_sa)
+            assert np.array_equal(hits_as_rows(sa.search(g, reads, sch)), want)
 
 
 def test_hit_buffer_overflow_reruns(gpu_device, monkeypatch):
@@ -126,6 +139,7 @@ def test_no_hits_and_device_resident_path(gpu_device):
     junk = np.array(rng.integers(1, 4, size=(10, 40)), np.uint8)  # random 40-mers: absent from 5 kbp
     assert len(sa.search(gpu, junk, sch)) == 0
     reads = mutate_reads(rng, recs, 100, 40, 1)
+    gpu.set_mode(verify=False, locate_sa=False)  # the reference's own work: FM ranks + LF walks
     direct = sa.search(gpu, reads, sch)
     gpu.stage(reads, sch, edit=True)
     n = gpu.run(count=True)
@@ -143,6 +157,12 @@ def test_no_hits_and_device_resident_path(gpu_device):
     assert st["ext_lines"] == cnt["ext_lines"]
     assert st["lf_steps"] == cnt["lf_steps"]
     assert st["cursors"] == cnt["leaves"]
+    # verify mode: fewer rank nodes, same hits
+    gpu.set_mode(verify=True, locate_sa=True)
+    gpu.run(count=True)
+    st2 = gpu.stats()
+    assert st2["rank_nodes"] < st["rank_nodes"] and st2["conversions"] > 0
+    assert np.array_equal(gpu.fetch(), direct)
 
 
 def test_errors_are_loud(gpu_device):
@@ -165,6 +185,8 @@ def test_medium_scale_parity(gpu_device, k, m, nreads, ref_len):
     sch = sa.search_scheme("h2-k2", 0, k, m)
     gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
     got = sa.search(gpu, pats, sch)
+    gpu.set_mode(verify=False, locate_sa=False)
+    assert np.array_equal(sa.search(gpu, pats, sch), got)
     ex = gpu.export()
     ref = O.Index.from_parts(6, ex["n"], lens, 16, ex["bwt_f"], ex["bwt_r"], ex["sampled"], ex["samples"])
     want, _ = ref.search(pats, sch, edit=True, nthreads=8)
