@@ -164,7 +164,9 @@ static Index* build(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec
     for (uint64_t i = 0; i < n; ++i) {
         uint64_t p = I->sa[i];
         uint64_t r = (uint64_t)(std::upper_bound(starts.begin(), starts.end(), p) - starts.begin()) - 1;
-        if ((p - starts[r]) % rate == 0) {
+        // sampled: in-record offsets that are multiples of the rate, and every
+        // delimiter (so no LF walk ever has to step through a '$')
+        if ((p - starts[r]) % rate == 0 || p - starts[r] == recLens[r]) {
             I->sampled[i >> 6] |= 1ull << (i & 63);
             I->samples.push_back((uint32_t)p);
         }

@@ -11,8 +11,10 @@
 // with rocPRIM's onesweep radix sort (u64 keys, u32 suffix ids), until every
 // rank group is a singleton. Random text finishes after 2 sorts at 3 Gbp.
 // Sampling: row i is sampled iff the position of
-// SA[i] inside its record is a multiple of the rate, so every record start
-// is sampled and LF walks never cross a delimiter.
+// SA[i] inside its record is a multiple of the rate or is the record's
+// delimiter. Record starts and delimiters are therefore sampled and no LF
+// walk (locate, densification) ever steps through a '$' — where LF is not
+// order-preserving for a text with several delimiters.
 
 #include <hip/hip_runtime.h>
 
@@ -122,7 +124,9 @@ __global__ void kSampledBits(const uint32_t* __restrict__ sa, uint64_t N, const 
             if (i >= N) break;
             const uint64_t p = sa[i];
             const uint32_t r = recordOf(starts, nrec, p);
-            if ((p - starts[r]) % rate == 0) w |= 1ull << j;
+            const uint64_t off = p - starts[r];
+            const uint64_t len = (r + 1 < nrec ? starts[r + 1] : N) - starts[r] - 1;
+            if (off % rate == 0 || off == len) w |= 1ull << j;  // delimiters always sampled
         }
         bits[b] = w;
     }
@@ -245,9 +249,9 @@ __device__ __forceinline__ uint32_t rankAll(const OccLine& L, uint32_t row, uint
 }
 
 // Densify the sampled SA to the full SA and recover the text from the BWT:
-// every sampled row (and row 0, the suffix "$" at n-1) seeds a backward LF
-// walk that stops at the next sampled row, writing SA[row] = pos and
-// T[pos-1] = BWT[row] on the way. Each row is visited by exactly one walk.
+// every sampled row seeds a backward LF walk that stops at the next sampled
+// row or at a record start, writing SA[row] = pos and T[pos-1] = BWT[row] on
+// the way ('$' entries of T stay 0). Each row is visited by exactly one walk.
 __global__ void kDensify(const OccLine* __restrict__ occ, uint64_t N, const uint32_t* __restrict__ samples,
                          const uint64_t* __restrict__ C, uint32_t rate, uint32_t* __restrict__ sa,
                          uint8_t* __restrict__ T, unsigned int* __restrict__ err) {
@@ -256,15 +260,15 @@ __global__ void kDensify(const OccLine* __restrict__ occ, uint64_t N, const uint
         const OccLine& L0 = occ[r0 >> 6];
         const uint32_t o0 = (uint32_t)(r0 & 63);
         const bool sampled = (L0.sampled >> o0) & 1ull;
-        if (!sampled && r0 != 0) continue;
-        uint64_t pos = sampled ? samples[L0.srank + __popcll(L0.sampled & lowMask(o0))] : N - 1;
+        if (!sampled) continue;
+        uint64_t pos = samples[L0.srank + __popcll(L0.sampled & lowMask(o0))];
         uint32_t row = (uint32_t)r0;
         sa[row] = (uint32_t)pos;
         for (uint32_t step = 0;; ++step) {
-            if (step > 2 * rate + 2) { atomicOr(err, 1u); break; }
+            if (step > rate) { atomicOr(err, 1u); break; }
             const OccLine& L = occ[row >> 6];
             const uint32_t c = symAt(L.plane, row & 63u);
-            if (pos == 0) break;
+            if (pos == 0 || c == 0) break;  // record start: the '$' before it is sampled
             T[pos - 1] = (uint8_t)c;
             row = (uint32_t)C[c] + rankAll(L, row, c);
             --pos;

@@ -41,12 +41,12 @@ def test_suffix_array_bwt_and_samples(sigma):
     # C array
     for c in range(sigma + 1):
         assert ex["C"][c] == sum(1 for x in T if x < c)
-    # samples: rows whose in-record offset is a multiple of the rate
+    # samples: rows whose in-record offset is a multiple of the rate, and delimiters
     starts = np.cumsum([0] + [len(r) + 1 for r in recs])[:-1]
     exp = []
     for row, p in enumerate(sa):
         rid = np.searchsorted(starts, p, side="right") - 1
-        if (p - starts[rid]) % 4 == 0:
+        if (p - starts[rid]) % 4 == 0 or p - starts[rid] == len(recs[rid]):
             exp.append(p)
             assert (int(ex["sampled"][row // 64]) >> (row % 64)) & 1
     assert ex["samples"].tolist() == exp
