@@ -141,12 +141,13 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    search_ms = locate_ms = sort_ms = 0.0
+    search_ms = text_ms = locate_ms = sort_ms = 0.0
     launches = 0
     for i in range(args.steps):
         nh = idx.run()
         st = idx.stats()
         search_ms += st["search_ms"]
+        text_ms += st["text_ms"]
         locate_ms += st["locate_ms"]
         sort_ms += st["sort_ms"]
         launches += st["search_launches"]
@@ -185,8 +186,12 @@ def main():
         extra = {"bytes_per_read": round((search_bytes + locate_bytes) / nreads, 1),
                  "nodes_per_read": round(cnt["nodes"] / nreads, 1),
                  "ext_lines_per_read": round(cnt["ext_lines"] / nreads, 1),
+                 "rank_nodes_per_read": round(cnt["rank_nodes"] / nreads, 1),
+                 "text_nodes_per_read": round(cnt["text_nodes"] / nreads, 1),
+                 "conversions_per_read": round(cnt["conversions"] / nreads, 2),
                  "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
-                 "search_ms": round(search_ms_step, 2), "locate_ms": round(locate_ms / args.steps, 2),
+                 "search_ms": round(search_ms_step, 2), "text_ms": round(text_ms / args.steps, 2),
+                 "locate_ms": round(locate_ms / args.steps, 2),
                  "sort_ms": round(sort_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
                  "search_grid": cnt["search_grid"],
                  "locate_achieved_GBs": round(locate_bytes / (locate_ms / args.steps / 1e3) / 1e9, 1)

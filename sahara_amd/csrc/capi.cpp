@@ -36,28 +36,29 @@ struct Ctx {
     DeviceIndex I;
 
     // staged inputs
-    DevBuf<uint8_t> pats;
+    DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern
     uint64_t npat = 0;
-    uint32_t m = 0;
-    DevBuf<uint32_t> scheme;
+    uint32_t m = 0, patWords = 0;
+    DevBuf<uint32_t> scheme, cover;
     uint32_t nsearch = 0;
     uint32_t maxErr = 0;
     bool edit = true;
     bool staged = false;
     bool verify = true;
     bool locateSA = true;
+    uint32_t split = 4;                   // text-phase threshold (rows per interval)
 
     // work buffers
-    DevBuf<uint4> stack, hits;
-    DevBuf<uint32_t> small;               // work, hitCount, flags
-    DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest
+    DevBuf<uint4> stack, hits, tasks;
+    DevBuf<uint32_t> small;               // work, hitCount, flags, filled, taskCount, textWork
+    DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> rowOff, k0, k1;
     DevBuf<char> tmp;
     DevBuf<sahara_hit> out;
     uint64_t nout = 0;
-    uint32_t hitCap = 0;
+    uint32_t hitCap = 0, taskCap = 0;
     sahara_stats stats{};
-    hipEvent_t ev[6] = {};
+    hipEvent_t ev[8] = {};
 
     ~Ctx() {
         for (auto& e : ev)
@@ -94,7 +95,7 @@ Ctx* newCtx(int device) {
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
-    c->small.reserve(4);
+    c->small.reserve(8);
     c->counters.reserve(8);
     SH_HIP(hipMemset(c->counters.ptr, 0, 8 * sizeof(unsigned long long)));
     return c.release();
@@ -136,18 +137,55 @@ void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, u
     }
 }
 
+// cover[s*m + pos] = a | b << 12 | E << 24: pattern positions [a, b) covered
+// before step pos, and E such that every remaining position admits a match
+// only at error count E (u == E and l <= E from pos to the end), else 31.
+void coverTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
+                std::vector<uint32_t>& out) {
+    out.assign((size_t)ns * m, 0);
+    for (uint32_t s = 0; s < ns; ++s) {
+        const uint32_t* P = pi + (size_t)s * m;
+        const uint32_t* L = l + (size_t)s * m;
+        const uint32_t* U = u + (size_t)s * m;
+        uint32_t a = P[0], b = P[0];
+        const uint32_t K = U[m - 1];
+        bool valid = true;
+        std::vector<uint32_t> E(m);
+        for (uint32_t p = m; p-- > 0;) {
+            valid = valid && U[p] == K && L[p] <= K;
+            E[p] = valid ? K : 31u;
+        }
+        for (uint32_t p = 0; p < m; ++p) {
+            out[(size_t)s * m + p] = a | (b << 12) | (E[p] << 24);
+            a = std::min(a, P[p]);
+            b = std::max(b, P[p] + 1);
+        }
+    }
+}
+
 void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l,
            const uint32_t* u, uint32_t ns, int edit) {
     if (npat == 0) throw Error("no patterns");
-    std::vector<uint32_t> packed;
+    std::vector<uint32_t> packed, cover;
     packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);
     if ((size_t)ns * m * 4 > 60 * 1024) throw Error("scheme too large for LDS (searches * len > 15360)");
+    if (ns > 255) throw Error("at most 255 searches per scheme");
     for (uint64_t i = 0; i < npat * m; ++i)
         if (ranks[i] == 0 || ranks[i] >= c->I.sigma) throw Error("pattern rank out of range for this index");
-    c->pats.reserve(npat * m);
-    SH_HIP(hipMemcpyAsync(c->pats.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
+    coverTable(pi, l, u, ns, m, cover);
+    c->patWords = (m + 7) / 8;
+    {
+        DevBuf<uint8_t> raw;
+        raw.reserve(npat * m);
+        SH_HIP(hipMemcpyAsync(raw.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
+        c->pats.reserve(npat * c->patWords);
+        launchPackPatterns(raw.ptr, npat, m, c->patWords, c->pats.ptr, c->st);
+        SH_HIP(hipStreamSynchronize(c->st));
+    }
     c->scheme.reserve(packed.size());
     SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
+    c->cover.reserve(cover.size());
+    SH_HIP(hipMemcpyAsync(c->cover.ptr, cover.data(), cover.size() * 4, hipMemcpyHostToDevice, c->st));
     SH_HIP(hipStreamSynchronize(c->st));
     c->npat = npat;
     c->m = m;
@@ -173,30 +211,48 @@ void run(Ctx* c, bool count) {
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     const uint64_t T = (uint64_t)blocks * 256;
     const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
-    c->stack.reserve((size_t)std::max<uint32_t>(stackCap, 5) * T);  // levels beyond the LDS part (bounded by stackCap)
+    c->stack.reserve((size_t)std::max<uint32_t>(stackCap, 5) * T);  // levels beyond the LDS part
     S.search_grid = blocks;
+
+    // text phase geometry (LDS per lane: window | pattern | stack)
+    // window: |t| + what both sides can still consume <= m + 3k symbols, plus
+    // the 16-B alignment of its start (31 symbols); rounded to whole uint4
+    const uint32_t winWords = ((c->m + 3 * c->maxErr + 31 + 8) / 8 + 3) & ~3u;
+    const uint32_t textStack = 2 * c->maxErr + 2;
+    const size_t textLds = (size_t)2 * c->nsearch * c->m * 4 +
+                           (size_t)256 * ((winWords + 1) + (c->patWords + 1) + 2 * textStack) * 4;
+    int tbpc = 0;
+    if (c->verify && c->m <= 4095 && textLds <= 160 * 1024) tbpc = textBlocksPerCU(sigma, c->edit, textLds);
+    const uint32_t split = tbpc > 0 ? c->split : 0u;
+    const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
 
     const uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (c->hitCap == 0) {
         c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (const char* e = std::getenv("SAHARA_HITCAP")) c->hitCap = (uint32_t)std::max(1L, std::atol(e));
     }
+    if (c->taskCap == 0) {
+        c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
+    }
     c->hits.reserve((size_t)c->hitCap + 1);
+    c->tasks.reserve((size_t)c->taskCap);
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 8 * sizeof(unsigned long long), c->st));
     c->nout = 0;
 
     for (uint64_t q0 = 0; q0 < c->npat; q0 += maxBatch) {
         const uint64_t nb = std::min<uint64_t>(maxBatch, c->npat - q0);
         ++S.batches;
-        uint32_t hostSmall[4];
+        uint32_t hostSmall[8];
         for (;;) {
-            SH_HIP(hipMemsetAsync(c->small.ptr, 0, 4 * sizeof(uint32_t), c->st));
+            SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), c->st));
             SearchArgs a{};
             a.occF = c->I.occF.ptr;
             a.occR = c->I.occR.ptr;
             for (int i = 0; i < 8; ++i) a.C[i] = (uint32_t)c->I.C[i];
             a.n = (uint32_t)c->I.n;
-            a.pats = c->pats.ptr + q0 * c->m;
+            a.pats = c->pats.ptr + q0 * c->patWords;
+            a.patWords = c->patWords;
             a.m = c->m;
             a.nsearch = c->nsearch;
             a.nitems = (uint32_t)(nb * c->nsearch);
@@ -205,29 +261,74 @@ void run(Ctx* c, bool count) {
             a.hitCount = c->small.ptr + 1;
             a.flags = c->small.ptr + 2;
             a.filled = c->small.ptr + 3;
+            a.taskCount = c->small.ptr + 4;
             a.stack = c->stack.ptr;
             a.stackCap = stackCap;
             a.hits = c->hits.ptr;
             a.hitCap = c->hitCap;
             a.counters = c->counters.ptr;
-            a.sa = c->I.saFull.ptr;
-            a.text4 = c->I.text4.ptr;
-            a.verify = c->verify ? 1u : 0u;
+            a.tasks = c->tasks.ptr;
+            a.taskCap = c->taskCap;
+            a.split = split;
             SH_HIP(hipEventRecord(c->ev[0], c->st));
             launchSearch(a, sigma, c->edit, count, blocks, lds, c->st);
             SH_HIP(hipEventRecord(c->ev[1], c->st));
-            SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+            SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
             SH_HIP(hipStreamSynchronize(c->st));
             S.search_ms += elapsed(c->ev[0], c->ev[1]);
             ++S.search_launches;
             if (hostSmall[2] & 1u) throw Error("search stack overflow (internal bound violated)");
-            if (hostSmall[2] & 2u) {
-                // hit buffer too small for this batch: grow and re-run it
+            if (hostSmall[2] & 8u) {  // task buffer too small: grow and re-run the batch
+                const uint64_t want = (uint64_t)hostSmall[4] + hostSmall[4] / 4 + 1024;
+                if (want >= (1ull << 32) - 2) throw Error("task buffer would exceed 2^32 tasks in one batch");
+                c->taskCap = (uint32_t)want;
+                c->tasks.reserve(c->taskCap);
+                continue;
+            }
+            if (hostSmall[2] & 2u) {  // hit buffer too small: grow and re-run the batch
                 const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
                 if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
                 c->hitCap = (uint32_t)want;
                 c->hits.reserve((size_t)c->hitCap + 1);
                 continue;
+            }
+            const uint32_t ntasks = std::min(hostSmall[4], c->taskCap);
+            if (ntasks) {
+                TextArgs t{};
+                t.sa = c->I.saFull.ptr;
+                t.text4w = reinterpret_cast<const uint32_t*>(c->I.text4.ptr);
+                t.pats = a.pats;
+                t.patWords = c->patWords;
+                t.m = c->m;
+                t.nsearch = c->nsearch;
+                t.scheme = c->scheme.ptr;
+                t.cover = c->cover.ptr;
+                t.tasks = c->tasks.ptr;
+                t.ntasks = ntasks;
+                t.work = c->small.ptr + 5;
+                t.hits = c->hits.ptr;
+                t.hitCap = c->hitCap;
+                t.hitCount = a.hitCount;
+                t.filled = a.filled;
+                t.flags = a.flags;
+                t.counters = c->counters.ptr;
+                t.winWords = winWords;
+                t.stackCap = textStack;
+                SH_HIP(hipEventRecord(c->ev[5], c->st));
+                launchText(t, sigma, c->edit, count, textBlocks, textLds, c->st);
+                SH_HIP(hipEventRecord(c->ev[6], c->st));
+                SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
+                SH_HIP(hipStreamSynchronize(c->st));
+                S.text_ms += elapsed(c->ev[5], c->ev[6]);
+                if (hostSmall[2] & 1u) throw Error("text-phase stack overflow (internal bound violated)");
+                if (hostSmall[2] & 16u) throw Error("text-phase window too small (internal bound violated)");
+                if (hostSmall[2] & 2u) {
+                    const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
+                    if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
+                    c->hitCap = (uint32_t)want;
+                    c->hits.reserve((size_t)c->hitCap + 1);
+                    continue;
+                }
             }
             break;
         }
@@ -300,7 +401,7 @@ void run(Ctx* c, bool count) {
         S.ext_lines = h[2];
         S.lf_steps = h[3];
         S.text_nodes = h[5];
-        S.conversions = h[6];
+        S.conversions = h[6];  // text tasks
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->stats = S;

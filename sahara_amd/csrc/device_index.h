@@ -44,6 +44,8 @@ struct DevBuf {  // minimal owning device buffer that only ever grows
     DevBuf& operator=(const DevBuf&) = delete;
 };
 
+constexpr uint64_t kTextPad = 1u << 16;  // zero padding after the packed text (text-phase windows)
+
 struct DeviceIndex {
     int device = 0;
     uint32_t sigma = 6;
@@ -58,7 +60,7 @@ struct DeviceIndex {
     DevBuf<uint64_t> dRecStarts;
     // Resident for the search (HBM is 288 GB; at 3 Gbp these are 12 + 1.5 GB):
     DevBuf<uint32_t> saFull;        // SA[row] for every row: locate = one read
-    DevBuf<uint8_t> text4;          // text, 4 bits per symbol (two per byte), '$' = 0
+    DevBuf<uint8_t> text4;          // text, 4 bits per symbol (two per byte), '$' = 0, kTextPad zero bytes after
     uint64_t deviceBytes() const {
         return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8 + saFull.cap * 4 +
                text4.cap;

@@ -430,8 +430,8 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
     // resident full SA + packed text for the search (locate = one read)
     I.saFull.reserve(N);
     SH_HIP(hipMemcpyAsync(I.saFull.ptr, sa.ptr, N * 4, hipMemcpyDeviceToDevice, st));
-    I.text4.reserve((N + 1) / 2 + 64);
-    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (N + 1) / 2 + 64, st));
+    I.text4.reserve((N + 1) / 2 + kTextPad);
+    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (N + 1) / 2 + kTextPad, st));
     hipLaunchKernelGGL(kPackText, dim3(gridFor((N + 1) / 2)), dim3(kTB), 0, st, T.ptr, N, I.text4.ptr);
     SH_HIP(hipGetLastError());
 
@@ -482,8 +482,8 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     hipLaunchKernelGGL(kDensify, dim3(gridFor(n)), dim3(kTB), 0, st, I.occF.ptr, n, I.samples.ptr, dC.ptr, rate,
                        I.saFull.ptr, bwt.ptr, err.ptr);
     SH_HIP(hipGetLastError());
-    I.text4.reserve((n + 1) / 2 + 64);
-    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (n + 1) / 2 + 64, st));
+    I.text4.reserve((n + 1) / 2 + kTextPad);
+    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (n + 1) / 2 + kTextPad, st));
     hipLaunchKernelGGL(kPackText, dim3(gridFor((n + 1) / 2)), dim3(kTB), 0, st, bwt.ptr, n, I.text4.ptr);
     SH_HIP(hipGetLastError());
     unsigned int herr = 0;

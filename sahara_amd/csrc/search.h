@@ -14,23 +14,47 @@ struct SearchArgs {
     const OccLine* occR;
     uint32_t C[8];
     uint32_t n;              // text length incl. delimiters (root interval length)
-    const uint8_t* pats;     // npat * m ranks
+    const uint32_t* pats;    // npat * patWords 4-bit packed pattern words
+    uint32_t patWords;
     uint32_t m;
     uint32_t nsearch;
     uint32_t nitems;         // npat * nsearch
     const uint32_t* scheme;  // nsearch * m packed entries (packScheme)
     uint32_t* work;          // item counter
-    uint4* stack;            // (stackCap - 4) * (grid threads) spilled nodes, [depth][lane]
+    uint4* stack;            // spilled DFS levels beyond the LDS part, [depth][grid thread]
     uint32_t stackCap;
-    uint4* hits;             // (qid, lb, len, e)
+    uint4* hits;             // (qid, lb, len, e) or (qid, text pos, 1, e | kPosKnown)
     uint32_t hitCap;
     uint32_t* hitCount;      // reserved slots (waves reserve ranges; unused slots have len 0)
-    uint32_t* filled;        // cursors actually written
-    uint32_t* flags;         // 1 = stack overflow, 2 = hit-buffer overflow, 4 = corrupt locate
-    unsigned long long* counters;  // nodes, rank nodes, lines, -, -, text nodes, conversions
-    const uint32_t* sa;      // full SA (text mode / verify)
-    const uint8_t* text4;    // 4-bit packed text
-    uint32_t verify;         // 1: continue singleton intervals against the text
+    uint32_t* filled;        // records actually written
+    uint32_t* flags;         // 1 stack, 2 hits, 4 locate, 8 tasks, 16 text window
+    unsigned long long* counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
+    uint4* tasks;            // text tasks (row, |t|, qid, meta | search << 24)
+    uint32_t taskCap;
+    uint32_t* taskCount;
+    uint32_t split;          // intervals of <= split rows go to the text phase (0: never)
+};
+
+struct TextArgs {
+    const uint32_t* sa;      // full SA
+    const uint32_t* text4w;  // 4-bit packed text as u32 words (8 symbols each)
+    const uint32_t* pats;
+    uint32_t patWords;
+    uint32_t m;
+    uint32_t nsearch;
+    const uint32_t* scheme;
+    const uint32_t* cover;   // nsearch * m: a | b << 12 | E << 24
+    const uint4* tasks;
+    uint32_t ntasks;
+    uint32_t* work;
+    uint4* hits;
+    uint32_t hitCap;
+    uint32_t* hitCount;
+    uint32_t* filled;
+    uint32_t* flags;
+    unsigned long long* counters;
+    uint32_t winWords;       // window words per lane (8 symbols each)
+    uint32_t stackCap;       // text DFS stack entries per lane
 };
 
 struct LocateArgs {
@@ -49,6 +73,11 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
+void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
+                hipStream_t st);
+void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t* dst,
+                        hipStream_t st);
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                   hipStream_t st);
 size_t rowOffsetsTempBytes(uint64_t nhits);

@@ -4,25 +4,42 @@
 // and fmc::LocateLinear (search.cpp:244-250) — semantics policy P0,
 // docs/semantics.md; CPU restatement in oracle/oracle.cpp (Searcher::visit).
 //
-// Execution model (one lane = one DFS, the wave shares the work queue):
-//   * Work items are (pattern, search) pairs. A lane with nothing to do takes
-//     the next item; all idle lanes of a wave are served by ONE atomic on the
-//     item counter (ballot + mbcnt prefix compaction).
-//   * Each lane walks its search tree depth-first. The node being expanded
-//     stays in registers; at every expansion the match child is pushed first
-//     and all error children above it, and one error child continues in
-//     registers. Hence the stack only holds siblings of error edges on the
-//     current path: at most k * (2*sigma - 2) entries (k <= 15), independent
-//     of the pattern length. Stacks live in HBM interleaved [depth][lane] so a
-//     wave's pushes/pops at equal depth coalesce; the hot top sits in L2.
-//   * An expansion ranks all sigma-1 symbols at lo and lo+len on the BWT of
-//     the extension side: one 64-B Occ line per distinct 64-row block (1 or 2
-//     lines), coalesced 16-B loads, popcount arithmetic — no LDS, no MFMA.
-//   * Leaves (pos == len) are compacted to the hit buffer with a wave ballot
-//     + one atomic per wave. Overflow of the hit buffer is flagged and the
-//     host re-runs the batch with a larger buffer; nothing is truncated.
-// Locate: one lane per reported cursor walks LF (<= rate-1 steps) on the
-// forward lines to a sampled row; each step is one 64-B line. Records are
+// Two phases per batch of patterns, both "one lane = one depth-first search,
+// the wave shares a work queue":
+//
+// Phase 1, kSearchFM: work items are (pattern, search) pairs. Each node ranks
+// all sigma-1 symbols at lo and lo+len on the BWT of its extension side — one
+// 64-B Occ line per distinct 64-row block. Lanes of a pair fetch each other's
+// lines together (<= 32 distinct lines per load instruction: address
+// translation stays off the critical path on a multi-GB index, see
+// tools/gather_bench.hip) and swap halves with DPP. As soon as a node's
+// interval holds at most `split` rows, the node is handed to phase 2 as one
+// *text task* per row instead of being ranked further.
+//
+// Phase 2, kSearchText: a text task is a node whose string t has a single
+// occurrence. Extending it by symbol c is non-empty iff c is the text's own
+// next symbol, so the rest of its subtree is the same DFS run against the
+// text. The lane copies the window of the 4-bit text that the subtree can
+// reach (full SA: one read) and the packed pattern into LDS and expands the
+// subtree there, without touching HBM. Nodes whose remaining positions admit
+// no further error are decided by one comparison of the remaining pattern
+// against the window.
+//
+// Both DFSs push the match child first and the error children above it and
+// continue with one error child in registers, so a stack holds at most the
+// siblings of the error edges on the current path: <= k*(2*sigma-2) (FM) or
+// <= 2k (text) entries, independent of the pattern length.
+//
+// The multiset of (qid, text position, e) leaves equals the reference DFS's:
+// a node of interval [lb, lb+len) expands to the same (path, occurrence)
+// pairs whether it is ranked or split into its len occurrences.
+//
+// Leaves are compacted into the hit buffer with a wave ballot + prefix count
+// into per-wave reserved slot ranges (one atomic per 64 slots). Overflow of
+// any buffer is flagged; the host re-runs the batch with a larger buffer.
+//
+// Locate: FM leaves resolve rows through the resident full SA (one read per
+// row) or, in the reference mode, by LF walks to the SA samples. Records are
 // packed into u64 keys (qid, text position, e) and radix-sorted for the
 // canonical (qid, seq_id, pos, e) order.
 
@@ -91,12 +108,94 @@ __device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t nib(uint32_t word, uint32_t i) { return (word >> ((i & 7u) * 4u)) & 0xFu; }
+
 constexpr uint32_t kWorkChunk = 256;  // items a wave takes per atomic
-constexpr uint32_t kHitChunk = 64;    // hit slots a wave reserves per atomic
-constexpr uint32_t kLdsDepth = 4;     // DFS stack levels kept in LDS (16 KB per block)
+constexpr uint32_t kTaskChunk = 64;   // text tasks a wave takes per atomic
+constexpr uint32_t kHitChunk = 64;    // hit / task slots a wave reserves per atomic
+constexpr uint32_t kLdsDepth = 4;     // FM DFS stack levels kept in LDS (16 KB per block)
+
+// Per-wave slot reservation for append-only outputs (hits, tasks): ballot +
+// prefix count inside the wave's current range; a fresh range of kHitChunk
+// slots costs one atomic. All lanes must call it (wave-uniform).
+struct SlotRange {
+    uint32_t next = 0, end = 0;
+    __device__ __forceinline__ bool take(bool want, uint32_t lane, uint64_t ltMask, uint32_t* counter,
+                                         uint32_t& slot) {
+        const uint64_t m = __ballot(want);
+        if (!m) return false;
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        const uint32_t rank = (uint32_t)__popcll(m & ltMask);
+        const uint32_t avail = end - next;
+        uint32_t base = 0;
+        if (cnt > avail) {
+            if (lane == 0) base = atomicAdd(counter, kHitChunk);
+            base = __shfl(base, 0);
+        }
+        slot = rank < avail ? next + rank : base + (rank - avail);
+        if (cnt > avail) { next = base + (cnt - avail); end = base + kHitChunk; }
+        else next += cnt;
+        return true;
+    }
+    // unused tail of the last range: empty records (len 0) for the locate scan
+    __device__ __forceinline__ void close(uint32_t lane, uint4* buf, uint32_t cap) {
+        for (uint32_t i = next + lane; i < end; i += 64)
+            if (i < cap) buf[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+};
+
+// Children of one DFS node under policy P0 (docs/semantics.md), with the
+// stack discipline described at the top. `occ[c]` says whether the child of
+// symbol c exists; `mk(c, kind)` builds it. Returns whether a child is kept
+// in registers (through `next`).
+template <int SIGMA, typename Node, typename MkChild, typename Push>
+__device__ __forceinline__ bool expandChildren(const uint32_t occ[SIGMA], uint32_t cq, bool matchOK, bool misOK,
+                                               bool delOK, bool insOK, const Node& insChild, MkChild mk, Push push,
+                                               Node& next) {
+    uint32_t nErr = insOK ? 1u : 0u;
+    bool hasM = false;
+#pragma unroll
+    for (int c = 1; c < SIGMA; ++c) {
+        if (occ[c]) {
+            if ((uint32_t)c == cq) hasM = matchOK;
+            else nErr += misOK ? 1u : 0u;
+            nErr += delOK ? 1u : 0u;
+        }
+    }
+    bool kept = false;
+    auto emit = [&](const Node& v) {
+        if (!kept) { next = v; kept = true; }
+        else push(v);
+    };
+    if (hasM && nErr) push(mk((int)cq, 0));  // match child below all its error siblings
+    if (insOK) emit(insChild);
+#pragma unroll
+    for (int c = 1; c < SIGMA; ++c) {
+        if (occ[c]) {
+            if ((uint32_t)c != cq && misOK) emit(mk(c, 1));
+            if (delOK) emit(mk(c, 2));
+        }
+    }
+    if (!kept && hasM) { next = mk((int)cq, 0); kept = true; }
+    return kept;
+}
+
+// kind: 0 = match (M), 1 = substitution (S), 2 = deletion (D), 3 = insertion (I)
+__device__ __forceinline__ uint32_t childMeta(uint32_t pos, uint32_t e, uint32_t lastL, uint32_t lastR, bool right,
+                                              uint32_t dl, uint32_t kind) {
+    const uint32_t op = kind == 2 ? OP_D : (kind == 3 ? OP_I : OP_MS);
+    const uint32_t npos = kind == 2 ? pos : pos + 1u;
+    const uint32_t ne = kind == 0 ? e : e + 1u;
+    const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
+    const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
+    const uint32_t nd = dl + (kind == 2 ? 1u : 0u) - (kind == 3 ? 1u : 0u);
+    return npos | (ne << 16) | (nl << 20) | (nr << 22) | (nd << 25);
+}
+
+// =========================================================== phase 1: FM ====
 
 template <int SIGMA, bool EDIT, bool COUNT>
-__global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
+__global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     extern __shared__ uint32_t sch[];
     for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) sch[i] = a.scheme[i];
     __syncthreads();
@@ -108,28 +207,21 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
     const bool odd = lane & 1u;
     // DFS stack: the bottom kLdsDepth levels live in LDS ([level][thread],
     // conflict-free 16-B rows when lanes sit at equal depth), deeper levels
-    // spill to HBM ([level][grid thread]). Typical depth stays in LDS.
+    // spill to HBM ([level][grid thread]).
     __shared__ uint4 lstk[kLdsDepth][256];
     uint4* stk = a.stack + gtid;
-    auto spush = [&](uint32_t d, const uint4& v) {
-        if (d < kLdsDepth) lstk[d][threadIdx.x] = v;
-        else stk[(size_t)(d - kLdsDepth) * T] = v;
-    };
-    auto spop = [&](uint32_t d) -> uint4 {
-        return d < kLdsDepth ? lstk[d][threadIdx.x] : stk[(size_t)(d - kLdsDepth) * T];
-    };
 
-    uint32_t sp = 0, pid = 0, sOff = 0;
+    uint32_t sp = 0, pid = 0, sIdx = 0;
     bool have = false, exhausted = false;
-    uint32_t qNext = 0, qEnd = 0, hNext = 0, hEnd = 0, filled = 0;  // wave-uniform
+    uint32_t qNext = 0, qEnd = 0, filled = 0;  // wave-uniform
     bool qDone = false;
+    SlotRange hitSlots, taskSlots;
     uint4 cur = make_uint4(0, 0, 0, 0);
-    uint64_t cNodes = 0, cRank = 0, cLines = 0, cText = 0, cConv = 0;
+    uint64_t cNodes = 0, cRank = 0, cLines = 0, cTasks = 0;
 
     for (;;) {
         // ---- refill idle lanes from the wave's private item range; the wave
-        // takes kWorkChunk items per atomic on the global counter, so one
-        // counter word serves the whole grid without saturating
+        // takes kWorkChunk items per atomic on the global counter
         const bool need = !have && sp == 0 && !exhausted;
         uint64_t pending = __ballot(need);
         while (pending) {  // wave-uniform
@@ -148,7 +240,7 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
             if (mine) {
                 const uint32_t item = qNext + rank;
                 pid = item / a.nsearch;
-                sOff = (item - pid * a.nsearch) * a.m;
+                sIdx = item - pid * a.nsearch;
                 cur = make_uint4(0u, 0u, a.n, kDeltaZero);
                 have = true;
             }
@@ -158,84 +250,65 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         if (qDone && need && !have) exhausted = true;
         if (!have && sp > 0) {
             --sp;
-            cur = spop(sp);
+            cur = sp < kLdsDepth ? lstk[sp][threadIdx.x] : stk[(size_t)(sp - kLdsDepth) * T];
             have = true;
         }
         if (!__any(have)) break;
 
-        // ---- leaves -> hit buffer: ballot + prefix compaction into the wave's
-        // reserved slot range; a new range of kHitChunk slots costs one atomic
         const uint32_t pos = cur.w & 0xFFFFu;
-        const bool leaf = have && pos == a.m;
-        const uint64_t lm = __ballot(leaf);
-        if (lm) {
-            const uint32_t cnt = (uint32_t)__popcll(lm);
-            const uint32_t rank = (uint32_t)__popcll(lm & ltMask);
-            const uint32_t avail = hEnd - hNext;
-            uint32_t base = 0;
-            if (cnt > avail) {
-                if (lane == 0) base = atomicAdd(a.hitCount, kHitChunk);
-                base = __shfl(base, 0);
-            }
-            if (leaf) {
-                const uint32_t idx = rank < avail ? hNext + rank : base + (rank - avail);
-                const bool known = (cur.w & kTextBit) != 0;
-                if (idx < a.hitCap)
-                    a.hits[idx] = make_uint4(pid, cur.x, known ? 1u : cur.z, ((cur.w >> 16) & 0xFu) | (known ? kPosKnown : 0u));
+        // ---- leaves -> hit buffer
+        {
+            const bool leaf = have && pos == a.m;
+            uint32_t slot;
+            if (hitSlots.take(leaf, lane, ltMask, a.hitCount, slot) && leaf) {
+                if (slot < a.hitCap) a.hits[slot] = make_uint4(pid, cur.x, cur.z, (cur.w >> 16) & 0xFu);
                 else atomicOr(a.flags, 2u);
                 have = false;
+                ++filled;
             }
-            if (cnt > avail) { hNext = base + (cnt - avail); hEnd = base + kHitChunk; }
-            else hNext += cnt;
-            filled += cnt;
         }
+        // ---- small intervals -> one text task per row (phase 2)
+        if (a.split) {
+            const bool conv = have && cur.z <= a.split;
+            const uint32_t tlen = pos + metaDelta(cur.w) - 16u;  // |t|
+            for (uint32_t j = 0; j < a.split; ++j) {  // wave-uniform trip count
+                const bool want = conv && j < cur.z;
+                uint32_t slot;
+                if (taskSlots.take(want, lane, ltMask, a.taskCount, slot) && want) {
+                    if (slot < a.taskCap)
+                        a.tasks[slot] = make_uint4(cur.x + j, tlen, pid, (cur.w & 0x00FFFFFFu) | (sIdx << 24));
+                    else atomicOr(a.flags, 8u);
+                    if (COUNT) ++cTasks;
+                }
+            }
+            if (conv) have = false;
+        }
+
         // ---- decode the node (per lane)
-        uint32_t e = 0, lastL = 0, lastR = 0, cq = 0, lb = 0, ub = 0;
-        bool right = false, matchOK = false, misOK = false, delOK = false, insOK = false, text = false;
-        uint32_t lo = 0, hi = 0, tc = 0;
+        uint32_t e = 0, lastL = 0, lastR = 0, cq = 0;
+        bool right = false, matchOK = false, misOK = false, delOK = false, insOK = false;
+        uint32_t lo = 0, hi = 0;
         bool needA = false, needB = false;
         if (have) {
             e = (cur.w >> 16) & 0xFu;
             lastL = (cur.w >> 20) & 3u;
             lastR = (cur.w >> 22) & 3u;
-            const uint32_t se = sch[sOff + pos];
-            const uint32_t q = se & 0xFFFFu;
-            lb = (se >> 16) & 0xFu;
-            ub = (se >> 20) & 0xFu;
+            const uint32_t se = sch[sIdx * a.m + pos];
+            const uint32_t q = se & 0xFFFFu, lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
             right = (se >> 24) & 1u;
-            cq = a.pats[(size_t)pid * a.m + q];
+            cq = nib(a.pats[(size_t)pid * a.patWords + (q >> 3)], q);
             const uint32_t side = right ? lastR : lastL;
             matchOK = lb <= e && e <= ub;
             misOK = lb <= e + 1 && e + 1 <= ub;
             delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
             insOK = EDIT && misOK && side != OP_D;
-            text = (cur.w & kTextBit) != 0;
-            if (!text && a.verify && cur.z == 1u) {
-                // singleton interval: resolve its text position once (full SA)
-                // and continue the same DFS against the resident text
-                const uint32_t p = a.sa[cur.x];
-                const uint32_t tlen = pos + metaDelta(cur.w) - 16u;
-                cur = make_uint4(p, p + tlen, 1u, cur.w | kTextBit);
-                text = true;
-                if (COUNT) ++cConv;
-            }
-            if (text) {
-                const uint32_t tp = right ? cur.y : cur.x - 1u;  // next text symbol
-                const bool inside = right ? (cur.y < a.n) : (cur.x > 0u);
-                if (inside && (matchOK || misOK || delOK)) tc = (a.text4[tp >> 1] >> ((tp & 1u) * 4u)) & 0xFu;
-            } else {
-                lo = right ? cur.y : cur.x;
-                hi = lo + cur.z;
-                needA = matchOK || misOK || delOK;
-                needB = needA && (hi >> 6) != (lo >> 6);
-            }
+            lo = right ? cur.y : cur.x;
+            hi = lo + cur.z;
+            needA = matchOK || misOK || delOK;
+            needB = needA && (hi >> 6) != (lo >> 6);
         }
 
-        // ---- pair-cooperative Occ line fetch (wave-uniform). Lanes 2i, 2i+1
-        // fetch each other's lines together: every load instruction touches
-        // at most 32 distinct 64-B lines (two lanes per line), which keeps
-        // address translation off the critical path on a multi-GB index
-        // (tools/gather_bench: 49.8 vs 21.7 Glines/s at 7 GB).
+        // ---- pair-cooperative Occ line fetch (wave-uniform)
         const uint64_t ownA = (uint64_t)(right ? a.occR : a.occF) + (uint64_t)(lo >> 6) * 64u;
         const uint64_t ownB = (uint64_t)(right ? a.occR : a.occF) + (uint64_t)(hi >> 6) * 64u;
         uint32_t ca[5], cb[5];
@@ -244,117 +317,275 @@ __global__ __launch_bounds__(256) void kSearch(SearchArgs a) {
         fetchLinePair(ownB, needB, odd, cb, pb);
 
         if (have) {
-        // ---- expand one node
-        const uint32_t dl = metaDelta(cur.w);
-        auto meta = [&](uint32_t npos, uint32_t ne, uint32_t op) -> uint32_t {
-            const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
-            const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
-            const uint32_t nd = dl + (op == OP_D ? 1u : 0u) - (op == OP_I ? 1u : 0u);
-            return npos | (ne << 16) | (nl << 20) | (nr << 22) | (cur.w & kTextBit) | (nd << 25);
-        };
-        if (COUNT) ++cNodes;
-
-        // child c = (fx[c], fy[c], occ[c]): forward / reverse lower bounds of an
-        // FM child, or the [start, end) text span of a text child
-        uint32_t occ[SIGMA], fx[SIGMA], fy[SIGMA];
+            if (COUNT) ++cNodes;
+            // child c = (fx[c], fy[c], occ[c]): forward / reverse lower bounds
+            uint32_t occ[SIGMA], fx[SIGMA], fy[SIGMA];
 #pragma unroll
-        for (int c = 0; c < SIGMA; ++c) occ[c] = fx[c] = fy[c] = 0;
-        if (text) {
-            // the only symbol that can extend a singleton is the text's own
-            if (COUNT) ++cText;
-            const uint32_t ns = right ? cur.x : cur.x - 1u, ne = right ? cur.y + 1u : cur.y;
+            for (int c = 0; c < SIGMA; ++c) occ[c] = fx[c] = fy[c] = 0;
+            if (needA) {
+                if (!needB) {
 #pragma unroll
-            for (int c = 1; c < SIGMA; ++c) {  // branch-free: keeps the arrays in registers
-                occ[c] = (uint32_t)c == tc ? 1u : 0u;
-                fx[c] = ns;
-                fy[c] = ne;
-            }
-        } else if (needA) {
-            if (!needB) {
-#pragma unroll
-                for (int i = 0; i < 5; ++i) cb[i] = ca[i];
-                pb[0] = pa[0]; pb[1] = pa[1]; pb[2] = pa[2];
-            }
-            if (COUNT) { ++cRank; cLines += needB ? 2 : 1; }
-            const uint64_t ml = lowMask(lo & 63u), mh = lowMask(hi & 63u);
-            uint32_t sum = 0, base[SIGMA];
-#pragma unroll
-            for (int c = 1; c < SIGMA; ++c) {
-                const uint32_t rl = ca[c - 1] + (uint32_t)__popcll(symMask(pa, c) & ml);
-                const uint32_t rh = cb[c - 1] + (uint32_t)__popcll(symMask(pb, c) & mh);
-                occ[c] = rh - rl;
-                base[c] = a.C[c] + rl;
-                sum += occ[c];
-            }
-            // bidirectional update: the other side moves by the occurrences of
-            // the smaller symbols, '$' first
-            uint32_t acc = (right ? cur.x : cur.y) + (cur.z - sum);
-#pragma unroll
-            for (int c = 1; c < SIGMA; ++c) {
-                fx[c] = right ? acc : base[c];
-                fy[c] = right ? base[c] : acc;
-                acc += occ[c];
-            }
-        }
-        auto child = [&](int c, uint32_t m) -> uint4 {
-            return make_uint4(fx[c], fy[c], occ[c], m);
-        };
-        // count error children; find the match child
-        uint32_t nErr = insOK ? 1u : 0u;
-        bool hasM = false;
-        uint4 mChild = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int c = 1; c < SIGMA; ++c) {
-            if (occ[c]) {
-                if ((uint32_t)c == cq) {
-                    hasM = matchOK;
-                    mChild = child(c, meta(pos + 1, e, OP_MS));
-                } else {
-                    nErr += misOK ? 1u : 0u;
+                    for (int i = 0; i < 5; ++i) cb[i] = ca[i];
+                    pb[0] = pa[0]; pb[1] = pa[1]; pb[2] = pa[2];
                 }
-                nErr += delOK ? 1u : 0u;
-            }
-        }
-        bool kept = false;
-        uint4 next = make_uint4(0, 0, 0, 0);
-        auto push = [&](const uint4& v) {
-            if (sp < a.stackCap) {
-                spush(sp, v);
-                ++sp;
-            } else {
-                atomicOr(a.flags, 1u);
-            }
-        };
-        auto emit = [&](const uint4& v) {
-            if (!kept) { next = v; kept = true; }
-            else push(v);
-        };
-        if (hasM && nErr) push(mChild);  // match child below all its error siblings
-        if (insOK) emit(make_uint4(cur.x, cur.y, cur.z, meta(pos + 1, e + 1, OP_I)));
+                if (COUNT) { ++cRank; cLines += needB ? 2 : 1; }
+                const uint64_t ml = lowMask(lo & 63u), mh = lowMask(hi & 63u);
+                uint32_t sum = 0, base[SIGMA];
 #pragma unroll
-        for (int c = 1; c < SIGMA; ++c) {
-            if (occ[c]) {
-                if ((uint32_t)c != cq && misOK) emit(child(c, meta(pos + 1, e + 1, OP_MS)));
-                if (delOK) emit(child(c, meta(pos, e + 1, OP_D)));
+                for (int c = 1; c < SIGMA; ++c) {
+                    const uint32_t rl = ca[c - 1] + (uint32_t)__popcll(symMask(pa, c) & ml);
+                    const uint32_t rh = cb[c - 1] + (uint32_t)__popcll(symMask(pb, c) & mh);
+                    occ[c] = rh - rl;
+                    base[c] = a.C[c] + rl;
+                    sum += occ[c];
+                }
+                // bidirectional update: the other side moves by the occurrences
+                // of the smaller symbols, '$' first
+                uint32_t acc = (right ? cur.x : cur.y) + (cur.z - sum);
+#pragma unroll
+                for (int c = 1; c < SIGMA; ++c) {
+                    fx[c] = right ? acc : base[c];
+                    fy[c] = right ? base[c] : acc;
+                    acc += occ[c];
+                }
             }
+            const uint32_t dl = metaDelta(cur.w);
+            auto mk = [&](int c, uint32_t kind) -> uint4 {
+                uint32_t f = 0, g = 0, o = 0;
+#pragma unroll
+                for (int s = 1; s < SIGMA; ++s)
+                    if (s == c) { f = fx[s]; g = fy[s]; o = occ[s]; }
+                return make_uint4(f, g, o, childMeta(pos, e, lastL, lastR, right, dl, kind));
+            };
+            auto push = [&](const uint4& v) {
+                if (sp < a.stackCap) {
+                    if (sp < kLdsDepth) lstk[sp][threadIdx.x] = v;
+                    else stk[(size_t)(sp - kLdsDepth) * T] = v;
+                    ++sp;
+                } else {
+                    atomicOr(a.flags, 1u);
+                }
+            };
+            const uint4 ins = make_uint4(cur.x, cur.y, cur.z, childMeta(pos, e, lastL, lastR, right, dl, 3));
+            uint4 next = make_uint4(0, 0, 0, 0);
+            have = expandChildren<SIGMA>(occ, cq, matchOK, misOK, delOK, insOK, ins, mk, push, next);
+            cur = next;
         }
-        if (!kept && hasM) { next = mChild; kept = true; }
-        have = kept;
-        cur = next;
-        }  // have
     }
-    // unused tail of the wave's last slot range: empty cursors (len 0)
-    for (uint32_t i = hNext + lane; i < hEnd; i += 64)
-        if (i < a.hitCap) a.hits[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (lane == 0 && filled) atomicAdd(a.filled, filled);
+    hitSlots.close(lane, a.hits, a.hitCap);
+    taskSlots.close(lane, a.tasks, a.taskCap);
+    if (filled) atomicAdd(a.filled, filled);  // per-lane counts
     if (COUNT) {
         atomicAdd(a.counters + 0, (unsigned long long)cNodes);
         atomicAdd(a.counters + 1, (unsigned long long)cRank);
         atomicAdd(a.counters + 2, (unsigned long long)cLines);
-        atomicAdd(a.counters + 5, (unsigned long long)cText);
-        atomicAdd(a.counters + 6, (unsigned long long)cConv);
+        atomicAdd(a.counters + 6, (unsigned long long)cTasks);
     }
 }
+
+// ========================================================= phase 2: text ====
+//
+// LDS: scheme[S*m] | cover[S*m] | per lane, interleaved so that the lanes of
+// a wave hit consecutive banks at equal offsets:
+//   window  (winWords u32 words of 8 nibbles + 1 pad)   W[j*256 + t]
+//   pattern (patWords u32 words of 8 nibbles + 1 pad)   P[j*256 + t]
+//   stack   (stackCap uint2 entries)                    S[d*256 + t]
+// cover entry: a | b << 12 | E << 24 — the covered pattern positions [a, b)
+// before step `pos`, and E = the error count at which every remaining
+// position admits a match only (u == E, l <= E from pos on), 31 if none.
+
+// 8 consecutive nibbles starting at nibble offset o of an interleaved word array
+__device__ __forceinline__ uint32_t nib8(const uint32_t* A, uint32_t o) {
+    const uint32_t w0 = A[(o >> 3) * 256u], w1 = A[((o >> 3) + 1u) * 256u];
+    const uint32_t sh = (o & 7u) * 4u;
+    return sh ? (w0 >> sh) | (w1 << (32u - sh)) : w0;
+}
+
+// pattern[p, p+len) == window[w, w+len) ?
+__device__ __forceinline__ bool equalRun(const uint32_t* P, uint32_t p, const uint32_t* W, uint32_t w,
+                                         uint32_t len) {
+    for (uint32_t i = 0; i < len; i += 8) {
+        const uint32_t n = min(8u, len - i);
+        const uint32_t mask = n == 8 ? 0xFFFFFFFFu : ((1u << (4u * n)) - 1u);
+        if ((nib8(P, p + i) ^ nib8(W, w + i)) & mask) return false;
+    }
+    return true;
+}
+
+template <int SIGMA, bool EDIT, bool COUNT>
+__global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
+    extern __shared__ uint32_t lds[];
+    uint32_t* sch = lds;
+    uint32_t* cov = lds + a.nsearch * a.m;
+    uint32_t* slot = cov + a.nsearch * a.m;
+    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) {
+        sch[i] = a.scheme[i];
+        cov[i] = a.cover[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t ltMask = (1ull << lane) - 1ull;
+    uint32_t* W = slot + threadIdx.x;
+    uint32_t* P = slot + (a.winWords + 1u) * 256u + threadIdx.x;
+    uint2* S = reinterpret_cast<uint2*>(slot + (a.winWords + a.patWords + 2u) * 256u) + threadIdx.x;
+    const uint32_t winLen = a.winWords * 8u;
+
+    uint32_t sp = 0, pid = 0, sIdx = 0, wb = 0, sBase = 0;
+    bool have = false, exhausted = false;
+    uint32_t qNext = 0, qEnd = 0, filled = 0;
+    bool qDone = false;
+    SlotRange hitSlots;
+    uint2 cur = make_uint2(0, 0);  // x = xo | yo << 16 (window offsets of t's [start, end)), y = meta
+    uint64_t cNodes = 0;
+
+    for (;;) {
+        // Starting a task costs two dependent global reads (SA, then the
+        // window) that stall the whole wave, so idle lanes are refilled in
+        // batches: only once half of the wave is idle (or nothing is left).
+        const bool idle = !have && sp == 0 && !exhausted;
+        const uint64_t idleMask = __ballot(idle);
+        const bool busy = __any(have || sp > 0);
+        const bool refill = !busy || __popcll(idleMask) >= 32;
+        const bool need = refill && idle;
+        uint64_t pending = refill ? idleMask : 0ull;
+        while (pending) {  // wave-uniform
+            if (qNext >= qEnd) {
+                if (qDone) break;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(a.work, kTaskChunk);
+                base = __shfl(base, 0);
+                if (base >= a.ntasks) { qDone = true; break; }
+                qNext = base;
+                qEnd = min(base + kTaskChunk, a.ntasks);
+            }
+            const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
+            const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
+            const bool mine = ((pending >> lane) & 1ull) && rank < take;
+            if (mine) {
+                // ---- start a task: resolve the row's text position (full SA),
+                // copy the pattern and the text window its subtree can reach
+                const uint4 t = a.tasks[qNext + rank];
+                const uint32_t x = a.sa[t.x];
+                pid = t.z;
+                sIdx = t.w >> 24;
+                sBase = sIdx * a.m;
+                const uint32_t meta = t.w & 0x00FFFFFFu;
+                const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
+                const uint32_t ca = cov[sBase + pos] & 0xFFFu;
+                const uint32_t K = (sch[sBase + a.m - 1] >> 20) & 0xFu;
+                const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
+                wb = (x > left ? x - left : 0u) & ~31u;            // 16-B aligned window start
+                const uint4* src = reinterpret_cast<const uint4*>(a.text4w + (wb >> 3));
+                for (uint32_t j = 0; j < a.winWords; j += 4) {
+                    const uint4 v = src[j >> 2];
+                    W[j * 256u] = v.x; W[(j + 1) * 256u] = v.y; W[(j + 2) * 256u] = v.z; W[(j + 3) * 256u] = v.w;
+                }
+                const uint32_t* ps = a.pats + (size_t)pid * a.patWords;
+                for (uint32_t j = 0; j < a.patWords; ++j) P[j * 256u] = ps[j];
+                P[a.patWords * 256u] = 0u;
+                cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
+                have = true;
+            }
+            pending &= ~__ballot(mine);
+            qNext += take;
+        }
+        if (qDone && need && !have) exhausted = true;
+        if (!have && sp > 0) {
+            --sp;
+            cur = S[sp * 256u];
+            have = true;
+        }
+        if (!__any(have || (!exhausted && sp == 0))) break;  // all lanes exhausted
+
+        const uint32_t pos = cur.y & 0xFFFFu;
+        const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
+        const uint32_t e = (cur.y >> 16) & 0xFu;
+        bool leaf = have && pos == a.m;
+        uint32_t leafStart = xo;
+        uint32_t se = 0, cv = 0;
+        if (have && !leaf) {
+            se = sch[sBase + pos];
+            cv = cov[sBase + pos];
+            if ((cv >> 24) == e) {
+                // ---- one-shot: no further error is possible on the remaining
+                // positions -> both remainders must match exactly
+                if (COUNT) ++cNodes;
+                const uint32_t ca = cv & 0xFFFu, cb = (cv >> 12) & 0xFFFu;
+                bool ok = xo >= ca;  // else the occurrence would start before text position 0
+                if (!ok && wb != 0) atomicOr(a.flags, 16u);
+                if (ok && yo + (a.m - cb) > winLen) { atomicOr(a.flags, 16u); ok = false; }
+                ok = ok && equalRun(P, 0, W, xo - ca, ca) && equalRun(P, cb, W, yo, a.m - cb);
+                leaf = ok;
+                leafStart = xo - ca;
+                have = ok;
+            }
+        }
+        {
+            uint32_t s;
+            if (hitSlots.take(leaf, lane, ltMask, a.hitCount, s) && leaf) {
+                if (s < a.hitCap) a.hits[s] = make_uint4(pid, wb + leafStart, 1u, e | kPosKnown);
+                else atomicOr(a.flags, 2u);
+                have = false;
+                ++filled;
+            }
+        }
+        if (have) {
+            if (COUNT) ++cNodes;
+            const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
+            const uint32_t q = se & 0xFFFFu, lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
+            const bool right = (se >> 24) & 1u;
+            const uint32_t cq = nib(P[(q >> 3) * 256u], q);
+            const uint32_t side = right ? lastR : lastL;
+            const bool matchOK = lb <= e && e <= ub;
+            const bool misOK = lb <= e + 1 && e + 1 <= ub;
+            const bool delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
+            const bool insOK = EDIT && misOK && side != OP_D;
+            // the text's next symbol on the extension side ('$' / text edge = 0)
+            const uint32_t to = right ? yo : xo - 1u;
+            uint32_t tc = 0;
+            if (right || xo > 0) {
+                if (to < winLen) tc = nib(W[(to >> 3) * 256u], to);
+                else atomicOr(a.flags, 16u);  // window too small (cannot happen)
+            } else if (wb != 0) {
+                atomicOr(a.flags, 16u);
+            }
+            // children: the one symbol the text offers (M or S), D with it, I
+            const bool sym = tc != 0;
+            const bool isM = sym && tc == cq && matchOK;
+            const bool hasS = sym && tc != cq && misOK;
+            const bool hasD = sym && delOK;
+            const uint32_t nspan = right ? (xo | ((yo + 1u) << 16)) : ((xo - 1u) | (yo << 16));
+            auto meta = [&](uint32_t kind) { return childMeta(pos, e, lastL, lastR, right, 16u, kind) & 0x00FFFFFFu; };
+            const uint32_t nErr = (insOK ? 1u : 0u) + (hasS ? 1u : 0u) + (hasD ? 1u : 0u);
+            auto push = [&](const uint2& v) {
+                if (sp < a.stackCap) S[(sp++) * 256u] = v;
+                else atomicOr(a.flags, 1u);
+            };
+            // match child below its error siblings; continue with the first
+            // error child (I, then S, then D) or, if none, with the match child
+            if (isM && nErr) push(make_uint2(nspan, meta(0)));
+            uint2 next = isM ? make_uint2(nspan, meta(0)) : make_uint2(0, 0);
+            bool kept = isM && !nErr;
+            if (insOK) { next = make_uint2(cur.x, meta(3)); kept = true; }
+            if (hasS) {
+                const uint2 v = make_uint2(nspan, meta(1));
+                if (insOK) push(v); else { next = v; kept = true; }
+            }
+            if (hasD) {
+                const uint2 v = make_uint2(nspan, meta(2));
+                if (insOK || hasS) push(v); else { next = v; kept = true; }
+            }
+            have = kept;
+            cur = next;
+        }
+    }
+    hitSlots.close(lane, a.hits, a.hitCap);
+    if (filled) atomicAdd(a.filled, filled);  // per-lane counts
+    if (COUNT) atomicAdd(a.counters + 5, (unsigned long long)cNodes);
+}
+
+// ================================================================ locate ====
 
 // One lane per reported cursor: locate every row of [lb, lb+len).
 template <bool COUNT>
@@ -365,7 +596,7 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
         const uint4 hit = a.hits[h];
         const uint64_t out = a.rowOff[h];
         const uint64_t e = hit.w & 0xFu;
-        if (hit.w & kPosKnown) {  // resolved during the search (text mode)
+        if (hit.w & kPosKnown) {  // resolved by the text phase
             a.keys[out] = ((uint64_t)hit.x << 36) | ((uint64_t)hit.y << 4) | e;
             continue;
         }
@@ -374,7 +605,7 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
                 a.keys[out + j] = ((uint64_t)hit.x << 36) | ((uint64_t)a.sa[hit.y + j] << 4) | e;
             continue;
         }
-        for (uint32_t j = 0; j < hit.z; ++j) {
+        for (uint32_t j = 0; j < hit.z; ++j) {  // fmc::LocateLinear: LF walk to a sample
             uint32_t row = hit.y + j;
             uint32_t st = 0;
             uint64_t gpos = 0;
@@ -443,18 +674,46 @@ __global__ void kDigest(const sahara_hit* __restrict__ h, uint64_t n, unsigned l
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, (unsigned long long)acc);
 }
 
+// pattern bytes (one symbol per byte) -> 4-bit words, patWords per pattern
+__global__ void kPackPatterns(const uint8_t* __restrict__ src, uint64_t npat, uint32_t m, uint32_t patWords,
+                              uint32_t* __restrict__ dst) {
+    const uint64_t total = npat * patWords;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = i / patWords;
+        const uint32_t w = (uint32_t)(i - p * patWords);
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t q = w * 8 + j;
+            if (q < m) v |= (uint32_t)(src[p * m + q] & 0xFu) << (4 * j);
+        }
+        dst[i] = v;
+    }
+}
+
 struct HitLen {
     __host__ __device__ uint64_t operator()(const uint4& h) const { return (uint64_t)h.z; }
 };
 
 template <int SIGMA>
-void launchSearchT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
+void launchFMT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     if (edit) {
-        if (count) hipLaunchKernelGGL((kSearch<SIGMA, true, true>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearch<SIGMA, true, false>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchFM<SIGMA, true, true>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchFM<SIGMA, true, false>), grid, dim3(256), lds, st, a);
     } else {
-        if (count) hipLaunchKernelGGL((kSearch<SIGMA, false, true>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearch<SIGMA, false, false>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchFM<SIGMA, false, true>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchFM<SIGMA, false, false>), grid, dim3(256), lds, st, a);
+    }
+}
+
+template <int SIGMA>
+void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
+    if (edit) {
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false>), grid, dim3(256), lds, st, a);
+    } else {
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false>), grid, dim3(256), lds, st, a);
     }
 }
 
@@ -463,16 +722,40 @@ void launchSearchT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     int b = 0;
     const void* f;
-    if (sigma == 5) f = edit ? (const void*)kSearch<5, true, false> : (const void*)kSearch<5, false, false>;
-    else            f = edit ? (const void*)kSearch<6, true, false> : (const void*)kSearch<6, false, false>;
+    if (sigma == 5) f = edit ? (const void*)kSearchFM<5, true, false> : (const void*)kSearchFM<5, false, false>;
+    else            f = edit ? (const void*)kSearchFM<6, true, false> : (const void*)kSearchFM<6, false, false>;
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b < 1 ? 1 : b;
 }
 
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
+    int b = 0;
+    const void* f;
+    if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false> : (const void*)kSearchText<5, false, false>;
+    else            f = edit ? (const void*)kSearchText<6, true, false> : (const void*)kSearchText<6, false, false>;
+    SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
+    return b;
+}
+
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                   hipStream_t st) {
-    if (sigma == 5) launchSearchT<5>(a, edit, count, dim3(blocks), lds, st);
-    else            launchSearchT<6>(a, edit, count, dim3(blocks), lds, st);
+    if (sigma == 5) launchFMT<5>(a, edit, count, dim3(blocks), lds, st);
+    else            launchFMT<6>(a, edit, count, dim3(blocks), lds, st);
+    SH_HIP(hipGetLastError());
+}
+
+void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
+                hipStream_t st) {
+    if (sigma == 5) launchTextT<5>(a, edit, count, dim3(blocks), lds, st);
+    else            launchTextT<6>(a, edit, count, dim3(blocks), lds, st);
+    SH_HIP(hipGetLastError());
+}
+
+void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t* dst,
+                        hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>((npat * patWords + 255) / 256, 65536);
+    hipLaunchKernelGGL(kPackPatterns, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, st, src, npat, m,
+                       patWords, dst);
     SH_HIP(hipGetLastError());
 }
 

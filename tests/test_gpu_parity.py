@@ -195,3 +195,29 @@ def test_medium_scale_parity(gpu_device, k, m, nreads, ref_len):
     found = np.zeros(nreads, bool)
     found[(got["qid"][got["qid"] % 2 == 0] // 2).astype(np.int64)] = True
     assert found.all()
+
+
+def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch):
+    """Occurrences that touch position 0, the last symbol of the text and
+    record delimiters: the text-phase windows are clamped there."""
+    rng = np.random.default_rng(21)
+    recs = random_records(rng, [60, 45, 200, 33, 90], 6)
+    m = 24
+    pats = []
+    for r in recs:
+        pats.append(r[:m])            # record start (incl. text position 0)
+        pats.append(r[len(r) - m:])   # record end (incl. the last text symbol)
+    pats = np.array(pats, np.uint8)
+    pats = np.vstack([pats, mutate_reads(rng, recs, 40, m, 2)])
+    # mutate the boundary patterns too
+    for i in range(0, 10, 3):
+        pats[i, 0] = 1 if pats[i, 0] != 1 else 2
+        pats[i + 1, -1] = 1 if pats[i + 1, -1] != 1 else 2
+    monkeypatch.setenv("SAHARA_TASKCAP", "5")  # also exercises the task-buffer re-run
+    for k in (1, 2, 3):
+        sch = sa.search_scheme("h2-k2", 0, k, m)
+        want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch)[0])
+        gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+        for verify, locate_sa in MODES:
+            gpu.set_mode(verify, locate_sa)
+            assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (k, verify, locate_sa)
