@@ -189,6 +189,10 @@ def main():
                  "rank_nodes_per_read": round(cnt["rank_nodes"] / nreads, 1),
                  "text_nodes_per_read": round(cnt["text_nodes"] / nreads, 1),
                  "conversions_per_read": round(cnt["conversions"] / nreads, 2),
+                 "fm_lane_util": round(cnt["nodes"] / max(1, 64 * cnt["fm_iterations"]), 3),
+                 "text_lane_util": round(cnt["text_active"] / max(1, 64 * cnt["text_iterations"]), 3),
+                 "text_iterations_per_wave": round(cnt["text_iterations"] / max(1, 4 * cnt["search_grid"]), 1),
+                 "text_refill_frac": round(cnt["text_refills"] / max(1, cnt["text_iterations"]), 3),
                  "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
                  "search_ms": round(search_ms_step, 2), "text_ms": round(text_ms / args.steps, 2),
                  "locate_ms": round(locate_ms / args.steps, 2),

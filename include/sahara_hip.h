@@ -75,6 +75,10 @@ typedef struct sahara_stats {
     uint64_t text_nodes;     /* nodes expanded against the resident text (verify mode) */
     uint64_t conversions;    /* text tasks: rows of small intervals handed to the text phase */
     double   text_ms;        /* device time of the text-phase kernels (HIP events) */
+    uint64_t fm_iterations;  /* wave iterations of the FM kernel (count=1) */
+    uint64_t text_iterations;/* wave iterations of the text kernel (count=1) */
+    uint64_t text_active;    /* sum of active lanes over text-kernel iterations (count=1) */
+    uint64_t text_refills;   /* text-kernel iterations that refilled lanes (count=1) */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);
@@ -101,9 +105,9 @@ int  sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* samp
 int  sahara_gpu_export_sa(void* ctx, uint32_t* sa);
 int  sahara_gpu_export_text(void* ctx, uint8_t* text);
 /* Execution mode of the search (default verify = 1, locate_sa = 1):
- *   verify    1: once a DFS node's interval holds at most 4 rows, resolve each
- *             row's text position through the resident SA and continue the
- *             identical DFS against the resident text (text phase);
+ *   verify    1: once a DFS node's interval is a single row (SAHARA_SPLIT rows),
+ *             resolve its text position through the resident SA and continue
+ *             the identical DFS against the resident text (text phase);
  *             0: rank every node on the FM-index.
  *   locate_sa 1: locate rows by one read of the resident SA; 0: LF walk to
  *             the SA samples (fmc::LocateLinear, search.cpp:246).

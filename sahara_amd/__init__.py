@@ -54,7 +54,9 @@ class Stats(C.Structure):
                 ("sort_ms", C.c_double), ("total_ms", C.c_double), ("nodes", C.c_uint64),
                 ("rank_nodes", C.c_uint64), ("ext_lines", C.c_uint64), ("lf_steps", C.c_uint64),
                 ("search_launches", C.c_uint32), ("search_grid", C.c_uint32),
-                ("text_nodes", C.c_uint64), ("conversions", C.c_uint64), ("text_ms", C.c_double)]
+                ("text_nodes", C.c_uint64), ("conversions", C.c_uint64), ("text_ms", C.c_double),
+                ("fm_iterations", C.c_uint64), ("text_iterations", C.c_uint64), ("text_active", C.c_uint64),
+                ("text_refills", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

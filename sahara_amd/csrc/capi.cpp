@@ -46,7 +46,9 @@ struct Ctx {
     bool staged = false;
     bool verify = true;
     bool locateSA = true;
-    uint32_t split = 4;                   // text-phase threshold (rows per interval)
+    uint32_t split = 1;                   // text-phase threshold (rows per interval)
+    uint32_t textSteps = 8;               // text-phase node expansions per lane per wave iteration
+    uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
 
     // work buffers
     DevBuf<uint4> stack, hits, tasks;
@@ -96,8 +98,8 @@ Ctx* newCtx(int device) {
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
     c->small.reserve(8);
-    c->counters.reserve(8);
-    SH_HIP(hipMemset(c->counters.ptr, 0, 8 * sizeof(unsigned long long)));
+    c->counters.reserve(16);
+    SH_HIP(hipMemset(c->counters.ptr, 0, 16 * sizeof(unsigned long long)));
     return c.release();
 }
 
@@ -221,6 +223,9 @@ void run(Ctx* c, bool count) {
     const uint32_t textStack = 2 * c->maxErr + 2;
     const size_t textLds = (size_t)2 * c->nsearch * c->m * 4 +
                            (size_t)256 * ((winWords + 1) + (c->patWords + 1) + 2 * textStack) * 4;
+    if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
+    if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
     int tbpc = 0;
     if (c->verify && c->m <= 4095 && textLds <= 160 * 1024) tbpc = textBlocksPerCU(sigma, c->edit, textLds);
     const uint32_t split = tbpc > 0 ? c->split : 0u;
@@ -237,7 +242,7 @@ void run(Ctx* c, bool count) {
     }
     c->hits.reserve((size_t)c->hitCap + 1);
     c->tasks.reserve((size_t)c->taskCap);
-    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 8 * sizeof(unsigned long long), c->st));
+    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), c->st));
     c->nout = 0;
 
     for (uint64_t q0 = 0; q0 < c->npat; q0 += maxBatch) {
@@ -314,6 +319,8 @@ void run(Ctx* c, bool count) {
                 t.counters = c->counters.ptr;
                 t.winWords = winWords;
                 t.stackCap = textStack;
+                t.steps = c->textSteps;
+                t.refillAt = c->refillAt;
                 SH_HIP(hipEventRecord(c->ev[5], c->st));
                 launchText(t, sigma, c->edit, count, textBlocks, textLds, c->st);
                 SH_HIP(hipEventRecord(c->ev[6], c->st));
@@ -393,7 +400,7 @@ void run(Ctx* c, bool count) {
         S.hits += rows;
     }
     if (count) {
-        unsigned long long h[8];
+        unsigned long long h[16];
         SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, c->st));
         SH_HIP(hipStreamSynchronize(c->st));
         S.nodes = h[0];
@@ -402,6 +409,10 @@ void run(Ctx* c, bool count) {
         S.lf_steps = h[3];
         S.text_nodes = h[5];
         S.conversions = h[6];  // text tasks
+        S.fm_iterations = h[7];
+        S.text_iterations = h[8];
+        S.text_active = h[9];
+        S.text_refills = h[10];
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->stats = S;

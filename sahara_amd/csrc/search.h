@@ -55,6 +55,8 @@ struct TextArgs {
     unsigned long long* counters;
     uint32_t winWords;       // window words per lane (8 symbols each)
     uint32_t stackCap;       // text DFS stack entries per lane
+    uint32_t steps;          // node expansions per lane between wave-level bookkeeping
+    uint32_t refillAt;       // refill idle lanes once this many are idle
 };
 
 struct LocateArgs {

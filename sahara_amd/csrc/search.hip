@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     bool qDone = false;
     SlotRange hitSlots, taskSlots;
     uint4 cur = make_uint4(0, 0, 0, 0);
-    uint64_t cNodes = 0, cRank = 0, cLines = 0, cTasks = 0;
+    uint64_t cNodes = 0, cRank = 0, cLines = 0, cTasks = 0, cIter = 0;
 
     for (;;) {
         // ---- refill idle lanes from the wave's private item range; the wave
@@ -254,6 +254,7 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
             have = true;
         }
         if (!__any(have)) break;
+        if (COUNT && lane == 0) ++cIter;
 
         const uint32_t pos = cur.w & 0xFFFFu;
         // ---- leaves -> hit buffer
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
         if (a.split) {
             const bool conv = have && cur.z <= a.split;
             const uint32_t tlen = pos + metaDelta(cur.w) - 16u;  // |t|
-            for (uint32_t j = 0; j < a.split; ++j) {  // wave-uniform trip count
+            for (uint32_t j = 0; __any(conv && j < cur.z); ++j) {  // wave-uniform trip count
                 const bool want = conv && j < cur.z;
                 uint32_t slot;
                 if (taskSlots.take(want, lane, ltMask, a.taskCount, slot) && want) {
@@ -380,6 +381,7 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
         atomicAdd(a.counters + 1, (unsigned long long)cRank);
         atomicAdd(a.counters + 2, (unsigned long long)cLines);
         atomicAdd(a.counters + 6, (unsigned long long)cTasks);
+        if (cIter) atomicAdd(a.counters + 7, (unsigned long long)cIter);
     }
 }
 
@@ -412,6 +414,7 @@ __device__ __forceinline__ bool equalRun(const uint32_t* P, uint32_t p, const ui
     return true;
 }
 
+
 template <int SIGMA, bool EDIT, bool COUNT>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
@@ -430,23 +433,24 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint32_t* P = slot + (a.winWords + 1u) * 256u + threadIdx.x;
     uint2* S = reinterpret_cast<uint2*>(slot + (a.winWords + a.patWords + 2u) * 256u) + threadIdx.x;
     const uint32_t winLen = a.winWords * 8u;
+    const uint32_t m = a.m;
 
-    uint32_t sp = 0, pid = 0, sIdx = 0, wb = 0, sBase = 0;
+    uint32_t sp = 0, pid = 0, wb = 0, sBase = 0;
     bool have = false, exhausted = false;
     uint32_t qNext = 0, qEnd = 0, filled = 0;
     bool qDone = false;
     SlotRange hitSlots;
     uint2 cur = make_uint2(0, 0);  // x = xo | yo << 16 (window offsets of t's [start, end)), y = meta
-    uint64_t cNodes = 0;
+    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0;
 
     for (;;) {
         // Starting a task costs two dependent global reads (SA, then the
         // window) that stall the whole wave, so idle lanes are refilled in
-        // batches: only once half of the wave is idle (or nothing is left).
+        // batches: once refillAt lanes are idle (or nothing else is left).
         const bool idle = !have && sp == 0 && !exhausted;
         const uint64_t idleMask = __ballot(idle);
         const bool busy = __any(have || sp > 0);
-        const bool refill = !busy || __popcll(idleMask) >= 32;
+        const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
         const bool need = refill && idle;
         uint64_t pending = refill ? idleMask : 0ull;
         while (pending) {  // wave-uniform
@@ -468,12 +472,11 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const uint4 t = a.tasks[qNext + rank];
                 const uint32_t x = a.sa[t.x];
                 pid = t.z;
-                sIdx = t.w >> 24;
-                sBase = sIdx * a.m;
+                sBase = (t.w >> 24) * m;
                 const uint32_t meta = t.w & 0x00FFFFFFu;
                 const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
                 const uint32_t ca = cov[sBase + pos] & 0xFFFu;
-                const uint32_t K = (sch[sBase + a.m - 1] >> 20) & 0xFu;
+                const uint32_t K = (sch[sBase + m - 1] >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
                 wb = (x > left ? x - left : 0u) & ~31u;            // 16-B aligned window start
                 const uint4* src = reinterpret_cast<const uint4*>(a.text4w + (wb >> 3));
@@ -491,98 +494,108 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             qNext += take;
         }
         if (qDone && need && !have) exhausted = true;
-        if (!have && sp > 0) {
-            --sp;
-            cur = S[sp * 256u];
-            have = true;
+        if (!__any(have || sp > 0 || (!exhausted && !qDone))) break;  // nothing left anywhere
+        if (COUNT) {
+            const uint64_t act = __ballot(have || sp > 0);
+            if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
         }
-        if (!__any(have || (!exhausted && sp == 0))) break;  // all lanes exhausted
 
-        const uint32_t pos = cur.y & 0xFFFFu;
-        const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
-        const uint32_t e = (cur.y >> 16) & 0xFu;
-        bool leaf = have && pos == a.m;
-        uint32_t leafStart = xo;
-        uint32_t se = 0, cv = 0;
-        if (have && !leaf) {
-            se = sch[sBase + pos];
-            cv = cov[sBase + pos];
+        // ---- up to a.steps node expansions per lane; a lane stops early
+        // at a leaf (emitted below) or when its subtree is exhausted
+        bool leaf = false;
+        uint32_t leafStart = 0, leafE = 0;
+        for (uint32_t step = 0; step < a.steps; ++step) {
+            if (!have) {
+                if (sp == 0) break;
+                --sp;
+                cur = S[sp * 256u];
+                have = true;
+            }
+            const uint32_t pos = cur.y & 0xFFFFu;
+            const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
+            const uint32_t e = (cur.y >> 16) & 0xFu;
+            if (pos == m) {  // leaf
+                leaf = true; leafStart = xo; leafE = e; have = false;
+                break;
+            }
+            if (COUNT) ++cNodes;
+            // all LDS reads of the node up front
+            const uint32_t se = sch[sBase + pos];
+            const uint32_t cv = cov[sBase + pos];
+            const uint32_t q = se & 0xFFFFu;
+            const uint32_t cq = nib(P[(q >> 3) * 256u], q);
+            const bool right = (se >> 24) & 1u;
+            const uint32_t to = right ? yo : xo - 1u;
+            const bool inside = right ? (yo < winLen) : (xo > 0u);
+            const uint32_t tw = W[((inside ? to : 0u) >> 3) * 256u];
             if ((cv >> 24) == e) {
                 // ---- one-shot: no further error is possible on the remaining
                 // positions -> both remainders must match exactly
-                if (COUNT) ++cNodes;
                 const uint32_t ca = cv & 0xFFFu, cb = (cv >> 12) & 0xFFFu;
-                bool ok = xo >= ca;  // else the occurrence would start before text position 0
-                if (!ok && wb != 0) atomicOr(a.flags, 16u);
-                if (ok && yo + (a.m - cb) > winLen) { atomicOr(a.flags, 16u); ok = false; }
-                ok = ok && equalRun(P, 0, W, xo - ca, ca) && equalRun(P, cb, W, yo, a.m - cb);
-                leaf = ok;
-                leafStart = xo - ca;
-                have = ok;
-            }
-        }
-        {
-            uint32_t s;
-            if (hitSlots.take(leaf, lane, ltMask, a.hitCount, s) && leaf) {
-                if (s < a.hitCap) a.hits[s] = make_uint4(pid, wb + leafStart, 1u, e | kPosKnown);
-                else atomicOr(a.flags, 2u);
+                bool ok = xo >= ca && yo + (m - cb) <= winLen;  // else: before text position 0
+                if (xo < ca && wb != 0) atomicOr(a.flags, 16u);
+                ok = ok && equalRun(P, 0, W, xo - ca, ca) && equalRun(P, cb, W, yo, m - cb);
                 have = false;
-                ++filled;
+                if (ok) { leaf = true; leafStart = xo - ca; leafE = e; break; }
+                continue;
             }
-        }
-        if (have) {
-            if (COUNT) ++cNodes;
             const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
-            const uint32_t q = se & 0xFFFFu, lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
-            const bool right = (se >> 24) & 1u;
-            const uint32_t cq = nib(P[(q >> 3) * 256u], q);
+            const uint32_t lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
             const uint32_t side = right ? lastR : lastL;
             const bool matchOK = lb <= e && e <= ub;
             const bool misOK = lb <= e + 1 && e + 1 <= ub;
             const bool delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
             const bool insOK = EDIT && misOK && side != OP_D;
-            // the text's next symbol on the extension side ('$' / text edge = 0)
-            const uint32_t to = right ? yo : xo - 1u;
-            uint32_t tc = 0;
-            if (right || xo > 0) {
-                if (to < winLen) tc = nib(W[(to >> 3) * 256u], to);
-                else atomicOr(a.flags, 16u);  // window too small (cannot happen)
-            } else if (wb != 0) {
-                atomicOr(a.flags, 16u);
-            }
+            if (!inside && !right && wb != 0) atomicOr(a.flags, 16u);  // window too small (cannot happen)
+            const uint32_t tc = inside ? nib(tw, to) : 0u;  // text's next symbol ('$' / edge = 0)
             // children: the one symbol the text offers (M or S), D with it, I
             const bool sym = tc != 0;
-            const bool isM = sym && tc == cq && matchOK;
-            const bool hasS = sym && tc != cq && misOK;
-            const bool hasD = sym && delOK;
+            const bool okM = sym && tc == cq && matchOK;
+            const bool okS = sym && tc != cq && misOK;
+            const bool okD = sym && delOK;
             const uint32_t nspan = right ? (xo | ((yo + 1u) << 16)) : ((xo - 1u) | (yo << 16));
-            auto meta = [&](uint32_t kind) { return childMeta(pos, e, lastL, lastR, right, 16u, kind) & 0x00FFFFFFu; };
-            const uint32_t nErr = (insOK ? 1u : 0u) + (hasS ? 1u : 0u) + (hasD ? 1u : 0u);
-            auto push = [&](const uint2& v) {
-                if (sp < a.stackCap) S[(sp++) * 256u] = v;
-                else atomicOr(a.flags, 1u);
+            const uint32_t base = (lastL << 20) | (lastR << 22);
+            // lastL/lastR after an op on this side (pos 0 sets both)
+            auto sideMeta = [&](uint32_t op) -> uint32_t {
+                const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
+                const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
+                return (nl << 20) | (nr << 22);
             };
+            (void)base;
+            const uint2 cM = make_uint2(nspan, (pos + 1u) | (e << 16) | sideMeta(OP_MS));
+            const uint2 cS = make_uint2(nspan, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_MS));
+            const uint2 cD = make_uint2(nspan, pos | ((e + 1u) << 16) | sideMeta(OP_D));
+            const uint2 cI = make_uint2(cur.x, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_I));
             // match child below its error siblings; continue with the first
             // error child (I, then S, then D) or, if none, with the match child
-            if (isM && nErr) push(make_uint2(nspan, meta(0)));
-            uint2 next = isM ? make_uint2(nspan, meta(0)) : make_uint2(0, 0);
-            bool kept = isM && !nErr;
-            if (insOK) { next = make_uint2(cur.x, meta(3)); kept = true; }
-            if (hasS) {
-                const uint2 v = make_uint2(nspan, meta(1));
-                if (insOK) push(v); else { next = v; kept = true; }
+            const uint32_t nErr = (insOK ? 1u : 0u) + (okS ? 1u : 0u) + (okD ? 1u : 0u);
+            const uint32_t npush = (okM && nErr ? 1u : 0u) + (insOK && okS ? 1u : 0u) + ((insOK || okS) && okD ? 1u : 0u);
+            if (sp + npush > a.stackCap) { atomicOr(a.flags, 1u); have = false; break; }
+            if (okM && nErr) S[(sp++) * 256u] = cM;
+            if (insOK && okS) S[(sp++) * 256u] = cS;
+            if ((insOK || okS) && okD) S[(sp++) * 256u] = cD;
+            have = nErr || okM;
+            cur = insOK ? cI : (okS ? cS : (okD ? cD : cM));
+        }
+        {
+            uint32_t s;
+            if (hitSlots.take(leaf, lane, ltMask, a.hitCount, s) && leaf) {
+                if (s < a.hitCap) a.hits[s] = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
+                else atomicOr(a.flags, 2u);
+                ++filled;
             }
-            if (hasD) {
-                const uint2 v = make_uint2(nspan, meta(2));
-                if (insOK || hasS) push(v); else { next = v; kept = true; }
-            }
-            have = kept;
-            cur = next;
         }
     }
     hitSlots.close(lane, a.hits, a.hitCap);
     if (filled) atomicAdd(a.filled, filled);  // per-lane counts
-    if (COUNT) atomicAdd(a.counters + 5, (unsigned long long)cNodes);
+    if (COUNT) {
+        atomicAdd(a.counters + 5, (unsigned long long)cNodes);
+        if (lane == 0) {
+            atomicAdd(a.counters + 8, (unsigned long long)tIter);
+            atomicAdd(a.counters + 9, (unsigned long long)tActive);
+            atomicAdd(a.counters + 10, (unsigned long long)tRefill);
+        }
+    }
 }
 
 // ================================================================ locate ====
