@@ -117,10 +117,23 @@ int  sahara_gpu_set_mode(void* ctx, int verify, int locate_sa);
 /* --- search + locate (replaces search.cpp:218-250) ---
  * pi/l/u: the expanded search scheme, n_searches rows of len entries each
  * (fmc::search_scheme::expand output, search.cpp:191; limitToHamming already
- * applied by the caller for edit == 0, search.cpp:226). */
+ * applied by the caller for edit == 0, search.cpp:226).
+ * max_hits > 0 is search_n (search.cpp:228,231): per query at most max_hits
+ * distinct (seq_id, pos), fewest errors first, each once with its minimum e
+ * (upstream's counting rule is unverified). Hits come back sorted by
+ * (qid, seq_id, pos, err) in a buffer released with sahara_gpu_free. */
 int  sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len,
                        const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,
                        int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits);
+/* --search_mode besthits (search_ng21::search_best[_n], search.cpp:233-241):
+ * n_schemes expanded schemes, scheme j covering exactly j errors, stored one
+ * after another in pi/l/u (n_searches[j] rows of len entries each). A pattern's
+ * hits are those of the first j that reports any; edit operations always on
+ * (ng21 is the edit-distance search regardless of -d). max_hits as above. */
+int  sahara_gpu_search_best(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len,
+                            const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                            const uint32_t* n_searches, uint32_t n_schemes, uint32_t max_hits,
+                            sahara_hit** hits, uint64_t* n_hits);
 
 /* Device-resident form of the same path for benchmarking: stage patterns and
  * scheme once, run search+locate+sort with results left in HBM, fetch later. */

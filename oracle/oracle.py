@@ -190,3 +190,26 @@ def bruteforce(records, pats, k, edit=True):
     n = lib().orc_bruteforce(_p(ranks, u8p), _p(lens, u64p), len(lens), _p(pats, u8p),
                              pats.shape[0], pats.shape[1], k, int(edit), C.byref(out))
     return _take(out, n)
+
+
+def search_best(index, pats, schemes, nthreads=1):
+    """search_ng21::search_best over per-exact-j schemes j = 0..k (search.cpp:233-241).
+
+    Restated as: for every pattern, the located hits of the smallest j whose
+    exact-j scheme (expand(generator(j, j), len), edit operations) reports any.
+    schemes: list of (pi, l, u), index j = error count. Returns hits[n, 4]."""
+    pats = np.ascontiguousarray(pats, dtype=np.uint8)
+    todo = np.arange(pats.shape[0], dtype=np.uint64)
+    out = []
+    for sch in schemes:
+        if len(todo) == 0:
+            break
+        h, _ = index.search(pats[todo], sch, edit=True, nthreads=nthreads)
+        if len(h):
+            h = h.copy()
+            h[:, 0] = todo[h[:, 0]]
+            out.append(h)
+            todo = np.setdiff1d(todo, np.unique(h[:, 0]))
+    if not out:
+        return np.zeros((0, 4), np.uint64)
+    return np.concatenate(out)

@@ -79,6 +79,9 @@ EXPORTED = {
     "sahara_gpu_search": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                     C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_uint64)]),
+    "sahara_gpu_search_best": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
+                                         u32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_uint64)]),
     "sahara_gpu_stage": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                    C.c_uint32, C.c_int]),
     "sahara_gpu_run": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
@@ -279,6 +282,33 @@ def search(index, queries, scheme, edit=True, max_hits=0):
     _check(lib().sahara_gpu_search(index._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
                                    _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit), max_hits,
                                    C.byref(out), C.byref(n)))
+    try:
+        if n.value == 0:
+            return np.zeros(0, HIT_DTYPE)
+        raw = (C.c_uint8 * (n.value * HIT_DTYPE.itemsize)).from_address(out.value)
+        return np.frombuffer(raw, dtype=HIT_DTYPE).copy()
+    finally:
+        lib().sahara_gpu_free(out)
+
+
+def search_best(index, queries, schemes, max_hits=0):
+    """fmc::search_ng21::search_best[_n] + LocateLinear (search.cpp:233-250).
+
+    schemes: list of (pi, l, u), entry j being the expanded exact-j scheme
+    (generator(j, j) expanded to len, search.cpp:235-237). Each query gets the
+    hits of the smallest j that reports any. Sorted HIT_DTYPE array."""
+    q = np.ascontiguousarray(queries, dtype=np.uint8)
+    if q.ndim != 2 or q.shape[0] == 0:
+        raise SaharaError("queries must be a non-empty (n_patterns, len) array")
+    pi = np.ascontiguousarray(np.concatenate([s[0] for s in schemes]), dtype=np.uint32)
+    l = np.ascontiguousarray(np.concatenate([s[1] for s in schemes]), dtype=np.uint32)
+    u = np.ascontiguousarray(np.concatenate([s[2] for s in schemes]), dtype=np.uint32)
+    ns = np.array([len(s[0]) for s in schemes], np.uint32)
+    out = C.c_void_p()
+    n = C.c_uint64()
+    _check(lib().sahara_gpu_search_best(index._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
+                                        _p(l, u32p), _p(u, u32p), _p(ns, u32p), len(schemes), max_hits,
+                                        C.byref(out), C.byref(n)))
     try:
         if n.value == 0:
             return np.zeros(0, HIT_DTYPE)

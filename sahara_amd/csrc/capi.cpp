@@ -82,6 +82,45 @@ int guarded(F&& f) {
     return -1;
 }
 
+bool hitLess(const sahara_hit& a, const sahara_hit& b) {
+    if (a.qid != b.qid) return a.qid < b.qid;
+    if (a.seq_id != b.seq_id) return a.seq_id < b.seq_id;
+    if (a.pos != b.pos) return a.pos < b.pos;
+    return a.err < b.err;
+}
+
+// --max_hits n (search_n / search_best_n, search.cpp:228,231,240). Upstream's
+// counting rule is unverifiable offline; policy here: per query,
+// the n distinct text positions (seq_id, pos) with the fewest errors, ties by
+// (seq_id, pos), each reported once with its minimum error count. Input and
+// output are in canonical (qid, seq_id, pos, err) order.
+void limitHits(std::vector<sahara_hit>& v, uint32_t n) {
+    size_t w = 0;
+    std::vector<sahara_hit> q;
+    for (size_t i = 0; i < v.size();) {
+        size_t j = i;
+        q.clear();
+        for (; j < v.size() && v[j].qid == v[i].qid; ++j)
+            if (q.empty() || q.back().seq_id != v[j].seq_id || q.back().pos != v[j].pos) q.push_back(v[j]);
+        if (q.size() > n) {
+            std::stable_sort(q.begin(), q.end(), [](const sahara_hit& a, const sahara_hit& b) { return a.err < b.err; });
+            q.resize(n);
+            std::sort(q.begin(), q.end(), hitLess);
+        }
+        for (auto& h : q) v[w++] = h;
+        i = j;
+    }
+    v.resize(w);
+}
+
+void handOver(const std::vector<sahara_hit>& v, sahara_hit** hits, uint64_t* n_hits) {
+    auto* buf = static_cast<sahara_hit*>(std::malloc(std::max<size_t>(v.size(), 1) * sizeof(sahara_hit)));
+    if (!buf) throw Error("out of host memory for hits");
+    if (!v.empty()) std::memcpy(buf, v.data(), v.size() * sizeof(sahara_hit));
+    *hits = buf;
+    *n_hits = v.size();
+}
+
 Ctx* newCtx(int device) {
     int n = 0;
     SH_HIP(hipGetDeviceCount(&n));
@@ -571,15 +610,63 @@ int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint
                       const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit, uint32_t max_hits,
                       sahara_hit** hits, uint64_t* n_hits) {
     return guarded([&] {
-        if (max_hits != 0) throw Error("--max_hits (search_n) is not implemented in this build yet");
         Ctx* c = ctxOf(ctx);
         stage(c, ranks, n_patterns, len, pi, l, u, n_searches, edit);
         run(c, false);
-        auto* buf = static_cast<sahara_hit*>(std::malloc(std::max<uint64_t>(c->nout, 1) * sizeof(sahara_hit)));
-        if (!buf) throw Error("out of host memory for hits");
-        if (c->nout) SH_HIP(hipMemcpy(buf, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
-        *hits = buf;
-        *n_hits = c->nout;
+        std::vector<sahara_hit> v(c->nout);
+        if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
+        if (max_hits) limitHits(v, max_hits);
+        handOver(v, hits, n_hits);
+    });
+}
+
+int sahara_gpu_search_best(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,
+                           const uint32_t* l, const uint32_t* u, const uint32_t* n_searches, uint32_t n_schemes,
+                           uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (!n_schemes) throw Error("sahara_gpu_search_best: no schemes");
+        // search_ng21::search_best (search.cpp:233-241): scheme j holds exactly j
+        // errors; a pattern leaves the work list at the first j that reports.
+        std::vector<uint64_t> todo(n_patterns);
+        for (uint64_t i = 0; i < n_patterns; ++i) todo[i] = i;
+        std::vector<uint8_t> sub;
+        std::vector<sahara_hit> all;
+        sahara_stats acc{};
+        uint64_t off = 0;
+        for (uint32_t j = 0; j < n_schemes && !todo.empty(); off += (uint64_t)n_searches[j] * len, ++j) {
+            const uint8_t* src = ranks;
+            if (todo.size() != n_patterns) {
+                sub.resize(todo.size() * len);
+                for (size_t i = 0; i < todo.size(); ++i)
+                    std::memcpy(sub.data() + i * len, ranks + todo[i] * len, len);
+                src = sub.data();
+            }
+            stage(c, src, todo.size(), len, pi + off, l + off, u + off, n_searches[j], 1);
+            run(c, false);
+            std::vector<sahara_hit> v(c->nout);
+            if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
+            acc.search_ms += c->stats.search_ms;
+            acc.locate_ms += c->stats.locate_ms;
+            acc.sort_ms += c->stats.sort_ms;
+            acc.total_ms += c->stats.total_ms;
+            acc.hits += c->stats.hits;
+            acc.patterns += c->stats.patterns;
+            std::vector<char> found(todo.size(), 0);
+            for (auto& h : v) {
+                found[h.qid] = 1;
+                h.qid = todo[h.qid];
+            }
+            all.insert(all.end(), v.begin(), v.end());
+            size_t w = 0;
+            for (size_t i = 0; i < todo.size(); ++i)
+                if (!found[i]) todo[w++] = todo[i];
+            todo.resize(w);
+        }
+        c->stats = acc;
+        std::sort(all.begin(), all.end(), hitLess);
+        if (max_hits) limitHits(all, max_hits);
+        handOver(all, hits, n_hits);
     });
 }
 

@@ -1,0 +1,183 @@
+"""The `sahara` CLI (bin/sahara): flags, stdout blocks, output format and exit
+codes of src/sahara/index.cpp and src/sahara/search.cpp, over the golden
+fixtures. Error paths that fail before the device is touched run on CPU."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import hits_as_rows
+from test_golden import CASES, GOLD, IDX, expected, limit_rows
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAHARA = os.path.join(ROOT, "bin", "sahara")
+
+
+def run(*args, cwd=None):
+    if not os.path.exists(SAHARA):
+        pytest.fail("bin/sahara missing: run `make` (or __graft_entry__.build())")
+    p = subprocess.run([SAHARA, *map(str, args)], capture_output=True, text=True, cwd=cwd, timeout=300)
+    return p.returncode, p.stdout, p.stderr
+
+
+def write(path, text):
+    path.write_text(text)
+    return path
+
+
+def test_list_generators():
+    rc, out, _ = run("search_scheme", "list-generators")
+    assert rc == 0
+    names = [line.split(" - ")[0].strip() for line in out.splitlines()]
+    assert {"backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3"} <= set(names)
+
+
+def test_no_command_is_an_error():
+    assert run()[0] == 1
+    assert run("frobnicate")[0] == 1
+
+
+def test_index_rejects_invalid_character(tmp_path):
+    fa = write(tmp_path / "r.fa", ">r1 first\nACGTACGTNNAC\n>r2\nACGXTT\n")
+    rc, out, err = run("index", fa)
+    assert rc == 1
+    assert out.startswith(f"constructing an index for {fa}\n")
+    assert "ref 'r2' (2) has invalid character 'X' (0x58) at position 3" in err
+    assert not (tmp_path / "r.fa.idx").exists()
+
+
+def test_index_dna4_rejects_n(tmp_path):
+    fa = write(tmp_path / "r.fa", ">r1\nACGTNACG\n")
+    rc, _, err = run("index", fa, "--dna4")
+    assert rc == 1 and "invalid character 'N' (0x4e) at position 4" in err
+
+
+def test_index_empty_reference(tmp_path):
+    fa = write(tmp_path / "r.fa", "")
+    rc, _, err = run("index", fa)
+    assert rc == 1 and "was empty - abort" in err
+
+
+def test_search_requires_query_and_index(tmp_path):
+    assert run("search", "-i", os.path.join(GOLD, IDX["a"]))[0] == 1
+    assert run("search", "-q", os.path.join(GOLD, "reads_a.fa"))[0] == 1
+
+
+def test_search_missing_index(tmp_path):
+    rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", tmp_path / "nope.idx")
+    assert rc == 1 and "no valid index path at" in err
+
+
+def test_search_unknown_sigma(tmp_path):
+    bad = tmp_path / "x.idx"
+    bad.write_bytes((7).to_bytes(8, "little") + b"\0" * 64)
+    rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", bad)
+    assert rc == 1 and "unknown index with 7 letters" in err
+
+
+def test_search_invalid_query_character(tmp_path):
+    q = write(tmp_path / "q.fa", ">q1\nACGTACGT\n>q2\nACGTAXGT\n")
+    rc, _, err = run("search", "-q", q, "-i", os.path.join(GOLD, IDX["a"]))
+    assert rc == 1
+    assert "query 'q2' (3) has invalid character at position 5 'X'(58)" in err
+
+
+def test_search_empty_queries(tmp_path):
+    q = write(tmp_path / "q.fa", "")
+    rc, _, err = run("search", "-q", q, "-i", os.path.join(GOLD, IDX["a"]))
+    assert rc == 1 and "was empty - abort" in err
+
+
+def test_search_bad_enum_values():
+    base = ["search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"])]
+    assert run(*base, "-m", "fast")[0] == 1
+    assert run(*base, "-d", "hamming")[0] == 1
+
+
+# ------------------------------------------------------------------ GPU ----
+
+def cli_args(c):
+    a = ["-e", c["k"], "-g", c["generator"], "-d", c["metric"], "-m", c["mode"]]
+    if not c["reverse"]:
+        a.append("--no-reverse")
+    return a
+
+
+def read_hits(path, cols):
+    a = np.loadtxt(path, dtype=np.uint64, ndmin=2)
+    return a.reshape(-1, cols)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixture,extra,name", [("a", [], "ref_a.fa.idx"), ("b", ["--dna4"], "ref_b.fa.dna4.idx")])
+def test_cli_index_writes_golden_bytes(fixture, extra, name, tmp_path, gpu_device):
+    fa = tmp_path / f"ref_{fixture}.fa"
+    shutil.copy(os.path.join(GOLD, f"ref_{fixture}.fa"), fa)
+    rc, out, err = run("index", fa, *extra)
+    assert rc == 0, err
+    assert "  references: " in out and "  index creation time:" in out and "  total time:" in out
+    assert (tmp_path / name).read_bytes() == open(os.path.join(GOLD, name), "rb").read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_cli_search_matches_golden(name, tmp_path, gpu_device):
+    c = CASES[name]
+    out = tmp_path / "hits.txt"
+    rc, so, err = run("search", "-q", os.path.join(GOLD, f"reads_{c['fixture']}.fa"),
+                      "-i", os.path.join(GOLD, IDX[c["fixture"]]), "-o", out, "--emit-errors", *cli_args(c))
+    assert rc == 0, err
+    assert np.array_equal(hits_as_rows(read_hits(out, 4)), expected(name))
+    assert f"  number of hits:      {c['hits']:>10}" in so
+    fwd = c["patterns"] // (2 if c["reverse"] else 1)
+    assert f"fwd queries: {fwd}\nbwd queries: {c['patterns'] - fwd}\n" in so
+    assert so.count("node count: ") == (c["k"] + 1 if c["mode"] == "besthits" else 1)
+
+
+@pytest.mark.gpu
+def test_cli_default_output_format(tmp_path, gpu_device):
+    rc, so, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                      "-e", 2, cwd=tmp_path)
+    assert rc == 0, err
+    rows = read_hits(tmp_path / "sahara-output.txt", 3)      # "qid seqId pos" (search.cpp:258)
+    want = expected("a_lev_k2")[:, :3]
+    assert np.array_equal(rows[np.lexsort(rows.T[::-1])], want[np.lexsort(want.T[::-1])])
+    for line in ("config:", "  query:               ", "  generator:           h2-k2",
+                 "  allowed errors:      2", "  reverse complements: true", "  search mode:         all",
+                 "  max hits:            0", "  output path:         sahara-output.txt", "stats:",
+                 "  ld queries time:", "  ld index time:", "  searchScheme time:", "  search time:",
+                 "  locate time:", "  result time:", "  total time:", "  queries per second:"):
+        assert line in so, line
+
+
+@pytest.mark.gpu
+def test_cli_limit_queries_and_max_hits(tmp_path, gpu_device):
+    out = tmp_path / "h.txt"
+    rc, so, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                      "-e", 2, "--limit_queries", 33, "--max_hits", 2, "--emit-errors", "-o", out)
+    assert rc == 0, err
+    want = expected("a_lev_k2")
+    want = limit_rows(want[want[:, 0] < 33], 2)
+    assert np.array_equal(hits_as_rows(read_hits(out, 4)), want)
+    assert "fwd queries: 16\nbwd queries: 17\n" in so
+
+
+@pytest.mark.gpu
+def test_cli_fm_only_mode(tmp_path, gpu_device):
+    out = tmp_path / "h.txt"
+    rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_b.fa"), "-i", os.path.join(GOLD, IDX["b"]),
+                     "-e", 3, "-g", "h2-k3", "--fm-only", "--emit-errors", "-o", out)
+    assert rc == 0, err
+    assert np.array_equal(hits_as_rows(read_hits(out, 4)), expected("b_lev_k3"))
+
+
+@pytest.mark.gpu
+def test_cli_errors_after_index_load(tmp_path, gpu_device):
+    q = write(tmp_path / "q.fa", ">q1\nACGTACGTAC\n>q2\nACGTAC\n")
+    rc, _, err = run("search", "-q", q, "-i", os.path.join(GOLD, IDX["a"]))
+    assert rc == 1 and "must have the length of the first" in err
+    rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                     "-g", "nope")
+    assert rc == 1 and 'unknown search scheme generetaror "nope"' in err
