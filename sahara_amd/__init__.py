@@ -300,9 +300,10 @@ def search_best(index, queries, schemes, max_hits=0):
     q = np.ascontiguousarray(queries, dtype=np.uint8)
     if q.ndim != 2 or q.shape[0] == 0:
         raise SaharaError("queries must be a non-empty (n_patterns, len) array")
-    pi = np.ascontiguousarray(np.concatenate([s[0] for s in schemes]), dtype=np.uint32)
-    l = np.ascontiguousarray(np.concatenate([s[1] for s in schemes]), dtype=np.uint32)
-    u = np.ascontiguousarray(np.concatenate([s[2] for s in schemes]), dtype=np.uint32)
+    def cat(i):
+        parts = [np.asarray(s[i], np.uint32).ravel() for s in schemes] or [np.zeros(1, np.uint32)]
+        return np.ascontiguousarray(np.concatenate(parts))
+    pi, l, u = cat(0), cat(1), cat(2)
     ns = np.array([len(s[0]) for s in schemes], np.uint32)
     out = C.c_void_p()
     n = C.c_uint64()

@@ -172,8 +172,8 @@ def test_errors_are_loud(gpu_device):
     bad = np.zeros((2, 10), np.uint8)  # rank 0 ('$') is not a query symbol
     with pytest.raises(sa.SaharaError, match="rank out of range"):
         sa.search(gpu, bad, sa.search_scheme("h2-k2", 0, 1, 10))
-    with pytest.raises(sa.SaharaError, match="max_hits"):
-        sa.search(gpu, np.ones((1, 10), np.uint8), sa.search_scheme("h2-k2", 0, 1, 10), max_hits=3)
+    with pytest.raises(sa.SaharaError, match="no schemes"):
+        sa.search_best(gpu, np.ones((1, 10), np.uint8), [])
 
 
 @pytest.mark.parametrize("k,m,nreads,ref_len", [(2, 100, 20000, 2_000_000), (3, 150, 3000, 1_000_000)])
