@@ -193,6 +193,10 @@ def main():
                  "text_lane_util": round(cnt["text_active"] / max(1, 64 * cnt["text_iterations"]), 3),
                  "text_iterations_per_wave": round(cnt["text_iterations"] / max(1, 4 * cnt["search_grid"]), 1),
                  "text_refill_frac": round(cnt["text_refills"] / max(1, cnt["text_iterations"]), 3),
+                 "text_cycle_split": {k: round(cnt[f"text_cycles_{k}"] / max(1, cnt["text_cycles_refill"]
+                                                  + cnt["text_cycles_step"] + cnt["text_cycles_emit"]), 3)
+                                      for k in ("refill", "step", "emit")},
+                 "text_compare_steps_per_read": round(cnt["text_compare_steps"] / nreads, 1),
                  "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
                  "search_ms": round(search_ms_step, 2), "text_ms": round(text_ms / args.steps, 2),
                  "locate_ms": round(locate_ms / args.steps, 2),

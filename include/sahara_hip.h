@@ -79,6 +79,10 @@ typedef struct sahara_stats {
     uint64_t text_iterations;/* wave iterations of the text kernel (count=1) */
     uint64_t text_active;    /* sum of active lanes over text-kernel iterations (count=1) */
     uint64_t text_refills;   /* text-kernel iterations that refilled lanes (count=1) */
+    uint64_t text_cycles_refill; /* shader cycles summed over text-kernel waves: task starts (count=1) */
+    uint64_t text_cycles_step;   /* ... node / compare micro-steps (count=1) */
+    uint64_t text_cycles_emit;   /* ... leaf emission (count=1) */
+    uint64_t text_compare_steps; /* exact-compare micro-steps, lane count (count=1) */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

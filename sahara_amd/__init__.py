@@ -56,7 +56,9 @@ class Stats(C.Structure):
                 ("search_launches", C.c_uint32), ("search_grid", C.c_uint32),
                 ("text_nodes", C.c_uint64), ("conversions", C.c_uint64), ("text_ms", C.c_double),
                 ("fm_iterations", C.c_uint64), ("text_iterations", C.c_uint64), ("text_active", C.c_uint64),
-                ("text_refills", C.c_uint64)]
+                ("text_refills", C.c_uint64), ("text_cycles_refill", C.c_uint64),
+                ("text_cycles_step", C.c_uint64), ("text_cycles_emit", C.c_uint64),
+                ("text_compare_steps", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -256,17 +256,17 @@ void run(Ctx* c, bool count) {
     S.search_grid = blocks;
 
     // text phase geometry (LDS per lane: window | pattern | stack)
-    // window: |t| + what both sides can still consume <= m + 3k symbols, plus
-    // the 16-B alignment of its start (31 symbols); rounded to whole uint4
-    const uint32_t winWords = ((c->m + 3 * c->maxErr + 31 + 8) / 8 + 3) & ~3u;
+    // window: |t| + what both sides can still consume <= m + 2k symbols, plus
+    // the word alignment of its start (7 symbols); an even number of words
+    const uint32_t winWords = ((c->m + 2 * c->maxErr + 7 + 7) / 8 + 1) & ~1u;
     const uint32_t textStack = 2 * c->maxErr + 2;
     const size_t textLds = (size_t)2 * c->nsearch * c->m * 4 +
-                           (size_t)256 * ((winWords + 1) + (c->patWords + 1) + 2 * textStack) * 4;
+                           (size_t)256 * (winWords + c->patWords + 2 * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
     int tbpc = 0;
-    if (c->verify && c->m <= 4095 && textLds <= 160 * 1024) tbpc = textBlocksPerCU(sigma, c->edit, textLds);
+    if (c->verify && c->m <= 2047 && textLds <= 160 * 1024) tbpc = textBlocksPerCU(sigma, c->edit, textLds);
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
 
@@ -367,7 +367,7 @@ void run(Ctx* c, bool count) {
                 SH_HIP(hipStreamSynchronize(c->st));
                 S.text_ms += elapsed(c->ev[5], c->ev[6]);
                 if (hostSmall[2] & 1u) throw Error("text-phase stack overflow (internal bound violated)");
-                if (hostSmall[2] & 16u) throw Error("text-phase window too small (internal bound violated)");
+                if (hostSmall[2] & 16u) throw Error("text phase: internal window/stack bound violated");
                 if (hostSmall[2] & 2u) {
                     const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
                     if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
@@ -452,6 +452,10 @@ void run(Ctx* c, bool count) {
         S.text_iterations = h[8];
         S.text_active = h[9];
         S.text_refills = h[10];
+        S.text_cycles_refill = h[11];
+        S.text_cycles_step = h[12];
+        S.text_cycles_emit = h[13];
+        S.text_compare_steps = h[14];
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->stats = S;

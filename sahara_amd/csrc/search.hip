@@ -387,66 +387,67 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 
 // ========================================================= phase 2: text ====
 //
-// LDS: scheme[S*m] | cover[S*m] | per lane, interleaved so that the lanes of
-// a wave hit consecutive banks at equal offsets:
-//   window  (winWords u32 words of 8 nibbles + 1 pad)   W[j*256 + t]
-//   pattern (patWords u32 words of 8 nibbles + 1 pad)   P[j*256 + t]
-//   stack   (stackCap uint2 entries)                    S[d*256 + t]
+// LDS: {scheme, cover}[S*m] (uint2) | per lane, interleaved so that the lanes
+// of a wave hit consecutive banks at equal offsets:
+//   window  (winWords u32 words of 8 nibbles)   W[j*256 + t]
+//   pattern (patWords u32 words of 8 nibbles)   P[j*256 + t]
+//   stack   (stackCap uint2 entries)            S[d*256 + t]
 // cover entry: a | b << 12 | E << 24 — the covered pattern positions [a, b)
 // before step `pos`, and E = the error count at which every remaining
 // position admits a match only (u == E, l <= E from pos on), 31 if none.
+//
+// A lane's state is one DFS node `cur` (x = window offsets xo | yo << 16 of
+// the text t matched so far, y = meta: pos | e << 16 | lastL << 20 |
+// lastR << 22) or, once cover E == e, an exact compare of the remainders
+// (bit 31 of y, progress in `cj`, geometry in `cw`/`cl`). Every micro-step is
+// straight-line code — one stack read, one table read, two nibble-run reads
+// of pattern and window, up to three stack writes — so the lanes of a wave
+// stay converged whatever mix of nodes and compares they hold.
 
-// 8 consecutive nibbles starting at nibble offset o of an interleaved word array
-__device__ __forceinline__ uint32_t nib8(const uint32_t* A, uint32_t o) {
-    const uint32_t w0 = A[(o >> 3) * 256u], w1 = A[((o >> 3) + 1u) * 256u];
-    const uint32_t sh = (o & 7u) * 4u;
-    return sh ? (w0 >> sh) | (w1 << (32u - sh)) : w0;
+// 8 consecutive nibbles starting at nibble offset o of an interleaved word
+// array of `words` words (reads past the end return garbage in the high
+// nibbles; callers mask them).
+__device__ __forceinline__ uint32_t nib8(const uint32_t* A, uint32_t o, uint32_t words) {
+    const uint32_t i = min(o >> 3, words - 1u);
+    const uint32_t w0 = A[i * 256u], w1 = A[min(i + 1u, words - 1u) * 256u];
+    return __builtin_amdgcn_alignbit(w1, w0, (o & 7u) * 4u);
 }
 
-// pattern[p, p+len) == window[w, w+len) ?
-__device__ __forceinline__ bool equalRun(const uint32_t* P, uint32_t p, const uint32_t* W, uint32_t w,
-                                         uint32_t len) {
-    for (uint32_t i = 0; i < len; i += 8) {
-        const uint32_t n = min(8u, len - i);
-        const uint32_t mask = n == 8 ? 0xFFFFFFFFu : ((1u << (4u * n)) - 1u);
-        if ((nib8(P, p + i) ^ nib8(W, w + i)) & mask) return false;
-    }
-    return true;
-}
-
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x2 u32x2a4 __attribute__((aligned(4)));
 
 template <int SIGMA, bool EDIT, bool COUNT>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
-    uint32_t* sch = lds;
-    uint32_t* cov = lds + a.nsearch * a.m;
-    uint32_t* slot = cov + a.nsearch * a.m;
-    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) {
-        sch[i] = a.scheme[i];
-        cov[i] = a.cover[i];
-    }
+    uint2* SC = reinterpret_cast<uint2*>(lds);
+    uint32_t* slot = lds + 2u * a.nsearch * a.m;
+    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = make_uint2(a.scheme[i], a.cover[i]);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t ltMask = (1ull << lane) - 1ull;
+    const uint32_t winWords = a.winWords, patWords = a.patWords;
     uint32_t* W = slot + threadIdx.x;
-    uint32_t* P = slot + (a.winWords + 1u) * 256u + threadIdx.x;
-    uint2* S = reinterpret_cast<uint2*>(slot + (a.winWords + a.patWords + 2u) * 256u) + threadIdx.x;
-    const uint32_t winLen = a.winWords * 8u;
+    uint32_t* P = slot + winWords * 256u + threadIdx.x;
+    uint2* S = reinterpret_cast<uint2*>(slot + (winWords + patWords) * 256u) + threadIdx.x;
+    const uint32_t winLen = winWords * 8u;
     const uint32_t m = a.m;
 
     uint32_t sp = 0, pid = 0, wb = 0, sBase = 0;
-    bool have = false, exhausted = false;
+    bool have = false, exhausted = false, bad = false;
     uint32_t qNext = 0, qEnd = 0, filled = 0;
     bool qDone = false;
     SlotRange hitSlots;
-    uint2 cur = make_uint2(0, 0);  // x = xo | yo << 16 (window offsets of t's [start, end)), y = meta
-    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0;
+    uint2 cur = make_uint2(0, 0);
+    uint32_t cj = 0, cw = 0, cl = 0;  // compare: progress; left/right window starts; left/right lengths
+    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0;
+    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
 
     for (;;) {
-        // Starting a task costs two dependent global reads (SA, then the
-        // window) that stall the whole wave, so idle lanes are refilled in
-        // batches: once refillAt lanes are idle (or nothing else is left).
+        // Starting a task costs dependent global reads (task, SA, window) that
+        // stall the whole wave, so idle lanes are refilled in batches: once
+        // refillAt lanes are idle (or nothing else is left).
+        if (COUNT) t0 = clock64();
         const bool idle = !have && sp == 0 && !exhausted;
         const uint64_t idleMask = __ballot(idle);
         const bool busy = __any(have || sp > 0);
@@ -475,18 +476,18 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 sBase = (t.w >> 24) * m;
                 const uint32_t meta = t.w & 0x00FFFFFFu;
                 const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
-                const uint32_t ca = cov[sBase + pos] & 0xFFFu;
-                const uint32_t K = (sch[sBase + m - 1] >> 20) & 0xFu;
+                const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
+                const uint32_t K = (SC[sBase + m - 1].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
-                wb = (x > left ? x - left : 0u) & ~31u;            // 16-B aligned window start
-                const uint4* src = reinterpret_cast<const uint4*>(a.text4w + (wb >> 3));
-                for (uint32_t j = 0; j < a.winWords; j += 4) {
-                    const uint4 v = src[j >> 2];
-                    W[j * 256u] = v.x; W[(j + 1) * 256u] = v.y; W[(j + 2) * 256u] = v.z; W[(j + 3) * 256u] = v.w;
+                wb = (x > left ? x - left : 0u) & ~7u;              // word-aligned window start
+                const u32x2a4* src = reinterpret_cast<const u32x2a4*>(a.text4w + (wb >> 3));
+                for (uint32_t j = 0; j < winWords; j += 2) {
+                    const u32x2 v = src[j >> 1];
+                    W[j * 256u] = v.x;
+                    W[(j + 1) * 256u] = v.y;
                 }
-                const uint32_t* ps = a.pats + (size_t)pid * a.patWords;
-                for (uint32_t j = 0; j < a.patWords; ++j) P[j * 256u] = ps[j];
-                P[a.patWords * 256u] = 0u;
+                const uint32_t* ps = a.pats + (size_t)pid * patWords;
+                for (uint32_t j = 0; j < patWords; ++j) P[j * 256u] = ps[j];
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
                 have = true;
             }
@@ -498,84 +499,120 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);
             if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
+            const uint64_t t1 = clock64();
+            cyRefill += t1 - t0;
+            t0 = t1;
         }
 
-        // ---- up to a.steps node expansions per lane; a lane stops early
-        // at a leaf (emitted below) or when its subtree is exhausted
+        // ---- up to a.steps micro-steps per lane; a lane that reaches a leaf
+        // holds it (stalls) until the emission below
         bool leaf = false;
         uint32_t leafStart = 0, leafE = 0;
         for (uint32_t step = 0; step < a.steps; ++step) {
-            if (!have) {
-                if (sp == 0) break;
-                --sp;
-                cur = S[sp * 256u];
-                have = true;
-            }
+            const bool pop = !have && !leaf && sp > 0;
+            const uint2 top = S[(pop ? sp - 1u : 0u) * 256u];
+            if (pop) { cur = top; --sp; have = true; }
+            const bool live = have && !leaf;
+            if (!__any(live)) break;  // wave-uniform
+
             const uint32_t pos = cur.y & 0xFFFFu;
             const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
             const uint32_t e = (cur.y >> 16) & 0xFu;
-            if (pos == m) {  // leaf
-                leaf = true; leafStart = xo; leafE = e; have = false;
-                break;
+            const uint2 sc = SC[sBase + min(pos, m - 1u)];
+            const uint32_t se = sc.x, cv = sc.y;
+            bool cmp = (cur.y >> 31) != 0u;
+
+            // a node at the end of the pattern is a leaf
+            const bool nodeLeaf = live && !cmp && pos == m;
+            // no error left for the remaining positions: switch to the compare
+            const bool toCmp = live && !cmp && pos < m && (cv >> 24) == e;
+            const uint32_t ca = cv & 0xFFFu, cb = (cv >> 12) & 0xFFFu;
+            const bool fits = xo >= ca && yo + (m - cb) <= winLen;  // else: runs off the text
+            bad = bad || (toCmp && xo < ca && wb != 0);
+            if (toCmp) {
+                cw = (xo - ca) | (yo << 16);
+                cl = ca | ((m - cb) << 16);
+                cj = 0;
+                cur.y |= 0x80000000u;
             }
-            if (COUNT) ++cNodes;
-            // all LDS reads of the node up front
-            const uint32_t se = sch[sBase + pos];
-            const uint32_t cv = cov[sBase + pos];
+            cmp = live && (cmp || (toCmp && fits));
+            const bool node = live && !cmp && !toCmp && pos < m;
+
+            // ---- reads of this micro-step: node -> pattern symbol pi[pos] and
+            // the text's next symbol on its side; compare -> two 8-symbol runs
             const uint32_t q = se & 0xFFFFu;
-            const uint32_t cq = nib(P[(q >> 3) * 256u], q);
             const bool right = (se >> 24) & 1u;
-            const uint32_t to = right ? yo : xo - 1u;
-            const bool inside = right ? (yo < winLen) : (xo > 0u);
-            const uint32_t tw = W[((inside ? to : 0u) >> 3) * 256u];
-            if ((cv >> 24) == e) {
-                // ---- one-shot: no further error is possible on the remaining
-                // positions -> both remainders must match exactly
-                const uint32_t ca = cv & 0xFFFu, cb = (cv >> 12) & 0xFFFu;
-                bool ok = xo >= ca && yo + (m - cb) <= winLen;  // else: before text position 0
-                if (xo < ca && wb != 0) atomicOr(a.flags, 16u);
-                ok = ok && equalRun(P, 0, W, xo - ca, ca) && equalRun(P, cb, W, yo, m - cb);
-                have = false;
-                if (ok) { leaf = true; leafStart = xo - ca; leafE = e; break; }
-                continue;
-            }
+            const uint32_t lenA = cl & 0xFFFFu, lenB = cl >> 16, total = lenA + lenB;
+            const bool segA1 = cj < lenA;
+            const uint32_t n1 = min(8u, (segA1 ? lenA : total) - min(cj, total));
+            const uint32_t cj2 = cj + n1;
+            const bool segA2 = cj2 < lenA;
+            const uint32_t n2 = min(8u, (segA2 ? lenA : total) - min(cj2, total));
+            const uint32_t po1 = cmp ? (segA1 ? cj : (m - lenB) + (cj - lenA)) : q;
+            const uint32_t wo1 = cmp ? (segA1 ? (cw & 0xFFFFu) + cj : (cw >> 16) + (cj - lenA))
+                                     : (right ? yo : xo - 1u);
+            const uint32_t po2 = segA2 ? cj2 : (m - lenB) + (cj2 - lenA);
+            const uint32_t wo2 = segA2 ? (cw & 0xFFFFu) + cj2 : (cw >> 16) + (cj2 - lenA);
+            const uint32_t p1 = nib8(P, po1, patWords), w1 = nib8(W, wo1, winWords);
+            const uint32_t p2 = nib8(P, po2, patWords), w2 = nib8(W, wo2, winWords);
+
+            // ---- compare
+            const uint32_t mask1 = n1 >= 8u ? 0xFFFFFFFFu : ((1u << (4u * n1)) - 1u);
+            const uint32_t mask2 = n2 >= 8u ? 0xFFFFFFFFu : ((1u << (4u * n2)) - 1u);
+            const bool same = (((p1 ^ w1) & mask1) | ((p2 ^ w2) & mask2)) == 0u;
+            const bool cmpDone = cmp && same && cj2 + n2 >= total;
+            if (cmp) cj = cj2 + n2;
+
+            // ---- node: children M/S (the text's symbol), D, I under policy P0
             const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
             const uint32_t lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
             const uint32_t side = right ? lastR : lastL;
-            const bool matchOK = lb <= e && e <= ub;
-            const bool misOK = lb <= e + 1 && e + 1 <= ub;
-            const bool delOK = EDIT && pos > 0 && e + 1 <= ub && side != OP_I;
-            const bool insOK = EDIT && misOK && side != OP_D;
-            if (!inside && !right && wb != 0) atomicOr(a.flags, 16u);  // window too small (cannot happen)
-            const uint32_t tc = inside ? nib(tw, to) : 0u;  // text's next symbol ('$' / edge = 0)
-            // children: the one symbol the text offers (M or S), D with it, I
-            const bool sym = tc != 0;
-            const bool okM = sym && tc == cq && matchOK;
+            const bool inside = right ? (yo < winLen) : (xo > 0u);
+            bad = bad || (node && !inside && !right && wb != 0);  // window too small (cannot happen)
+            const uint32_t cq = p1 & 0xFu;
+            const uint32_t tc = inside ? (w1 & 0xFu) : 0u;  // '$' / edge = 0
+            const bool sym = node && tc != 0u;
+            const bool okM = sym && tc == cq && lb <= e && e <= ub;
+            const bool misOK = lb <= e + 1u && e + 1u <= ub;
             const bool okS = sym && tc != cq && misOK;
-            const bool okD = sym && delOK;
+            const bool okD = EDIT && sym && pos > 0u && e + 1u <= ub && side != OP_I;
+            const bool okI = EDIT && node && misOK && side != OP_D;
             const uint32_t nspan = right ? (xo | ((yo + 1u) << 16)) : ((xo - 1u) | (yo << 16));
-            const uint32_t base = (lastL << 20) | (lastR << 22);
-            // lastL/lastR after an op on this side (pos 0 sets both)
+            const uint32_t nl = pos == 0u ? 1u : 0u;  // pos 0 sets both sides
+            const uint32_t keepL = right && !nl ? lastL : 0xFFu, keepR = !right && !nl ? lastR : 0xFFu;
             auto sideMeta = [&](uint32_t op) -> uint32_t {
-                const uint32_t nl = pos == 0 ? op : (right ? lastL : op);
-                const uint32_t nr = pos == 0 ? op : (right ? op : lastR);
-                return (nl << 20) | (nr << 22);
+                return ((keepL == 0xFFu ? op : keepL) << 20) | ((keepR == 0xFFu ? op : keepR) << 22);
             };
-            (void)base;
             const uint2 cM = make_uint2(nspan, (pos + 1u) | (e << 16) | sideMeta(OP_MS));
             const uint2 cS = make_uint2(nspan, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_MS));
             const uint2 cD = make_uint2(nspan, pos | ((e + 1u) << 16) | sideMeta(OP_D));
             const uint2 cI = make_uint2(cur.x, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_I));
             // match child below its error siblings; continue with the first
-            // error child (I, then S, then D) or, if none, with the match child
-            const uint32_t nErr = (insOK ? 1u : 0u) + (okS ? 1u : 0u) + (okD ? 1u : 0u);
-            const uint32_t npush = (okM && nErr ? 1u : 0u) + (insOK && okS ? 1u : 0u) + ((insOK || okS) && okD ? 1u : 0u);
-            if (sp + npush > a.stackCap) { atomicOr(a.flags, 1u); have = false; break; }
-            if (okM && nErr) S[(sp++) * 256u] = cM;
-            if (insOK && okS) S[(sp++) * 256u] = cS;
-            if ((insOK || okS) && okD) S[(sp++) * 256u] = cD;
-            have = nErr || okM;
-            cur = insOK ? cI : (okS ? cS : (okD ? cD : cM));
+            // error child (I, then S, then D) or, if none, with the match child.
+            // Unconditional stores: slots above the new top are scratch (the
+            // stack never exceeds 2k entries, stackCap = 2k + 2).
+            const uint32_t nErr = (okI ? 1u : 0u) + (okS ? 1u : 0u) + (okD ? 1u : 0u);
+            const uint32_t pa = okM && nErr ? 1u : 0u, pb = okI && okS ? 1u : 0u;
+            const uint32_t pc = (okI || okS) && okD ? 1u : 0u;
+            bad = bad || (sp + pa + pb + pc > a.stackCap);
+            const uint32_t spw = min(sp, a.stackCap - 1u);
+            S[spw * 256u] = cM;
+            S[min(spw + pa, a.stackCap - 1u) * 256u] = cS;
+            S[min(spw + pa + pb, a.stackCap - 1u) * 256u] = cD;
+            if (node) sp = min(sp + pa + pb + pc, a.stackCap);
+
+            // ---- next state
+            const bool leafNow = nodeLeaf || cmpDone;
+            if (leafNow) { leaf = true; leafStart = cmp ? (cw & 0xFFFFu) : xo; leafE = e; }
+            const bool cont = node ? (nErr != 0u || okM) : (cmp && same && !cmpDone);
+            if (node) cur = okI ? cI : (okS ? cS : (okD ? cD : cM));
+            if (live) have = cont;
+            if (COUNT) { cNodes += node ? 1u : 0u; cCmp += cmp ? 1u : 0u; }
+        }
+        if (COUNT) {
+            const uint64_t t1 = clock64();
+            cyStep += t1 - t0;
+            t0 = t1;
         }
         {
             uint32_t s;
@@ -585,16 +622,22 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 ++filled;
             }
         }
+        if (COUNT) cyEmit += clock64() - t0;
     }
     hitSlots.close(lane, a.hits, a.hitCap);
     if (filled) atomicAdd(a.filled, filled);  // per-lane counts
+    if (__any(bad) && lane == 0) atomicOr(a.flags, 16u);
     if (COUNT) {
         atomicAdd(a.counters + 5, (unsigned long long)cNodes);
         if (lane == 0) {
             atomicAdd(a.counters + 8, (unsigned long long)tIter);
             atomicAdd(a.counters + 9, (unsigned long long)tActive);
             atomicAdd(a.counters + 10, (unsigned long long)tRefill);
+            atomicAdd(a.counters + 11, (unsigned long long)cyRefill);
+            atomicAdd(a.counters + 12, (unsigned long long)cyStep);
+            atomicAdd(a.counters + 13, (unsigned long long)cyEmit);
         }
+        atomicAdd(a.counters + 14, (unsigned long long)cCmp);
     }
 }
 
