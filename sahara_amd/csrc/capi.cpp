@@ -39,7 +39,7 @@ struct Ctx {
     DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern
     uint64_t npat = 0;
     uint32_t m = 0, patWords = 0;
-    DevBuf<uint32_t> scheme, cover;
+    DevBuf<uint32_t> scheme, cover;        // FM scheme table; text table (textTable)
     uint32_t nsearch = 0;
     uint32_t maxErr = 0;
     bool edit = true;
@@ -178,26 +178,29 @@ void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, u
     }
 }
 
-// cover[s*m + pos] = a | b << 12 | E << 24: pattern positions [a, b) covered
-// before step pos, and E such that every remaining position admits a match
-// only at error count E (u == E and l <= E from pos to the end), else 31.
-void coverTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
-                std::vector<uint32_t>& out) {
-    out.assign((size_t)ns * m, 0);
+// Text-phase table, two words per (search, pos):
+//   x = packScheme(...) | run << 25 — run = number of consecutive positions
+//       from pos (<= 127) on the same side with u == u[pos] and l <= u[pos]:
+//       a node at pos with e == u[pos] has no error child anywhere in that
+//       run, so the DFS is a forced chain of matches through it;
+//   y = a | b << 12 — pattern positions [a, b) covered before step pos.
+void textTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
+               const std::vector<uint32_t>& packed, std::vector<uint32_t>& out) {
+    out.assign((size_t)ns * m * 2, 0);
     for (uint32_t s = 0; s < ns; ++s) {
         const uint32_t* P = pi + (size_t)s * m;
         const uint32_t* L = l + (size_t)s * m;
         const uint32_t* U = u + (size_t)s * m;
+        const uint32_t* Q = packed.data() + (size_t)s * m;
         uint32_t a = P[0], b = P[0];
-        const uint32_t K = U[m - 1];
-        bool valid = true;
-        std::vector<uint32_t> E(m);
-        for (uint32_t p = m; p-- > 0;) {
-            valid = valid && U[p] == K && L[p] <= K;
-            E[p] = valid ? K : 31u;
-        }
         for (uint32_t p = 0; p < m; ++p) {
-            out[(size_t)s * m + p] = a | (b << 12) | (E[p] << 24);
+            const uint32_t right = (Q[p] >> 24) & 1u;
+            uint32_t run = 1;
+            while (run < 127 && p + run < m && ((Q[p + run] >> 24) & 1u) == right && U[p + run] == U[p] &&
+                   L[p + run] <= U[p])
+                ++run;
+            out[((size_t)s * m + p) * 2] = Q[p] | (run << 25);
+            out[((size_t)s * m + p) * 2 + 1] = a | (b << 12);
             a = std::min(a, P[p]);
             b = std::max(b, P[p] + 1);
         }
@@ -213,13 +216,13 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     if (ns > 255) throw Error("at most 255 searches per scheme");
     for (uint64_t i = 0; i < npat * m; ++i)
         if (ranks[i] == 0 || ranks[i] >= c->I.sigma) throw Error("pattern rank out of range for this index");
-    coverTable(pi, l, u, ns, m, cover);
+    textTable(pi, l, u, ns, m, packed, cover);
     c->patWords = (m + 7) / 8;
     {
         DevBuf<uint8_t> raw;
         raw.reserve(npat * m);
         SH_HIP(hipMemcpyAsync(raw.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
-        c->pats.reserve(npat * c->patWords);
+        c->pats.reserve(npat * c->patWords + 4);  // + tail words read by paired loads
         launchPackPatterns(raw.ptr, npat, m, c->patWords, c->pats.ptr, c->st);
         SH_HIP(hipStreamSynchronize(c->st));
     }
@@ -345,8 +348,7 @@ void run(Ctx* c, bool count) {
                 t.patWords = c->patWords;
                 t.m = c->m;
                 t.nsearch = c->nsearch;
-                t.scheme = c->scheme.ptr;
-                t.cover = c->cover.ptr;
+                t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
                 t.tasks = c->tasks.ptr;
                 t.ntasks = ntasks;
                 t.work = c->small.ptr + 5;
@@ -361,6 +363,7 @@ void run(Ctx* c, bool count) {
                 t.steps = c->textSteps;
                 t.refillAt = c->refillAt;
                 SH_HIP(hipEventRecord(c->ev[5], c->st));
+                launchResolveTasks(c->tasks.ptr, ntasks, c->I.saFull.ptr, c->st);
                 launchText(t, sigma, c->edit, count, textBlocks, textLds, c->st);
                 SH_HIP(hipEventRecord(c->ev[6], c->st));
                 SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));

@@ -36,14 +36,13 @@ struct SearchArgs {
 };
 
 struct TextArgs {
-    const uint32_t* sa;      // full SA
+    const uint32_t* sa;      // full SA (tasks arrive resolved by launchResolveTasks)
     const uint32_t* text4w;  // 4-bit packed text as u32 words (8 symbols each)
     const uint32_t* pats;
     uint32_t patWords;
     uint32_t m;
     uint32_t nsearch;
-    const uint32_t* scheme;
-    const uint32_t* cover;   // nsearch * m: a | b << 12 | E << 24
+    const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
     const uint4* tasks;
     uint32_t ntasks;
     uint32_t* work;
@@ -78,6 +77,7 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
+void launchResolveTasks(uint4* tasks, uint32_t n, const uint32_t* sa, hipStream_t st);
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t* dst,
                         hipStream_t st);
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,

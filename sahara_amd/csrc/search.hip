@@ -387,41 +387,71 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 
 // ========================================================= phase 2: text ====
 //
-// LDS: {scheme, cover}[S*m] (uint2) | per lane, interleaved so that the lanes
-// of a wave hit consecutive banks at equal offsets:
+// LDS: table[S*m] (uint2: packed scheme | run << 25, covered [a, b)) | per
+// lane, interleaved so that the lanes of a wave hit consecutive banks at
+// equal offsets:
 //   window  (winWords u32 words of 8 nibbles)   W[j*256 + t]
 //   pattern (patWords u32 words of 8 nibbles)   P[j*256 + t]
 //   stack   (stackCap uint2 entries)            S[d*256 + t]
-// cover entry: a | b << 12 | E << 24 — the covered pattern positions [a, b)
-// before step `pos`, and E = the error count at which every remaining
-// position admits a match only (u == E, l <= E from pos on), 31 if none.
 //
 // A lane's state is one DFS node `cur` (x = window offsets xo | yo << 16 of
-// the text t matched so far, y = meta: pos | e << 16 | lastL << 20 |
-// lastR << 22) or, once cover E == e, an exact compare of the remainders
-// (bit 31 of y, progress in `cj`, geometry in `cw`/`cl`). Every micro-step is
-// straight-line code — one stack read, one table read, two nibble-run reads
-// of pattern and window, up to three stack writes — so the lanes of a wave
-// stay converged whatever mix of nodes and compares they hold.
+// the text t matched so far, y = pos | e << 16 | lastL << 20 | lastR << 22).
+// Every micro-step is straight-line code — one stack read, one table read,
+// one 16-symbol read of pattern and of window, three stack writes — so the
+// lanes of a wave stay converged. A node with e == u[pos] has no error child
+// in the forced run of positions that follows it (table `run`), so it takes
+// up to 16 forced matches at once: the DFS visits the same chain of nodes,
+// one micro-step per 16 of them.
 
-// 8 consecutive nibbles starting at nibble offset o of an interleaved word
+// 16 consecutive nibbles starting at nibble offset o of an interleaved word
 // array of `words` words (reads past the end return garbage in the high
 // nibbles; callers mask them).
-__device__ __forceinline__ uint32_t nib8(const uint32_t* A, uint32_t o, uint32_t words) {
+__device__ __forceinline__ uint64_t nib16(const uint32_t* A, uint32_t o, uint32_t words) {
     const uint32_t i = min(o >> 3, words - 1u);
-    const uint32_t w0 = A[i * 256u], w1 = A[min(i + 1u, words - 1u) * 256u];
-    return __builtin_amdgcn_alignbit(w1, w0, (o & 7u) * 4u);
+    const uint32_t w0 = A[i * 256u], w1 = A[min(i + 1u, words - 1u) * 256u], w2 = A[min(i + 2u, words - 1u) * 256u];
+    const uint32_t sh = (o & 7u) * 4u;
+    return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef u32x2 u32x2a4 __attribute__((aligned(4)));
+
+// Copy two word arrays (window, pattern) from global memory into this lane's
+// interleaved LDS slots: all loads of a 16-word block are issued before the
+// first store, so a task start costs one memory round trip for m <~ 110.
+__device__ __forceinline__ void copyPair(uint32_t* DA, const u32x2a4* A, uint32_t na, uint32_t* DB,
+                                         const u32x2a4* B, uint32_t nb) {
+    const uint32_t n = max(na, nb);
+    for (uint32_t b = 0; b < n; b += 16) {
+        u32x2 va[8], vb[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t j = b + 2u * i;
+            if (j < na) va[i] = A[j >> 1];
+            if (j < nb) vb[i] = B[j >> 1];
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t j = b + 2u * i;
+            if (j < na) { DA[j * 256u] = va[i].x; if (j + 1u < na) DA[(j + 1u) * 256u] = va[i].y; }
+            if (j < nb) { DB[j * 256u] = vb[i].x; if (j + 1u < nb) DB[(j + 1u) * 256u] = vb[i].y; }
+        }
+    }
+}
+
+// Text tasks carry an SA row; replace it by its text position (one SA read
+// per task, fully parallel) so the text kernel starts a task with one round trip.
+__global__ void kResolveTasks(uint4* __restrict__ tasks, uint32_t n, const uint32_t* __restrict__ sa) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        tasks[i].x = sa[tasks[i].x];
+}
 
 template <int SIGMA, bool EDIT, bool COUNT>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     uint2* SC = reinterpret_cast<uint2*>(lds);
     uint32_t* slot = lds + 2u * a.nsearch * a.m;
-    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = make_uint2(a.scheme[i], a.cover[i]);
+    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = a.table[i];
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -437,15 +467,32 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     bool have = false, exhausted = false, bad = false;
     uint32_t qNext = 0, qEnd = 0, filled = 0;
     bool qDone = false;
+    // task chunks: the current one's records (one per lane) and the next one's,
+    // prefetched a chunk ahead so a refill needs no dependent task read
+    uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
+    uint32_t nBase = 0, nEnd = 0, qBase = 0;
+    bool haveNext = false;
+    {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(a.work, kTaskChunk);
+        base = __shfl(base, 0);
+        if (base < a.ntasks) {
+            nBase = base;
+            nEnd = min(base + kTaskChunk, a.ntasks);
+            if (base + lane < nEnd) nextRec = a.tasks[base + lane];
+            haveNext = true;
+        } else {
+            qDone = true;
+        }
+    }
     SlotRange hitSlots;
     uint2 cur = make_uint2(0, 0);
-    uint32_t cj = 0, cw = 0, cl = 0;  // compare: progress; left/right window starts; left/right lengths
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
 
     for (;;) {
-        // Starting a task costs dependent global reads (task, SA, window) that
-        // stall the whole wave, so idle lanes are refilled in batches: once
+        // Starting a task costs a global round trip (window + pattern) that
+        // stalls the whole wave, so idle lanes are refilled in batches: once
         // refillAt lanes are idle (or nothing else is left).
         if (COUNT) t0 = clock64();
         const bool idle = !have && sp == 0 && !exhausted;
@@ -456,46 +503,58 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         uint64_t pending = refill ? idleMask : 0ull;
         while (pending) {  // wave-uniform
             if (qNext >= qEnd) {
-                if (qDone) break;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(a.work, kTaskChunk);
-                base = __shfl(base, 0);
-                if (base >= a.ntasks) { qDone = true; break; }
-                qNext = base;
-                qEnd = min(base + kTaskChunk, a.ntasks);
+                // switch to the prefetched chunk, prefetch the one after it
+                if (!haveNext) break;
+                qBase = nBase;
+                qNext = nBase;
+                qEnd = nEnd;
+                curRec = nextRec;
+                haveNext = false;
+                if (!qDone) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(a.work, kTaskChunk);
+                    base = __shfl(base, 0);
+                    if (base >= a.ntasks) {
+                        qDone = true;
+                    } else {
+                        nBase = base;
+                        nEnd = min(base + kTaskChunk, a.ntasks);
+                        if (base + lane < nEnd) nextRec = a.tasks[base + lane];
+                        haveNext = true;
+                    }
+                }
+                if (qNext >= qEnd) continue;
             }
             const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
             const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
             const bool mine = ((pending >> lane) & 1ull) && rank < take;
+            // the chunk's task records sit one per lane: fetch ours by shuffle
+            const uint32_t srcLane = (qNext - qBase + rank) & 63u;
+            const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
+                                       __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
             if (mine) {
-                // ---- start a task: resolve the row's text position (full SA),
-                // copy the pattern and the text window its subtree can reach
-                const uint4 t = a.tasks[qNext + rank];
-                const uint32_t x = a.sa[t.x];
+                // ---- start a task (x = its text position, resolved by
+                // kResolveTasks): copy the pattern and the text window its
+                // subtree can reach
+                const uint32_t x = t.x;
                 pid = t.z;
                 sBase = (t.w >> 24) * m;
                 const uint32_t meta = t.w & 0x00FFFFFFu;
                 const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
                 const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
-                const uint32_t K = (SC[sBase + m - 1].x >> 20) & 0xFu;
+                const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
                 wb = (x > left ? x - left : 0u) & ~7u;              // word-aligned window start
-                const u32x2a4* src = reinterpret_cast<const u32x2a4*>(a.text4w + (wb >> 3));
-                for (uint32_t j = 0; j < winWords; j += 2) {
-                    const u32x2 v = src[j >> 1];
-                    W[j * 256u] = v.x;
-                    W[(j + 1) * 256u] = v.y;
-                }
-                const uint32_t* ps = a.pats + (size_t)pid * patWords;
-                for (uint32_t j = 0; j < patWords; ++j) P[j * 256u] = ps[j];
+                copyPair(W, reinterpret_cast<const u32x2a4*>(a.text4w + (wb >> 3)), winWords, P,
+                         reinterpret_cast<const u32x2a4*>(a.pats + (size_t)pid * patWords), patWords);
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
                 have = true;
             }
             pending &= ~__ballot(mine);
             qNext += take;
         }
-        if (qDone && need && !have) exhausted = true;
-        if (!__any(have || sp > 0 || (!exhausted && !qDone))) break;  // nothing left anywhere
+        if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
+        if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);
             if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
@@ -518,72 +577,47 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t pos = cur.y & 0xFFFFu;
             const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
             const uint32_t e = (cur.y >> 16) & 0xFu;
-            const uint2 sc = SC[sBase + min(pos, m - 1u)];
-            const uint32_t se = sc.x, cv = sc.y;
-            bool cmp = (cur.y >> 31) != 0u;
-
-            // a node at the end of the pattern is a leaf
-            const bool nodeLeaf = live && !cmp && pos == m;
-            // no error left for the remaining positions: switch to the compare
-            const bool toCmp = live && !cmp && pos < m && (cv >> 24) == e;
-            const uint32_t ca = cv & 0xFFFu, cb = (cv >> 12) & 0xFFFu;
-            const bool fits = xo >= ca && yo + (m - cb) <= winLen;  // else: runs off the text
-            bad = bad || (toCmp && xo < ca && wb != 0);
-            if (toCmp) {
-                cw = (xo - ca) | (yo << 16);
-                cl = ca | ((m - cb) << 16);
-                cj = 0;
-                cur.y |= 0x80000000u;
-            }
-            cmp = live && (cmp || (toCmp && fits));
-            const bool node = live && !cmp && !toCmp && pos < m;
-
-            // ---- reads of this micro-step: node -> pattern symbol pi[pos] and
-            // the text's next symbol on its side; compare -> two 8-symbol runs
-            const uint32_t q = se & 0xFFFFu;
-            const bool right = (se >> 24) & 1u;
-            const uint32_t lenA = cl & 0xFFFFu, lenB = cl >> 16, total = lenA + lenB;
-            const bool segA1 = cj < lenA;
-            const uint32_t n1 = min(8u, (segA1 ? lenA : total) - min(cj, total));
-            const uint32_t cj2 = cj + n1;
-            const bool segA2 = cj2 < lenA;
-            const uint32_t n2 = min(8u, (segA2 ? lenA : total) - min(cj2, total));
-            const uint32_t po1 = cmp ? (segA1 ? cj : (m - lenB) + (cj - lenA)) : q;
-            const uint32_t wo1 = cmp ? (segA1 ? (cw & 0xFFFFu) + cj : (cw >> 16) + (cj - lenA))
-                                     : (right ? yo : xo - 1u);
-            const uint32_t po2 = segA2 ? cj2 : (m - lenB) + (cj2 - lenA);
-            const uint32_t wo2 = segA2 ? (cw & 0xFFFFu) + cj2 : (cw >> 16) + (cj2 - lenA);
-            const uint32_t p1 = nib8(P, po1, patWords), w1 = nib8(W, wo1, winWords);
-            const uint32_t p2 = nib8(P, po2, patWords), w2 = nib8(W, wo2, winWords);
-
-            // ---- compare
-            const uint32_t mask1 = n1 >= 8u ? 0xFFFFFFFFu : ((1u << (4u * n1)) - 1u);
-            const uint32_t mask2 = n2 >= 8u ? 0xFFFFFFFFu : ((1u << (4u * n2)) - 1u);
-            const bool same = (((p1 ^ w1) & mask1) | ((p2 ^ w2) & mask2)) == 0u;
-            const bool cmpDone = cmp && same && cj2 + n2 >= total;
-            if (cmp) cj = cj2 + n2;
-
-            // ---- node: children M/S (the text's symbol), D, I under policy P0
             const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
+            const uint32_t se = SC[sBase + min(pos, m - 1u)].x;
+            const uint32_t q = se & 0xFFFFu;
             const uint32_t lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
+            const bool right = (se >> 24) & 1u;
+            const uint32_t run = se >> 25;
+
+            const bool atLeaf = live && pos == m;
+            const bool node = live && pos < m;
+            const bool forced = e == ub;  // no error child at this position or the rest of its run
+            const uint32_t n = forced ? min(run, 16u) : 1u;
+            // pattern positions [q, q+n) (right) or (q-n, q] (left); text the
+            // same number of symbols beyond the span on that side
+            const uint32_t po = right ? q : q + 1u - n;
+            const uint32_t wo = right ? yo : xo - n;
+            const bool inside = right ? (yo + n <= winLen) : (xo >= n);
+            bad = bad || (node && !inside && (right || wb != 0));  // window too small (cannot happen)
+            const uint64_t pv = nib16(P, po, patWords), wv = nib16(W, wo, winWords);
+            const uint64_t mask = n >= 16u ? ~0ull : ((1ull << (4u * n)) - 1ull);
+
+            // forced run: all n symbols must match ('$' / padding never does)
+            const bool runOK = node && forced && inside && ((pv ^ wv) & mask) == 0ull;
+            // single node (not forced): children M/S (the text's symbol), D, I under policy P0
+            const uint32_t cq = (uint32_t)pv & 0xFu;
+            const uint32_t tc = inside ? ((uint32_t)wv & 0xFu) : 0u;
+            const bool one = node && !forced;
             const uint32_t side = right ? lastR : lastL;
-            const bool inside = right ? (yo < winLen) : (xo > 0u);
-            bad = bad || (node && !inside && !right && wb != 0);  // window too small (cannot happen)
-            const uint32_t cq = p1 & 0xFu;
-            const uint32_t tc = inside ? (w1 & 0xFu) : 0u;  // '$' / edge = 0
-            const bool sym = node && tc != 0u;
+            const bool sym = one && tc != 0u;
             const bool okM = sym && tc == cq && lb <= e && e <= ub;
             const bool misOK = lb <= e + 1u && e + 1u <= ub;
             const bool okS = sym && tc != cq && misOK;
             const bool okD = EDIT && sym && pos > 0u && e + 1u <= ub && side != OP_I;
-            const bool okI = EDIT && node && misOK && side != OP_D;
-            const uint32_t nspan = right ? (xo | ((yo + 1u) << 16)) : ((xo - 1u) | (yo << 16));
-            const uint32_t nl = pos == 0u ? 1u : 0u;  // pos 0 sets both sides
+            const bool okI = EDIT && one && misOK && side != OP_D;
+            const uint32_t adv = runOK ? n : 1u;
+            const uint32_t nspan = right ? (xo | ((yo + adv) << 16)) : ((xo - adv) | (yo << 16));
+            const bool nl = pos == 0u;  // pos 0 sets both sides
             const uint32_t keepL = right && !nl ? lastL : 0xFFu, keepR = !right && !nl ? lastR : 0xFFu;
             auto sideMeta = [&](uint32_t op) -> uint32_t {
                 return ((keepL == 0xFFu ? op : keepL) << 20) | ((keepR == 0xFFu ? op : keepR) << 22);
             };
-            const uint2 cM = make_uint2(nspan, (pos + 1u) | (e << 16) | sideMeta(OP_MS));
+            const uint2 cM = make_uint2(nspan, (pos + adv) | (e << 16) | sideMeta(OP_MS));
             const uint2 cS = make_uint2(nspan, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_MS));
             const uint2 cD = make_uint2(nspan, pos | ((e + 1u) << 16) | sideMeta(OP_D));
             const uint2 cI = make_uint2(cur.x, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_I));
@@ -595,19 +629,17 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t pa = okM && nErr ? 1u : 0u, pb = okI && okS ? 1u : 0u;
             const uint32_t pc = (okI || okS) && okD ? 1u : 0u;
             bad = bad || (sp + pa + pb + pc > a.stackCap);
-            const uint32_t spw = min(sp, a.stackCap - 1u);
+            const uint32_t cap1 = a.stackCap - 1u;
+            const uint32_t spw = min(sp, cap1);
             S[spw * 256u] = cM;
-            S[min(spw + pa, a.stackCap - 1u) * 256u] = cS;
-            S[min(spw + pa + pb, a.stackCap - 1u) * 256u] = cD;
-            if (node) sp = min(sp + pa + pb + pc, a.stackCap);
+            S[min(spw + pa, cap1) * 256u] = cS;
+            S[min(spw + pa + pb, cap1) * 256u] = cD;
+            sp = min(sp + pa + pb + pc, a.stackCap);
 
-            // ---- next state
-            const bool leafNow = nodeLeaf || cmpDone;
-            if (leafNow) { leaf = true; leafStart = cmp ? (cw & 0xFFFFu) : xo; leafE = e; }
-            const bool cont = node ? (nErr != 0u || okM) : (cmp && same && !cmpDone);
+            if (atLeaf) { leaf = true; leafStart = xo; leafE = e; }
             if (node) cur = okI ? cI : (okS ? cS : (okD ? cD : cM));
-            if (live) have = cont;
-            if (COUNT) { cNodes += node ? 1u : 0u; cCmp += cmp ? 1u : 0u; }
+            if (live) have = runOK || nErr != 0u || okM;
+            if (COUNT) { cNodes += one ? 1u : 0u; cCmp += (node && forced) ? 1u : 0u; }
         }
         if (COUNT) {
             const uint64_t t1 = clock64();
@@ -804,6 +836,13 @@ void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32
                 hipStream_t st) {
     if (sigma == 5) launchTextT<5>(a, edit, count, dim3(blocks), lds, st);
     else            launchTextT<6>(a, edit, count, dim3(blocks), lds, st);
+    SH_HIP(hipGetLastError());
+}
+
+void launchResolveTasks(uint4* tasks, uint32_t n, const uint32_t* sa, hipStream_t st) {
+    if (!n) return;
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(kResolveTasks, dim3(blocks), dim3(256), 0, st, tasks, n, sa);
     SH_HIP(hipGetLastError());
 }
 
