@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
+                    help="measured HBM bytes per launch per kernel (tools/profile.sh + tools/pmc_summary.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,13 +158,9 @@ def main():
     digest = idx.digest()
 
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        rec = torch.tensor([nh, digest & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64, device="cuda")
-        allrec = [torch.zeros_like(rec) for _ in range(world)]
-        dist.all_gather(allrec, rec)  # RCCL over xGMI: per-rank hit counts + digests
-        total_hits = int(sum(int(r[0]) for r in allrec))
+        from sahara_amd.dist import max_over_ranks, sum_over_ranks
+        elapsed = max_over_ranks(elapsed, device="cuda")  # RCCL over xGMI
+        total_hits = sum_over_ranks(nh, device="cuda")
     else:
         total_hits = nh
 
@@ -178,12 +176,32 @@ def main():
     roofline = None
     extra = {}
     if cnt:
-        search_bytes = 64.0 * cnt["ext_lines"] + pats.size  # Occ lines + pattern bytes
-        locate_bytes = 64.0 * (cnt["lf_steps"] + 2 * cnt["hits"])  # LF lines + final line + sample
-        achieved = search_bytes / (search_ms_step / 1e3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
-        extra = {"bytes_per_read": round((search_bytes + locate_bytes) / nreads, 1),
+        # algorithmic bytes per step: FM = 64-B Occ lines touched
+        # + pattern bytes; text = per task its window, packed pattern, task
+        # record and SA entry; locate = one SA read per FM-located row
+        search_bytes = 64.0 * cnt["ext_lines"] + pats.size
+        win_words = ((rlen + 2 * k + 14) // 8 + 1) & ~1
+        pat_words = (rlen + 7) // 8
+        text_bytes = cnt["conversions"] * (4.0 * (win_words + pat_words) + 16 + 4)
+        locate_bytes = 4.0 * cnt["hits"]
+        text_ms_step = text_ms / args.steps
+        kern = {"kSearchFM": {"ms": round(search_ms_step, 2), "bytes": search_bytes,
+                              "GBs": round(search_bytes / (search_ms_step / 1e3) / 1e9, 1)},
+                "kSearchText": {"ms": round(text_ms_step, 2), "bytes": text_bytes,
+                                "GBs": round(text_bytes / max(text_ms_step, 1e-6) * 1e3 / 1e9, 1)}}
+        dom = max(kern, key=lambda n: kern[n]["ms"])
+        achieved = kern[dom]["GBs"]
+        per_launch = max(1, launches // args.steps)  # one FM and one text launch per batch
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "algorithmic_bytes_per_launch": round(kern[dom]["bytes"] / per_launch)}
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            tr = json.load(open(args.traffic_json)).get(dom)
+            if tr:
+                roofline["traffic"] = tr
+        extra = {"bytes_per_read": round((search_bytes + text_bytes + locate_bytes) / nreads, 1),
+                 "kernels": {n: {"ms": v["ms"], "algorithmic_GBs": v["GBs"],
+                                 "bytes_per_read": round(v["bytes"] / nreads, 1)} for n, v in kern.items()},
                  "nodes_per_read": round(cnt["nodes"] / nreads, 1),
                  "ext_lines_per_read": round(cnt["ext_lines"] / nreads, 1),
                  "rank_nodes_per_read": round(cnt["rank_nodes"] / nreads, 1),
@@ -202,8 +220,7 @@ def main():
                  "locate_ms": round(locate_ms / args.steps, 2),
                  "sort_ms": round(sort_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
                  "search_grid": cnt["search_grid"],
-                 "locate_achieved_GBs": round(locate_bytes / (locate_ms / args.steps / 1e3) / 1e9, 1)
-                 if locate_ms > 0 else None}
+                 }
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -1,0 +1,89 @@
+"""Multi-rank sharding on CPU: world size 2 over gloo.
+
+Each rank searches its contiguous read shard (reads + reverse complements)
+with the CPU restatement, the hits are gathered to rank 0 by
+sahara_amd.dist.gather_hits, and the result must equal the single-process
+search of all reads. The GPU path uses the same helpers over RCCL (bench.py).
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from helpers import hits_as_rows, mutate_reads, random_records
+
+K = 2
+M = 40
+
+
+def _inputs():
+    rng = np.random.default_rng(77)
+    recs = random_records(rng, [3000, 1200], sigma=6, repeats=True)
+    reads = mutate_reads(rng, recs, 45, M, K)
+    return recs, reads
+
+
+def _with_rc(reads):
+    comp = np.array([0, 5, 3, 2, 4, 1], np.uint8)
+    out = np.empty((2 * len(reads), reads.shape[1]), np.uint8)
+    out[0::2] = reads
+    out[1::2] = comp[reads[:, ::-1]]
+    return out
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import oracle
+    from sahara_amd.dist import gather_hits, max_over_ranks, shard_bounds, sum_over_ranks
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        recs, reads = _inputs()
+        lo, hi = shard_bounds(len(reads), world, rank)
+        I = oracle.Index.build(recs, sigma=6)
+        h, _ = I.search(_with_rc(reads[lo:hi]), oracle.scheme("h2-k2", 0, K, M), edit=True)
+        allh = gather_hits(h, qid_offset=2 * lo)
+        total = sum_over_ranks(len(h))
+        t = max_over_ranks(float(rank + 1))
+        if rank == 0:
+            np.save(os.path.join(outdir, "gathered.npy"), allh)
+            np.save(os.path.join(outdir, "meta.npy"), np.array([total, t]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_bounds_partition():
+    from sahara_amd.dist import shard_bounds
+    for n in (0, 1, 7, 10_000_000, 80_000_000):
+        for w in (1, 2, 3, 8):
+            b = [shard_bounds(n, w, r) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+            assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
+
+
+@pytest.mark.parametrize("world", [2])
+def test_two_rank_gather_equals_single_process(world):
+    import oracle
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
+        got = np.load(os.path.join(d, "gathered.npy"))
+        total, t = np.load(os.path.join(d, "meta.npy"))
+    recs, reads = _inputs()
+    I = oracle.Index.build(recs, sigma=6)
+    want, _ = I.search(_with_rc(reads), oracle.scheme("h2-k2", 0, K, M), edit=True)
+    assert len(want) > 0
+    assert np.array_equal(hits_as_rows(got), hits_as_rows(want))
+    assert int(total) == len(want)
+    assert t == float(world)  # max over ranks
