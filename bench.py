@@ -197,8 +197,10 @@ def main():
                     "algorithmic_bytes_per_launch": round(kern[dom]["bytes"] / per_launch)}
         if args.traffic_json and os.path.exists(args.traffic_json):
             tr = json.load(open(args.traffic_json)).get(dom)
-            if tr:
-                roofline["traffic"] = tr
+            if tr:  # HBM bytes per launch from the committed PMC pass (FETCH_SIZE, calibrated)
+                roofline["traffic"] = tr["bytes_per_launch"]
+                roofline["traffic_GBs"] = tr["traffic_GBs"]
+                roofline["traffic_source"] = os.path.relpath(args.traffic_json, ROOT)
         extra = {"bytes_per_read": round((search_bytes + text_bytes + locate_bytes) / nreads, 1),
                  "kernels": {n: {"ms": v["ms"], "algorithmic_GBs": v["GBs"],
                                  "bytes_per_read": round(v["bytes"] / nreads, 1)} for n, v in kern.items()},
