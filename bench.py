@@ -143,7 +143,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    search_ms = text_ms = locate_ms = sort_ms = 0.0
+    search_ms = text_ms = locate_ms = sort_ms = seed_ms = 0.0
     launches = 0
     for i in range(args.steps):
         nh = idx.run()
@@ -152,6 +152,7 @@ def main():
         text_ms += st["text_ms"]
         locate_ms += st["locate_ms"]
         sort_ms += st["sort_ms"]
+        seed_ms += st["seed_ms"]
         launches += st["search_launches"]
     barrier()
     elapsed = time.perf_counter() - t0
@@ -220,8 +221,9 @@ def main():
                  "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
                  "search_ms": round(search_ms_step, 2), "text_ms": round(text_ms / args.steps, 2),
                  "locate_ms": round(locate_ms / args.steps, 2),
-                 "sort_ms": round(sort_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
-                 "search_grid": cnt["search_grid"],
+                 "sort_ms": round(sort_ms / args.steps, 2), "seed_ms": round(seed_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
+                 "search_grid": cnt["search_grid"], "text_grid": cnt["text_grid"],
+                 "pipelined": bool(cnt["pipelined"]),
                  }
 
     cpu = None

@@ -82,7 +82,10 @@ typedef struct sahara_stats {
     uint64_t text_cycles_refill; /* shader cycles summed over text-kernel waves: task starts (count=1) */
     uint64_t text_cycles_step;   /* ... node / compare micro-steps (count=1) */
     uint64_t text_cycles_emit;   /* ... leaf emission (count=1) */
-    uint64_t text_compare_steps; /* exact-compare micro-steps, lane count (count=1) */
+    uint64_t text_compare_steps; /* forced-run micro-steps, lane count (count=1) */
+    uint32_t text_grid;          /* text-kernel workgroups per launch */
+    uint32_t pipelined;          /* 1 if FM and text phases of consecutive batches overlapped */
+    double   seed_ms;            /* starting cursors (k-mer table lookups) */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

@@ -58,7 +58,8 @@ class Stats(C.Structure):
                 ("fm_iterations", C.c_uint64), ("text_iterations", C.c_uint64), ("text_active", C.c_uint64),
                 ("text_refills", C.c_uint64), ("text_cycles_refill", C.c_uint64),
                 ("text_cycles_step", C.c_uint64), ("text_cycles_emit", C.c_uint64),
-                ("text_compare_steps", C.c_uint64)]
+                ("text_compare_steps", C.c_uint64), ("text_grid", C.c_uint32), ("pipelined", C.c_uint32),
+                ("seed_ms", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -39,7 +39,7 @@ struct Ctx {
     DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern
     uint64_t npat = 0;
     uint32_t m = 0, patWords = 0;
-    DevBuf<uint32_t> scheme, cover;        // FM scheme table; text table (textTable)
+    DevBuf<uint32_t> scheme, cover, kmerStart;        // FM scheme table; text table (textTable)
     uint32_t nsearch = 0;
     uint32_t maxErr = 0;
     bool edit = true;
@@ -50,9 +50,23 @@ struct Ctx {
     uint32_t textSteps = 8;               // text-phase node expansions per lane per wave iteration
     uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
 
-    // work buffers
-    DevBuf<uint4> stack, hits, tasks;
-    DevBuf<uint32_t> small;               // work, hitCount, flags, filled, taskCount, textWork
+    // work buffers. Batches alternate between two slots so that the FM phase
+    // of batch i+1 (stream `st`) runs while batch i finishes its text phase,
+    // locate and sort (stream `stB`).
+    struct Slot {
+        DevBuf<uint4> hits, tasks;
+        DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, -, seedCount
+        DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512)
+        hipEvent_t fmStart = nullptr, seedDone = nullptr, fmDone = nullptr, textStart = nullptr, textDone = nullptr,
+                   free = nullptr;
+    } slot[2];
+    hipStream_t stB = nullptr;
+    uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
+    size_t pinnedCap = 0;
+    bool pipeline = true;
+    DevBuf<uint4> stack, seeds;           // FM spill stack; starting cursors (stream st only)
+    DevBuf<uint32_t> seedItem;
+    DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> rowOff, k0, k1;
     DevBuf<char> tmp;
@@ -65,6 +79,11 @@ struct Ctx {
     ~Ctx() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& sl : slot)
+            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmDone, sl.textStart, sl.textDone, sl.free})
+                if (e) (void)hipEventDestroy(e);
+        if (pinned) (void)hipHostFree(pinned);
+        if (stB) (void)hipStreamDestroy(stB);
         if (st) (void)hipStreamDestroy(st);
     }
 };
@@ -135,7 +154,14 @@ Ctx* newCtx(int device) {
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
+    for (auto& sl : c->slot) {
+        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
+            SH_HIP(hipEventCreate(e));
+        sl.small.reserve(8);
+        sl.queues.reserve(512);
+    }
     c->small.reserve(8);
     c->counters.reserve(16);
     SH_HIP(hipMemset(c->counters.ptr, 0, 16 * sizeof(unsigned long long)));
@@ -230,6 +256,20 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
     c->cover.reserve(cover.size());
     SH_HIP(hipMemcpyAsync(c->cover.ptr, cover.data(), cover.size() * 4, hipMemcpyHostToDevice, c->st));
+    // searches whose first kmerK steps admit no error start from the k-mer table
+    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu);
+    const uint32_t K = c->I.kmerK;
+    for (uint32_t s = 0; K && K <= m && s < ns; ++s) {
+        bool exact = true;
+        uint32_t lo = pi[(size_t)s * m];
+        for (uint32_t p = 0; p < K; ++p) {
+            exact = exact && u[(size_t)s * m + p] == 0;
+            lo = std::min(lo, pi[(size_t)s * m + p]);
+        }
+        if (exact) kst[s] = lo;
+    }
+    c->kmerStart.reserve(ns);
+    SH_HIP(hipMemcpyAsync(c->kmerStart.ptr, kst.data(), ns * 4, hipMemcpyHostToDevice, c->st));
     SH_HIP(hipStreamSynchronize(c->st));
     c->npat = npat;
     c->m = m;
@@ -238,20 +278,44 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     c->staged = true;
 }
 
-float elapsed(hipEvent_t a, hipEvent_t b) {
-    float ms = 0;
-    SH_HIP(hipEventElapsedTime(&ms, a, b));
-    return ms;
-}
+
+// One pass over the staged patterns in batches of <= 4M. Per batch:
+//   stream st : kSearchFM                              -> hits, tasks of its slot
+//   stream stB: kResolveTasks, kSearchText, locate, sort, decode
+// Two slots alternate, so the FM phase of batch i+1 (memory-latency bound)
+// overlaps the text phase of batch i (ALU bound). Buffer overflow is detected
+// after the fact from each batch's flags; the whole pass is then redone on one
+// stream with grown buffers (`serial`), re-running a batch until it fits.
+void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
 
 void run(Ctx* c, bool count) {
     if (!c->staged) throw Error("sahara_gpu_run: nothing staged");
     auto t0 = std::chrono::steady_clock::now();
+    if (const char* e = std::getenv("SAHARA_PIPELINE")) c->pipeline = std::atol(e) != 0;
     sahara_stats S{};
+    bool overflow = false;
+    runPass(c, count, !c->pipeline, S, overflow);
+    if (overflow) {
+        S = sahara_stats{};
+        runPass(c, count, true, S, overflow);
+    }
+    S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->stats = S;
+}
+
+void growCap(uint32_t& cap, uint32_t seen) {
+    const uint64_t want = (uint64_t)seen + seen / 4 + 1024;
+    if (want >= (1ull << 32) - 2) throw Error("a work buffer would exceed 2^32 entries in one batch");
+    cap = std::max<uint32_t>(cap, (uint32_t)want);
+}
+
+void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
+    overflow = false;
     S.patterns = c->npat;
     const uint32_t sigma = c->I.sigma;
     const size_t lds = (size_t)c->nsearch * c->m * 4;
-    const int bpc = searchBlocksPerCU(sigma, c->edit, lds);
+    int bpc = searchBlocksPerCU(sigma, c->edit, lds);
+    if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(bpc, std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     const uint64_t T = (uint64_t)blocks * 256;
     const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
@@ -270,8 +334,11 @@ void run(Ctx* c, bool count) {
     if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
     int tbpc = 0;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024) tbpc = textBlocksPerCU(sigma, c->edit, textLds);
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(tbpc, std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
+    S.text_grid = split ? textBlocks : 0u;
+    S.pipelined = serial ? 0u : 1u;
 
     const uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (c->hitCap == 0) {
@@ -282,124 +349,152 @@ void run(Ctx* c, bool count) {
         c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
     }
-    c->hits.reserve((size_t)c->hitCap + 1);
-    c->tasks.reserve((size_t)c->taskCap);
-    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), c->st));
+    const uint64_t nbatch = (c->npat + maxBatch - 1) / maxBatch;
+    if (c->pinnedCap < nbatch * 8) {
+        if (c->pinned) SH_HIP(hipHostFree(c->pinned));
+        c->pinned = nullptr;
+        SH_HIP(hipHostMalloc(&c->pinned, nbatch * 8 * sizeof(uint32_t)));
+        c->pinnedCap = nbatch * 8;
+    }
+    hipStream_t sA = c->st, sB = serial ? c->st : c->stB;
+    SH_HIP(hipStreamSynchronize(c->st));
+    SH_HIP(hipStreamSynchronize(c->stB));
+    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
+    for (auto& sl : c->slot) SH_HIP(hipEventRecord(sl.free, sA));
 
-    for (uint64_t q0 = 0; q0 < c->npat; q0 += maxBatch) {
-        const uint64_t nb = std::min<uint64_t>(maxBatch, c->npat - q0);
-        ++S.batches;
-        uint32_t hostSmall[8];
-        for (;;) {
-            SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), c->st));
-            SearchArgs a{};
-            a.occF = c->I.occF.ptr;
-            a.occR = c->I.occR.ptr;
-            for (int i = 0; i < 8; ++i) a.C[i] = (uint32_t)c->I.C[i];
-            a.n = (uint32_t)c->I.n;
-            a.pats = c->pats.ptr + q0 * c->patWords;
-            a.patWords = c->patWords;
-            a.m = c->m;
-            a.nsearch = c->nsearch;
-            a.nitems = (uint32_t)(nb * c->nsearch);
-            a.scheme = c->scheme.ptr;
-            a.work = c->small.ptr;
-            a.hitCount = c->small.ptr + 1;
-            a.flags = c->small.ptr + 2;
-            a.filled = c->small.ptr + 3;
-            a.taskCount = c->small.ptr + 4;
-            a.stack = c->stack.ptr;
-            a.stackCap = stackCap;
-            a.hits = c->hits.ptr;
-            a.hitCap = c->hitCap;
-            a.counters = c->counters.ptr;
-            a.tasks = c->tasks.ptr;
-            a.taskCap = c->taskCap;
-            a.split = split;
-            SH_HIP(hipEventRecord(c->ev[0], c->st));
-            launchSearch(a, sigma, c->edit, count, blocks, lds, c->st);
-            SH_HIP(hipEventRecord(c->ev[1], c->st));
-            SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
-            SH_HIP(hipStreamSynchronize(c->st));
-            S.search_ms += elapsed(c->ev[0], c->ev[1]);
-            ++S.search_launches;
-            if (hostSmall[2] & 1u) throw Error("search stack overflow (internal bound violated)");
-            if (hostSmall[2] & 8u) {  // task buffer too small: grow and re-run the batch
-                const uint64_t want = (uint64_t)hostSmall[4] + hostSmall[4] / 4 + 1024;
-                if (want >= (1ull << 32) - 2) throw Error("task buffer would exceed 2^32 tasks in one batch");
-                c->taskCap = (uint32_t)want;
-                c->tasks.reserve(c->taskCap);
-                continue;
-            }
-            if (hostSmall[2] & 2u) {  // hit buffer too small: grow and re-run the batch
-                const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
-                if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
-                c->hitCap = (uint32_t)want;
-                c->hits.reserve((size_t)c->hitCap + 1);
-                continue;
-            }
-            const uint32_t ntasks = std::min(hostSmall[4], c->taskCap);
-            if (ntasks) {
-                TextArgs t{};
-                t.sa = c->I.saFull.ptr;
-                t.text4w = reinterpret_cast<const uint32_t*>(c->I.text4.ptr);
-                t.pats = a.pats;
-                t.patWords = c->patWords;
-                t.m = c->m;
-                t.nsearch = c->nsearch;
-                t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
-                t.tasks = c->tasks.ptr;
-                t.ntasks = ntasks;
-                t.work = c->small.ptr + 5;
-                t.hits = c->hits.ptr;
-                t.hitCap = c->hitCap;
-                t.hitCount = a.hitCount;
-                t.filled = a.filled;
-                t.flags = a.flags;
-                t.counters = c->counters.ptr;
-                t.winWords = winWords;
-                t.stackCap = textStack;
-                t.steps = c->textSteps;
-                t.refillAt = c->refillAt;
-                SH_HIP(hipEventRecord(c->ev[5], c->st));
-                launchResolveTasks(c->tasks.ptr, ntasks, c->I.saFull.ptr, c->st);
-                launchText(t, sigma, c->edit, count, textBlocks, textLds, c->st);
-                SH_HIP(hipEventRecord(c->ev[6], c->st));
-                SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
-                SH_HIP(hipStreamSynchronize(c->st));
-                S.text_ms += elapsed(c->ev[5], c->ev[6]);
-                if (hostSmall[2] & 1u) throw Error("text-phase stack overflow (internal bound violated)");
-                if (hostSmall[2] & 16u) throw Error("text phase: internal window/stack bound violated");
-                if (hostSmall[2] & 2u) {
-                    const uint64_t want = (uint64_t)hostSmall[1] + hostSmall[1] / 4 + 1024;
-                    if (want >= (1ull << 32) - 2) throw Error("hit buffer would exceed 2^32 cursors in one batch");
-                    c->hitCap = (uint32_t)want;
-                    c->hits.reserve((size_t)c->hitCap + 1);
-                    continue;
-                }
-            }
-            break;
+    auto issueFM = [&](uint64_t b) {
+        Ctx::Slot& sl = c->slot[b & 1];
+        const uint64_t q0 = b * maxBatch, nb = std::min<uint64_t>(maxBatch, c->npat - q0);
+        sl.hits.reserve((size_t)c->hitCap + 1);
+        sl.tasks.reserve((size_t)c->taskCap);
+        SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
+        SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), sA));
+        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 512 * sizeof(uint32_t), sA));
+        SearchArgs a{};
+        a.occF = c->I.occF.ptr;
+        a.occR = c->I.occR.ptr;
+        for (int i = 0; i < 8; ++i) a.C[i] = (uint32_t)c->I.C[i];
+        a.n = (uint32_t)c->I.n;
+        a.pats = c->pats.ptr + q0 * c->patWords;
+        a.patWords = c->patWords;
+        a.m = c->m;
+        a.nsearch = c->nsearch;
+        a.nitems = (uint32_t)(nb * c->nsearch);
+        a.scheme = c->scheme.ptr;
+        a.work = sl.queues.ptr;
+        a.hitCount = sl.small.ptr + 1;
+        a.flags = sl.small.ptr + 2;
+        a.filled = sl.small.ptr + 3;
+        a.taskCount = sl.small.ptr + 4;
+        a.stack = c->stack.ptr;
+        a.stackCap = stackCap;
+        a.hits = sl.hits.ptr;
+        a.hitCap = c->hitCap;
+        a.counters = c->counters.ptr;
+        a.tasks = sl.tasks.ptr;
+        a.taskCap = c->taskCap;
+        a.split = split;
+        // starting cursors; reference execution (verify off) ranks every node
+        // from the root, so it does not use the k-mer table
+        SeedArgs sd{};
+        sd.pats = a.pats;
+        sd.patWords = c->patWords;
+        sd.nsearch = c->nsearch;
+        sd.nitems = a.nitems;
+        sd.n = a.n;
+        sd.kmer = c->verify && c->I.kmerK ? c->I.kmer.ptr : nullptr;
+        sd.kmerK = c->I.kmerK;
+        sd.kmerStart = c->kmerStart.ptr;
+        c->seeds.reserve(a.nitems);
+        c->seedItem.reserve(a.nitems);
+        sd.seeds = c->seeds.ptr;
+        sd.seedItem = c->seedItem.ptr;
+        sd.seedCount = sl.small.ptr + 6;
+        a.seeds = c->seeds.ptr;
+        a.seedItem = c->seedItem.ptr;
+        a.seedCount = sl.small.ptr + 6;
+        SH_HIP(hipEventRecord(sl.fmStart, sA));
+        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sA);
+        SH_HIP(hipEventRecord(sl.seedDone, sA));
+        launchSearch(a, sigma, c->edit, count, blocks, lds, sA);
+        SH_HIP(hipEventRecord(sl.fmDone, sA));
+        ++S.search_launches;
+    };
+    auto issueText = [&](uint64_t b) {
+        Ctx::Slot& sl = c->slot[b & 1];
+        const uint64_t q0 = b * maxBatch;
+        SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+        SH_HIP(hipEventRecord(sl.textStart, sB));
+        if (split) {
+            TextArgs t{};
+            t.sa = c->I.saFull.ptr;
+            t.text4w = reinterpret_cast<const uint32_t*>(c->I.text4.ptr);
+            t.pats = c->pats.ptr + q0 * c->patWords;
+            t.patWords = c->patWords;
+            t.m = c->m;
+            t.nsearch = c->nsearch;
+            t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
+            t.tasks = sl.tasks.ptr;
+            t.taskCount = sl.small.ptr + 4;
+            t.taskCap = c->taskCap;
+            t.work = sl.queues.ptr + 256;
+            t.hits = sl.hits.ptr;
+            t.hitCap = c->hitCap;
+            t.hitCount = sl.small.ptr + 1;
+            t.filled = sl.small.ptr + 3;
+            t.flags = sl.small.ptr + 2;
+            t.counters = c->counters.ptr;
+            t.winWords = winWords;
+            t.stackCap = textStack;
+            t.steps = c->textSteps;
+            t.refillAt = c->refillAt;
+            launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
+            launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+        }
+        SH_HIP(hipEventRecord(sl.textDone, sB));
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 8, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sB));
+    };
+    // locate: row offsets (exclusive scan of len), SA / LF locate, canonical
+    // sort, decode into the device-resident output. Needs the batch's counts.
+    auto finish = [&](uint64_t b) {
+        Ctx::Slot& sl = c->slot[b & 1];
+        const uint64_t q0 = b * maxBatch, nb = std::min<uint64_t>(maxBatch, c->npat - q0);
+        SH_HIP(hipStreamSynchronize(sB));
+        const uint32_t* hs = c->pinned + b * 8;
+        float ms = 0;
+        SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
+        S.seed_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, sl.seedDone, sl.fmDone));
+        S.search_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+        S.text_ms += ms;
+        if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
+        if (hs[2] & 16u) throw Error("text phase: internal window/stack bound violated");
+        if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
+            if (hs[2] & 8u) growCap(c->taskCap, hs[4]);
+            if (hs[2] & 2u) growCap(c->hitCap, hs[1]);
+            overflow = true;
+            SH_HIP(hipEventRecord(sl.free, sB));
+            return false;
         }
         // reserved slots incl. len-0 holes; a wave's last range may reach past
         // the capacity without having written there (no overflow flag)
-        const uint64_t nh = std::min<uint64_t>(hostSmall[1], c->hitCap);
-        S.cursors += hostSmall[3];
-
-        // locate: row offsets (exclusive scan of len), LF walks, canonical sort, decode
-        SH_HIP(hipEventRecord(c->ev[2], c->st));
-        SH_HIP(hipMemsetAsync(c->hits.ptr + nh, 0, sizeof(uint4), c->st));
+        const uint64_t nh = std::min<uint64_t>(hs[1], c->hitCap);
+        S.cursors += hs[3];
+        SH_HIP(hipEventRecord(c->ev[2], sB));
+        SH_HIP(hipMemsetAsync(sl.hits.ptr + nh, 0, sizeof(uint4), sB));
         c->rowOff.reserve(nh + 1);
         const size_t scanBytes = rowOffsetsTempBytes(nh);
         c->tmp.reserve(scanBytes + 256);
-        rowOffsets(c->hits.ptr, nh, c->rowOff.ptr, c->tmp.ptr, c->tmp.cap, c->st);
+        rowOffsets(sl.hits.ptr, nh, c->rowOff.ptr, c->tmp.ptr, c->tmp.cap, sB);
         uint64_t rows = 0;
-        SH_HIP(hipMemcpyAsync(&rows, c->rowOff.ptr + nh, 8, hipMemcpyDeviceToHost, c->st));
-        SH_HIP(hipStreamSynchronize(c->st));
+        SH_HIP(hipMemcpyAsync(&rows, c->rowOff.ptr + nh, 8, hipMemcpyDeviceToHost, sB));
+        SH_HIP(hipStreamSynchronize(sB));
         c->k0.reserve(std::max<uint64_t>(rows, 1));
         c->k1.reserve(std::max<uint64_t>(rows, 1));
         LocateArgs la{};
-        la.hits = c->hits.ptr;
+        la.hits = sl.hits.ptr;
         la.nhits = nh;
         la.rowOff = c->rowOff.ptr;
         la.occF = c->I.occF.ptr;
@@ -411,40 +506,66 @@ void run(Ctx* c, bool count) {
         la.counters = c->counters.ptr + 3;
         la.sa = c->I.saFull.ptr;
         la.useSA = c->locateSA ? 1u : 0u;
-        launchLocate(la, count, c->st);
-        SH_HIP(hipEventRecord(c->ev[3], c->st));
+        SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sB));
+        launchLocate(la, count, sB);
+        SH_HIP(hipEventRecord(sl.free, sB));  // the slot's hits are consumed
+        SH_HIP(hipEventRecord(c->ev[3], sB));
         unsigned endBit = 36;
         while ((1ull << (endBit - 36)) < nb) ++endBit;
-        const size_t sb = sortTempBytes(rows);
-        c->tmp.reserve(sb + 256);
-        uint64_t* sorted = sortKeys(c->k0.ptr, c->k1.ptr, rows, std::min(endBit, 64u), c->tmp.ptr, c->tmp.cap, c->st);
-        // grow the output (device-resident) and decode
-        if (c->nout + rows > c->out.cap) {
+        const size_t sbytes = sortTempBytes(rows);
+        c->tmp.reserve(sbytes + 256);
+        uint64_t* sorted = sortKeys(c->k0.ptr, c->k1.ptr, rows, std::min(endBit, 64u), c->tmp.ptr, c->tmp.cap, sB);
+        if (c->nout + rows > c->out.cap) {  // grow the device-resident output
             const size_t want = std::max<size_t>((c->nout + rows) + (c->nout + rows) / 2, 1024);
             sahara_hit* np = nullptr;
             SH_HIP(hipMalloc(&np, want * sizeof(sahara_hit)));
-            if (c->nout)
-                SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, c->st));
-            SH_HIP(hipStreamSynchronize(c->st));
+            if (c->nout) SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, sB));
+            SH_HIP(hipStreamSynchronize(sB));
             c->out.release();
             c->out.ptr = np;
             c->out.cap = want;
         }
-        launchDecode(sorted, rows, q0, c->I.dRecStarts.ptr, (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout,
-                     c->st);
-        SH_HIP(hipEventRecord(c->ev[4], c->st));
-        SH_HIP(hipMemcpyAsync(hostSmall, c->small.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
-        SH_HIP(hipStreamSynchronize(c->st));
-        if (hostSmall[2] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
-        S.locate_ms += elapsed(c->ev[2], c->ev[3]);
-        S.sort_ms += elapsed(c->ev[3], c->ev[4]);
+        launchDecode(sorted, rows, q0, c->I.dRecStarts.ptr, (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, sB);
+        SH_HIP(hipEventRecord(c->ev[4], sB));
+        uint32_t lflags = 0;
+        SH_HIP(hipMemcpyAsync(&lflags, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sB));
+        SH_HIP(hipStreamSynchronize(sB));
+        if (lflags & 4u) throw Error("locate walked off the SA samples (corrupt index)");
+        SH_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        S.locate_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
+        S.sort_ms += ms;
         c->nout += rows;
         S.hits += rows;
+        return true;
+    };
+
+    if (!serial) {
+        issueFM(0);
+        for (uint64_t b = 0; b < nbatch; ++b) {
+            if (b + 1 < nbatch) issueFM(b + 1);
+            issueText(b);
+            ++S.batches;
+            finish(b);
+        }
+        SH_HIP(hipStreamSynchronize(sA));
+        if (overflow) return;  // the caller redoes the pass serially with the grown buffers
+    } else {
+        for (uint64_t b = 0; b < nbatch; ++b) {
+            ++S.batches;
+            for (;;) {  // re-run the batch until its buffers suffice
+                overflow = false;
+                issueFM(b);
+                issueText(b);
+                if (finish(b)) break;
+            }
+        }
+        overflow = false;
     }
     if (count) {
         unsigned long long h[16];
-        SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, c->st));
-        SH_HIP(hipStreamSynchronize(c->st));
+        SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, sB));
+        SH_HIP(hipStreamSynchronize(sB));
         S.nodes = h[0];
         S.rank_nodes = h[1];
         S.ext_lines = h[2];
@@ -460,8 +581,6 @@ void run(Ctx* c, bool count) {
         S.text_cycles_emit = h[13];
         S.text_compare_steps = h[14];
     }
-    S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    c->stats = S;
 }
 
 }  // namespace

@@ -61,9 +61,15 @@ struct DeviceIndex {
     // Resident for the search (HBM is 288 GB; at 3 Gbp these are 12 + 1.5 GB):
     DevBuf<uint32_t> saFull;        // SA[row] for every row: locate = one read
     DevBuf<uint8_t> text4;          // text, 4 bits per symbol (two per byte), '$' = 0, kTextPad zero bytes after
+    // k-mer table: the bidirectional cursor {lb, lbRev, len, 0} of every
+    // ACGT string of length kmerK (2 bits per symbol, first symbol most
+    // significant). A search whose first kmerK steps admit no error starts
+    // at depth kmerK with one lookup instead of kmerK rank steps.
+    DevBuf<uint4> kmer;
+    uint32_t kmerK = 0;
     uint64_t deviceBytes() const {
         return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8 + saFull.cap * 4 +
-               text4.cap;
+               text4.cap + kmer.cap * sizeof(uint4);
     }
 };
 
@@ -73,6 +79,11 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec,
                     uint32_t rate, const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits,
                     const uint32_t* samples, uint64_t nsamples, hipStream_t st);
+// depth of the k-mer table for a text of n symbols: floor(log4 n) - 2 (the
+// mean interval then still holds ~16-64 rows), at most 14 (4.3 GB);
+// SAHARA_KMER overrides (0 = no table)
+uint32_t kmerDepth(uint64_t n);
+void buildKmerTable(DeviceIndex& I, uint32_t K, hipStream_t st);
 void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits,
                  uint32_t* samples, hipStream_t st);
 

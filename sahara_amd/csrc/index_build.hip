@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
@@ -378,6 +379,46 @@ void setC(DeviceIndex& I, const uint64_t totals[6], uint64_t nrec) {
 
 }  // namespace
 
+// ----------------------------------------------------------- k-mer table ----
+struct Cvec {
+    uint64_t v[8];
+};
+
+// Level j of the table from level j-1: each string w extends to the right by
+// A, C, G, T (extendRight on the reverse BWT: one rank of all symbols at lbRev
+// and lbRev + len; the forward lb moves by the occurrences of the smaller
+// symbols, '$' first). Empty intervals stay empty.
+__global__ void kKmerLevel(const OccLine* __restrict__ occR, Cvec C, uint32_t sigma, const uint4* __restrict__ prev,
+                           uint64_t count, uint4* __restrict__ next) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 w = prev[i];
+        uint4 out[4] = {};
+        if (w.z) {
+            const uint32_t lo = w.y, hi = w.y + w.z;
+            const OccLine& A = occR[lo >> 6];
+            const OccLine& B = occR[hi >> 6];
+            const uint64_t ml = lowMask(lo & 63u), mh = lowMask(hi & 63u);
+            uint32_t occ[6] = {}, base[6] = {}, sum = 0;
+            for (uint32_t c = 1; c < sigma; ++c) {
+                const uint32_t rl = A.cnt[c - 1] + (uint32_t)__popcll(symMask(A.plane, c) & ml);
+                const uint32_t rh = B.cnt[c - 1] + (uint32_t)__popcll(symMask(B.plane, c) & mh);
+                occ[c] = rh - rl;
+                base[c] = (uint32_t)C.v[c] + rl;
+                sum += occ[c];
+            }
+            uint32_t acc = w.x + (w.z - sum);
+            uint32_t j = 0;
+            for (uint32_t c = 1; c < sigma; ++c) {
+                const bool acgt = !(sigma == 6 && c == 4);  // N is not in the table
+                if (acgt) out[j++] = occ[c] ? make_uint4(acc, base[c], occ[c], 0u) : make_uint4(0u, 0u, 0u, 0u);
+                acc += occ[c];
+            }
+        }
+        for (int j = 0; j < 4; ++j) next[i * 4 + j] = out[j];
+    }
+}
+
 void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma,
                    uint32_t rate, hipStream_t st) {
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
@@ -444,6 +485,7 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
     for (int c = 0; c < 5; ++c)
         if (totalsR[c] != totals[c]) throw Error("forward/reverse symbol counts differ");
     SH_HIP(hipStreamSynchronize(st));
+    buildKmerTable(I, kmerDepth(N), st);
 }
 
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec, uint32_t rate,
@@ -490,6 +532,42 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     SH_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, st));
     SH_HIP(hipStreamSynchronize(st));
     if (herr) throw Error("SA densification walk exceeded its bound (inconsistent .idx samples)");
+    buildKmerTable(I, kmerDepth(n), st);
+}
+
+uint32_t kmerDepth(uint64_t n) {
+    uint32_t lg = 0;
+    while (lg < 31 && (1ull << (2 * (lg + 1))) <= n) ++lg;  // floor(log4 n)
+    int k = (int)lg - 2;
+    if (const char* e = std::getenv("SAHARA_KMER")) k = std::atoi(e);
+    return (uint32_t)std::max(0, std::min(k, 14));
+}
+
+void buildKmerTable(DeviceIndex& I, uint32_t K, hipStream_t st) {
+    I.kmerK = 0;
+    I.kmer.release();
+    if (K == 0) return;
+    Cvec C;
+    for (int c = 0; c < 8; ++c) C.v[c] = I.C[c];
+    DevBuf<uint4> t0, t1;  // levels 0 .. K-1, alternating
+    const uint64_t maxPrev = 1ull << (2 * (K - 1));
+    t0.reserve(maxPrev);
+    if (K > 1) t1.reserve(maxPrev);
+    I.kmer.reserve(1ull << (2 * K));
+    const uint4 root = make_uint4(0u, 0u, (uint32_t)I.n, 0u);
+    SH_HIP(hipMemcpyAsync(t0.ptr, &root, sizeof(root), hipMemcpyHostToDevice, st));
+    uint4* prev = t0.ptr;
+    uint64_t count = 1;
+    for (uint32_t j = 1; j <= K; ++j) {
+        uint4* next = j == K ? I.kmer.ptr : (prev == t0.ptr ? t1.ptr : t0.ptr);
+        hipLaunchKernelGGL(kKmerLevel, dim3((unsigned)std::min<uint64_t>((count + 255) / 256, 1u << 16)), dim3(256), 0,
+                           st, I.occR.ptr, C, I.sigma, prev, count, next);
+        SH_HIP(hipGetLastError());
+        count *= 4;
+        prev = next;
+    }
+    SH_HIP(hipStreamSynchronize(st));
+    I.kmerK = K;
 }
 
 void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits, uint32_t* samples,

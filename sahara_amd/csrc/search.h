@@ -19,6 +19,9 @@ struct SearchArgs {
     uint32_t m;
     uint32_t nsearch;
     uint32_t nitems;         // npat * nsearch
+    const uint4* seeds;      // starting cursors (kSeedItems), *seedCount of them
+    const uint32_t* seedItem;  // their items (pattern * nsearch + search)
+    const uint32_t* seedCount;
     const uint32_t* scheme;  // nsearch * m packed entries (packScheme)
     uint32_t* work;          // item counter
     uint4* stack;            // spilled DFS levels beyond the LDS part, [depth][grid thread]
@@ -35,6 +38,20 @@ struct SearchArgs {
     uint32_t split;          // intervals of <= split rows go to the text phase (0: never)
 };
 
+struct SeedArgs {
+    const uint32_t* pats;
+    uint32_t patWords;
+    uint32_t nsearch;
+    uint32_t nitems;
+    uint32_t n;
+    const uint4* kmer;          // k-mer table (DeviceIndex::kmer), nullptr = start every item at the root
+    uint32_t kmerK;
+    const uint32_t* kmerStart;  // per search: pattern offset of its error-free first kmerK steps, ~0u = n/a
+    uint4* seeds;
+    uint32_t* seedItem;
+    uint32_t* seedCount;
+};
+
 struct TextArgs {
     const uint32_t* sa;      // full SA (tasks arrive resolved by launchResolveTasks)
     const uint32_t* text4w;  // 4-bit packed text as u32 words (8 symbols each)
@@ -44,7 +61,8 @@ struct TextArgs {
     uint32_t nsearch;
     const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
     const uint4* tasks;
-    uint32_t ntasks;
+    const uint32_t* taskCount;  // tasks written by the FM kernel (device-side: no host round trip)
+    uint32_t taskCap;
     uint32_t* work;
     uint4* hits;
     uint32_t hitCap;
@@ -77,7 +95,9 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
-void launchResolveTasks(uint4* tasks, uint32_t n, const uint32_t* sa, hipStream_t st);
+void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);
+void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const uint32_t* sa, uint32_t blocks,
+                        hipStream_t st);
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t* dst,
                         hipStream_t st);
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,

@@ -110,7 +110,7 @@ __device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
 
 __device__ __forceinline__ uint32_t nib(uint32_t word, uint32_t i) { return (word >> ((i & 7u) * 4u)) & 0xFu; }
 
-constexpr uint32_t kWorkChunk = 256;  // items a wave takes per atomic
+constexpr uint32_t kSeedChunk = 64;   // seeds a wave takes per atomic
 constexpr uint32_t kTaskChunk = 64;   // text tasks a wave takes per atomic
 constexpr uint32_t kHitChunk = 64;    // hit / task slots a wave reserves per atomic
 constexpr uint32_t kLdsDepth = 4;     // FM DFS stack levels kept in LDS (16 KB per block)
@@ -141,6 +141,36 @@ struct SlotRange {
     __device__ __forceinline__ void close(uint32_t lane, uint4* buf, uint32_t cap) {
         for (uint32_t i = next + lane; i < end; i += 64)
             if (i < cap) buf[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+};
+
+// Work queue split into kStripes stripes with one counter each (128 B apart):
+// a wave starts on the stripe of its XCD (blockIdx % 8) and moves on when it
+// is drained. A single counter serialises at ~90 chunk grabs per microsecond
+// device-wide; eight of them keep a chunk grab off the critical path.
+constexpr uint32_t kStripes = 8;
+constexpr uint32_t kStripeStride = 32;  // u32 between counters
+struct StripedQueue {
+    uint32_t* ctr;
+    uint32_t n, stripe, tries = 0;
+    __device__ StripedQueue(uint32_t* c, uint32_t total) : ctr(c), n(total), stripe(blockIdx.x % kStripes) {}
+    // next chunk [b, e) of at most `chunk` items (wave-uniform); false when all stripes are drained
+    __device__ bool next(uint32_t lane, uint32_t chunk, uint32_t& b, uint32_t& e) {
+        while (tries < kStripes) {
+            const uint32_t s0 = (uint32_t)((uint64_t)n * stripe / kStripes);
+            const uint32_t s1 = (uint32_t)((uint64_t)n * (stripe + 1) / kStripes);
+            uint32_t off = 0;
+            if (lane == 0) off = s0 < s1 ? atomicAdd(ctr + stripe * kStripeStride, chunk) : 0xFFFFFFFFu;
+            off = __shfl(off, 0);
+            if (off != 0xFFFFFFFFu && off < s1 - s0) {
+                b = s0 + off;
+                e = min(b + chunk, s1);
+                return true;
+            }
+            stripe = (stripe + 1) % kStripes;
+            ++tries;
+        }
+        return false;
     }
 };
 
@@ -192,6 +222,85 @@ __device__ __forceinline__ uint32_t childMeta(uint32_t pos, uint32_t e, uint32_t
     return npos | (ne << 16) | (nl << 20) | (nr << 22) | (nd << 25);
 }
 
+// ========================================================= seeds ====
+// One thread per work item (pattern, search): its starting cursor. A search
+// whose first kmerK steps admit no error starts at depth kmerK from the k-mer
+// table (the DFS would reach the same node through kmerK forced matches);
+// items whose k-mer does not occur end here. Every other item starts at the
+// root. Surviving items are appended (wave ballot + one atomic per wave) to
+// the seed list that kSearchFM consumes.
+template <int SIGMA>
+__device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& keep) {
+    uint4 cur = make_uint4(0u, 0u, a.n, kDeltaZero);
+    keep = i < a.nitems;
+    if (keep && a.kmer) {
+        const uint32_t pid = i / a.nsearch, s = i - pid * a.nsearch;
+        const uint32_t ks = a.kmerStart[s];
+        if (ks != 0xFFFFFFFFu) {
+            const uint32_t* pw = a.pats + (size_t)pid * a.patWords + (ks >> 3);
+            const uint32_t w0 = pw[0], w1 = pw[1], w2 = pw[2];
+            const uint32_t sh = (ks & 7u) * 4u;
+            const uint64_t run = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) |
+                                 ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
+            uint32_t code = 0;
+            bool acgt = true;
+            for (uint32_t j = 0; j < a.kmerK; ++j) {
+                const uint32_t c = (uint32_t)(run >> (4u * j)) & 0xFu;  // A1 C2 G3 (N4) T5|T4
+                acgt = acgt && !(SIGMA == 6 && c == 4u);
+                code = code * 4u + ((SIGMA == 6 && c == 5u) ? 3u : c - 1u);
+            }
+            if (acgt) {
+                const uint4 t = a.kmer[code & ((1u << (2u * a.kmerK)) - 1u)];
+                cur = make_uint4(t.x, t.y, t.z, packMeta(a.kmerK, 0u, OP_MS, OP_MS));
+                keep = t.z != 0u;
+            }
+        }
+    }
+    return cur;
+}
+
+// Each block takes 1024 consecutive items per round (4 per thread, so four
+// table lookups are in flight per lane) and appends the survivors with one
+// atomic per round.
+template <int SIGMA>
+__global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
+    __shared__ uint32_t wcount[4], blockBase;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t ltMask = (1ull << lane) - 1ull;
+    for (uint32_t base = blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
+        uint4 cur[4];
+        bool keep[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k]);
+        uint64_t m[4];
+        uint32_t wsum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            m[k] = __ballot(keep[k]);
+            wsum += (uint32_t)__popcll(m[k]);
+        }
+        if (lane == 0) wcount[w] = wsum;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+            blockBase = tot ? atomicAdd(a.seedCount, tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t slot = blockBase;
+        for (uint32_t j = 0; j < w; ++j) slot += wcount[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t at = slot + (uint32_t)__popcll(m[k] & ltMask);
+            if (keep[k]) {
+                a.seeds[at] = cur[k];
+                a.seedItem[at] = base + k * 256u + threadIdx.x;
+            }
+            slot += (uint32_t)__popcll(m[k]);
+        }
+        __syncthreads();  // wcount / blockBase reused next round
+    }
+}
+
 // =========================================================== phase 1: FM ====
 
 template <int SIGMA, bool EDIT, bool COUNT>
@@ -218,36 +327,68 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     SlotRange hitSlots, taskSlots;
     uint4 cur = make_uint4(0, 0, 0, 0);
     uint64_t cNodes = 0, cRank = 0, cLines = 0, cTasks = 0, cIter = 0;
+    // seeds (kSeedItems: starting cursor + item) arrive in chunks of 64, one
+    // record per lane, prefetched a chunk ahead so a refill costs no memory trip
+    const uint32_t nseeds = *a.seedCount;
+    uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
+    uint32_t curItem = 0, nextItem = 0, nBase = 0, nEnd = 0, qBase = 0;
+    bool haveNext = false;
+    StripedQueue queue(a.work, nseeds);
+    {
+        uint32_t b = 0, e = 0;
+        if (queue.next(lane, kSeedChunk, b, e)) {
+            nBase = b;
+            nEnd = e;
+            if (b + lane < e) { nextRec = a.seeds[b + lane]; nextItem = a.seedItem[b + lane]; }
+            haveNext = true;
+        } else {
+            qDone = true;
+        }
+    }
 
     for (;;) {
-        // ---- refill idle lanes from the wave's private item range; the wave
-        // takes kWorkChunk items per atomic on the global counter
+        // ---- refill idle lanes from the wave's current seed chunk
         const bool need = !have && sp == 0 && !exhausted;
         uint64_t pending = __ballot(need);
         while (pending) {  // wave-uniform
             if (qNext >= qEnd) {
-                if (qDone) break;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(a.work, kWorkChunk);
-                base = __shfl(base, 0);
-                if (base >= a.nitems) { qDone = true; break; }
-                qNext = base;
-                qEnd = min(base + kWorkChunk, a.nitems);
+                if (!haveNext) break;
+                qBase = nBase;
+                qNext = nBase;
+                qEnd = nEnd;
+                curRec = nextRec;
+                curItem = nextItem;
+                haveNext = false;
+                if (!qDone) {
+                    uint32_t b = 0, e = 0;
+                    if (!queue.next(lane, kSeedChunk, b, e)) {
+                        qDone = true;
+                    } else {
+                        nBase = b;
+                        nEnd = e;
+                        if (b + lane < e) { nextRec = a.seeds[b + lane]; nextItem = a.seedItem[b + lane]; }
+                        haveNext = true;
+                    }
+                }
+                if (qNext >= qEnd) continue;
             }
             const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
             const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
             const bool mine = ((pending >> lane) & 1ull) && rank < take;
+            const uint32_t src = (qNext - qBase + rank) & 63u;
+            const uint4 sd = make_uint4(__shfl(curRec.x, src), __shfl(curRec.y, src), __shfl(curRec.z, src),
+                                        __shfl(curRec.w, src));
+            const uint32_t item = __shfl(curItem, src);
             if (mine) {
-                const uint32_t item = qNext + rank;
                 pid = item / a.nsearch;
                 sIdx = item - pid * a.nsearch;
-                cur = make_uint4(0u, 0u, a.n, kDeltaZero);
+                cur = sd;
                 have = true;
             }
             pending &= ~__ballot(mine);
             qNext += take;
         }
-        if (qDone && need && !have) exhausted = true;
+        if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
         if (!have && sp > 0) {
             --sp;
             cur = sp < kLdsDepth ? lstk[sp][threadIdx.x] : stk[(size_t)(sp - kLdsDepth) * T];
@@ -397,20 +538,31 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 // A lane's state is one DFS node `cur` (x = window offsets xo | yo << 16 of
 // the text t matched so far, y = pos | e << 16 | lastL << 20 | lastR << 22).
 // Every micro-step is straight-line code — one stack read, one table read,
-// one 16-symbol read of pattern and of window, three stack writes — so the
+// 8-symbol reads of the window on both sides of the span and of the pattern at
+// pi[pos] and pi[pos+1], three stack writes — so the
 // lanes of a wave stay converged. A node with e == u[pos] has no error child
 // in the forced run of positions that follows it (table `run`), so it takes
-// up to 16 forced matches at once: the DFS visits the same chain of nodes,
+// up to 8 forced matches at once: the DFS visits the same chain of nodes,
 // one micro-step per 16 of them.
 
-// 16 consecutive nibbles starting at nibble offset o of an interleaved word
-// array of `words` words (reads past the end return garbage in the high
-// nibbles; callers mask them).
-__device__ __forceinline__ uint64_t nib16(const uint32_t* A, uint32_t o, uint32_t words) {
+// 8 consecutive nibbles [o, o+8) of an interleaved word array of `words`
+// words (past the end: garbage, callers bound-check)
+__device__ __forceinline__ uint32_t nib8(const uint32_t* A, uint32_t o, uint32_t words) {
     const uint32_t i = min(o >> 3, words - 1u);
-    const uint32_t w0 = A[i * 256u], w1 = A[min(i + 1u, words - 1u) * 256u], w2 = A[min(i + 2u, words - 1u) * 256u];
-    const uint32_t sh = (o & 7u) * 4u;
-    return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
+    const uint32_t w0 = A[i * 256u], w1 = A[min(i + 1u, words - 1u) * 256u];
+    return __builtin_amdgcn_alignbit(w1, w0, (o & 7u) * 4u);
+}
+// the pattern run read at position q in direction r (branch-free): right ->
+// [q, q+8); left -> [q-7, q] top-aligned (q in nibble 7, zeros below 0)
+__device__ __forceinline__ uint32_t patRun(const uint32_t* A, uint32_t q, bool r, uint32_t words) {
+    const uint32_t o = r ? q : (q >= 7u ? q - 7u : 0u);
+    const uint32_t v = nib8(A, o, words);
+    return (!r && q < 7u) ? v << (4u * (7u - q)) : v;
+}
+// the 8 nibbles [end-8, end), zero where end-8+i < 0 (nibble 7 = end-1)
+__device__ __forceinline__ uint32_t left8(const uint32_t* A, uint32_t end, uint32_t words) {
+    const uint32_t v = nib8(A, end >= 8u ? end - 8u : 0u, words);
+    return end >= 8u ? v : (end == 0u ? 0u : v << (32u - 4u * end));
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -441,7 +593,9 @@ __device__ __forceinline__ void copyPair(uint32_t* DA, const u32x2a4* A, uint32_
 
 // Text tasks carry an SA row; replace it by its text position (one SA read
 // per task, fully parallel) so the text kernel starts a task with one round trip.
-__global__ void kResolveTasks(uint4* __restrict__ tasks, uint32_t n, const uint32_t* __restrict__ sa) {
+__global__ void kResolveTasks(uint4* __restrict__ tasks, const uint32_t* __restrict__ count, uint32_t cap,
+                              const uint32_t* __restrict__ sa) {
+    const uint32_t n = min(*count, cap);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         tasks[i].x = sa[tasks[i].x];
 }
@@ -462,6 +616,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint2* S = reinterpret_cast<uint2*>(slot + (winWords + patWords) * 256u) + threadIdx.x;
     const uint32_t winLen = winWords * 8u;
     const uint32_t m = a.m;
+    const uint32_t ntasks = min(*a.taskCount, a.taskCap);
 
     uint32_t sp = 0, pid = 0, wb = 0, sBase = 0;
     bool have = false, exhausted = false, bad = false;
@@ -472,14 +627,13 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
     uint32_t nBase = 0, nEnd = 0, qBase = 0;
     bool haveNext = false;
+    StripedQueue queue(a.work, ntasks);
     {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(a.work, kTaskChunk);
-        base = __shfl(base, 0);
-        if (base < a.ntasks) {
-            nBase = base;
-            nEnd = min(base + kTaskChunk, a.ntasks);
-            if (base + lane < nEnd) nextRec = a.tasks[base + lane];
+        uint32_t b = 0, e = 0;
+        if (queue.next(lane, kTaskChunk, b, e)) {
+            nBase = b;
+            nEnd = e;
+            if (b + lane < e) nextRec = a.tasks[b + lane];
             haveNext = true;
         } else {
             qDone = true;
@@ -511,15 +665,13 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 curRec = nextRec;
                 haveNext = false;
                 if (!qDone) {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(a.work, kTaskChunk);
-                    base = __shfl(base, 0);
-                    if (base >= a.ntasks) {
+                    uint32_t b = 0, e = 0;
+                    if (!queue.next(lane, kTaskChunk, b, e)) {
                         qDone = true;
                     } else {
-                        nBase = base;
-                        nEnd = min(base + kTaskChunk, a.ntasks);
-                        if (base + lane < nEnd) nextRec = a.tasks[base + lane];
+                        nBase = b;
+                        nEnd = e;
+                        if (b + lane < e) nextRec = a.tasks[b + lane];
                         haveNext = true;
                     }
                 }
@@ -578,49 +730,96 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
             const uint32_t e = (cur.y >> 16) & 0xFu;
             const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
-            const uint32_t se = SC[sBase + min(pos, m - 1u)].x;
-            const uint32_t q = se & 0xFFFFu;
-            const uint32_t lb = (se >> 16) & 0xFu, ub = (se >> 20) & 0xFu;
-            const bool right = (se >> 24) & 1u;
-            const uint32_t run = se >> 25;
+            const uint32_t t0 = SC[sBase + min(pos, m - 1u)].x;       // this step
+            const uint32_t t1 = SC[sBase + min(pos + 1u, m - 1u)].x;  // the next step (children S, I)
+            const uint32_t q0 = t0 & 0xFFFFu, lb0 = (t0 >> 16) & 0xFu, ub0 = (t0 >> 20) & 0xFu;
+            const bool r0 = (t0 >> 24) & 1u;
+            const uint32_t run0 = t0 >> 25;
+            const uint32_t q1 = t1 & 0xFFFFu, ub1 = (t1 >> 20) & 0xFu;
+            const bool r1 = (t1 >> 24) & 1u;
+            const uint32_t run1 = t1 >> 25;
+
+            // ---- reads (8 symbols each): the text on both sides of the span —
+            // TR = t[yo, yo+8), TL = t[xo-8, xo) — and the pattern runs at
+            // pi[pos] and pi[pos+1] in their directions (a left run is read
+            // top-aligned: its first symbol, pi[.], in the top nibble).
+            const uint32_t TR = nib8(W, yo, winWords);
+            const uint32_t TL = left8(W, xo, winWords);
+            const uint32_t P0 = patRun(P, q0, r0, patWords), P1 = patRun(P, q1, r1, patWords);
+            // does the pattern run Pw (k symbols) match the text on side r
+            // beyond the span, after skipping s symbols a sibling consumed?
+            // '$', the text's ends and window padding (0) never match.
+            auto runEq = [&](uint32_t Pw, bool r, uint32_t s, uint32_t k, bool& in) -> bool {
+                in = r ? (yo + s + k <= winLen) : (s + k <= xo);
+                const uint32_t sh = 32u - 4u * k;
+                const uint32_t d = r ? (((TR >> (4u * s)) ^ Pw) << sh) : (((TL << (4u * s)) ^ Pw) >> sh);
+                return in && d == 0u;
+            };
 
             const bool atLeaf = live && pos == m;
             const bool node = live && pos < m;
-            const bool forced = e == ub;  // no error child at this position or the rest of its run
-            const uint32_t n = forced ? min(run, 16u) : 1u;
-            // pattern positions [q, q+n) (right) or (q-n, q] (left); text the
-            // same number of symbols beyond the span on that side
-            const uint32_t po = right ? q : q + 1u - n;
-            const uint32_t wo = right ? yo : xo - n;
-            const bool inside = right ? (yo + n <= winLen) : (xo >= n);
-            bad = bad || (node && !inside && (right || wb != 0));  // window too small (cannot happen)
-            const uint64_t pv = nib16(P, po, patWords), wv = nib16(W, wo, winWords);
-            const uint64_t mask = n >= 16u ? ~0ull : ((1ull << (4u * n)) - 1ull);
-
-            // forced run: all n symbols must match ('$' / padding never does)
-            const bool runOK = node && forced && inside && ((pv ^ wv) & mask) == 0ull;
-            // single node (not forced): children M/S (the text's symbol), D, I under policy P0
-            const uint32_t cq = (uint32_t)pv & 0xFu;
-            const uint32_t tc = inside ? ((uint32_t)wv & 0xFu) : 0u;
+            const bool forced = e == ub0;  // no error child at this position or the rest of its run
             const bool one = node && !forced;
-            const uint32_t side = right ? lastR : lastL;
+
+            // ---- forced node: up to 8 matches at once
+            const uint32_t nF = min(run0, 8u);
+            bool inF;
+            const bool runOK = node && forced && runEq(P0, r0, 0u, nF, inF);
+            bad = bad || (node && forced && !inF && (r0 || wb != 0));
+
+            // ---- branching node: children M/S (the text's symbol), D, I under policy P0
+            const bool in1 = r0 ? (yo < winLen) : (xo > 0u);
+            const uint32_t tc = in1 ? (r0 ? (TR & 0xFu) : (TL >> 28)) : 0u;
+            const uint32_t cq = r0 ? (P0 & 0xFu) : (P0 >> 28);
+            bad = bad || (one && !in1 && (r0 || wb != 0));
+            const uint32_t side = r0 ? lastR : lastL;
             const bool sym = one && tc != 0u;
-            const bool okM = sym && tc == cq && lb <= e && e <= ub;
-            const bool misOK = lb <= e + 1u && e + 1u <= ub;
-            const bool okS = sym && tc != cq && misOK;
-            const bool okD = EDIT && sym && pos > 0u && e + 1u <= ub && side != OP_I;
-            const bool okI = EDIT && one && misOK && side != OP_D;
-            const uint32_t adv = runOK ? n : 1u;
-            const uint32_t nspan = right ? (xo | ((yo + adv) << 16)) : ((xo - adv) | (yo << 16));
-            const bool nl = pos == 0u;  // pos 0 sets both sides
-            const uint32_t keepL = right && !nl ? lastL : 0xFFu, keepR = !right && !nl ? lastR : 0xFFu;
+            const bool okM = sym && tc == cq && lb0 <= e && e <= ub0;
+            const bool misOK = lb0 <= e + 1u && e + 1u <= ub0;
+            bool okS = sym && tc != cq && misOK;
+            bool okD = EDIT && sym && pos > 0u && e + 1u <= ub0 && side != OP_I;
+            bool okI = EDIT && one && misOK && side != OP_D;
+            // An error child whose own position admits no further error starts
+            // a forced run: check it here (up to 7 symbols) and drop the child
+            // if it mismatches, instead of spending a micro-step on it.
+            const uint32_t nD = min(run0, 7u), n1 = min(run1, 7u);
+            const bool fD = okD && e + 1u == ub0;
+            const bool fS = okS && pos + 1u < m && e + 1u == ub1;
+            const bool fI = okI && pos + 1u < m && e + 1u == ub1;
+            bool inD, inS, inI;
+            const bool eqD = runEq(P0, r0, 1u, nD, inD);
+            const bool eqS = runEq(P1, r1, r1 == r0 ? 1u : 0u, n1, inS);
+            const bool eqI = runEq(P1, r1, 0u, n1, inI);
+            bad = bad || (fD && !inD && (r0 || wb != 0)) || (fS && !inS && (r1 || wb != 0)) ||
+                  (fI && !inI && (r1 || wb != 0));
+            okD = okD && (!fD || eqD);
+            okS = okS && (!fS || eqS);
+            okI = okI && (!fI || eqI);
+
+            // ---- children
+            const bool nl = pos == 0u;  // an operation at pos 0 sets both sides
+            const uint32_t keepL = r0 && !nl ? lastL : 0xFFu, keepR = !r0 && !nl ? lastR : 0xFFu;
             auto sideMeta = [&](uint32_t op) -> uint32_t {
                 return ((keepL == 0xFFu ? op : keepL) << 20) | ((keepR == 0xFFu ? op : keepR) << 22);
             };
-            const uint2 cM = make_uint2(nspan, (pos + adv) | (e << 16) | sideMeta(OP_MS));
-            const uint2 cS = make_uint2(nspan, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_MS));
-            const uint2 cD = make_uint2(nspan, pos | ((e + 1u) << 16) | sideMeta(OP_D));
-            const uint2 cI = make_uint2(cur.x, (pos + 1u) | ((e + 1u) << 16) | sideMeta(OP_I));
+            // after a forced run on side r the last operation there is a match
+            auto runMeta = [&](uint32_t meta, bool r, bool did) -> uint32_t {
+                const uint32_t sh = r ? 22u : 20u;
+                return did ? ((meta & ~(3u << sh)) | (OP_MS << sh)) : meta;
+            };
+            auto extend = [&](uint32_t span, bool r, uint32_t k) -> uint32_t {
+                return r ? span + (k << 16) : span - k;
+            };
+            const uint32_t nspan = extend(cur.x, r0, 1u);  // the text symbol consumed by M/S/D
+            const uint32_t kS = fS ? n1 : 0u, kD = fD ? nD : 0u, kI = fI ? n1 : 0u;
+            const uint2 cM = make_uint2(forced ? extend(cur.x, r0, nF) : nspan,
+                                        (pos + (forced ? nF : 1u)) | (e << 16) | sideMeta(OP_MS));
+            const uint2 cS = make_uint2(extend(nspan, r1, kS),
+                                        (pos + 1u + kS) | ((e + 1u) << 16) | runMeta(sideMeta(OP_MS), r1, fS));
+            const uint2 cD = make_uint2(extend(nspan, r0, kD),
+                                        (pos + kD) | ((e + 1u) << 16) | runMeta(sideMeta(OP_D), r0, fD));
+            const uint2 cI = make_uint2(extend(cur.x, r1, kI),
+                                        (pos + 1u + kI) | ((e + 1u) << 16) | runMeta(sideMeta(OP_I), r1, fI));
             // match child below its error siblings; continue with the first
             // error child (I, then S, then D) or, if none, with the match child.
             // Unconditional stores: slots above the new top are scratch (the
@@ -839,10 +1038,15 @@ void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32
     SH_HIP(hipGetLastError());
 }
 
-void launchResolveTasks(uint4* tasks, uint32_t n, const uint32_t* sa, hipStream_t st) {
-    if (!n) return;
-    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(kResolveTasks, dim3(blocks), dim3(256), 0, st, tasks, n, sa);
+void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st) {
+    if (sigma == 5) hipLaunchKernelGGL((kSeedItems<5>), dim3(blocks), dim3(256), 0, st, a);
+    else            hipLaunchKernelGGL((kSeedItems<6>), dim3(blocks), dim3(256), 0, st, a);
+    SH_HIP(hipGetLastError());
+}
+
+void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const uint32_t* sa, uint32_t blocks,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(kResolveTasks, dim3(blocks), dim3(256), 0, st, tasks, count, cap, sa);
     SH_HIP(hipGetLastError());
 }
 
