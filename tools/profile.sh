@@ -4,7 +4,7 @@
 # Usage: tools_profile.sh <outdir> "<group1>" "<group2>" ... -- [bench args...]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$1; shift
+OUT=$(realpath -m "$1"); shift
 groups=()
 while [ $# -gt 0 ] && [ "$1" != "--" ]; do groups+=("$1"); shift; done
 [ "$1" == "--" ] && shift

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 "$R/bench.py" --no-cpu --no-count "$@" > "$OUT/trace.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "kSearch|kResolve|kLocate" -d "$OUT/pmc_fetch" -o run \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "kSearch|kSeed|kResolve|kLocate" -d "$OUT/pmc_fetch" -o run \
     --output-format csv -- python3 "$R/bench.py" --no-cpu --no-count "$@" > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" || { echo "pmc failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "kGroup" -d "$OUT/calib" -o run \
     --output-format csv -- "$R/tools/gather_bench" > "$OUT/calib.txt" 2> "$OUT/calib.err" || { echo "calib failed"; exit 1; }

@@ -27,7 +27,7 @@ def main(d, out, txt=None):
     stats = {}
     for r in csv.DictReader(open(f"{d}/trace/run_kernel_stats.csv")):
         k = short(r["Name"])
-        if k.startswith("kSearch") or k.startswith("kResolve") or k.startswith("kLocate"):
+        if k.startswith(("kSearch", "kSeed", "kResolve", "kLocate")):
             stats[k] = (int(r["Calls"]), float(r["AverageNs"]) / 1e3)
     # calibration: kGroup<U, G> dispatches: lines = 2048 blocks * 256 / G * 64 iters * U
     cal = []
