@@ -218,6 +218,7 @@ def main():
                                                   + cnt["text_cycles_step"] + cnt["text_cycles_emit"]), 3)
                                       for k in ("refill", "step", "emit")},
                  "text_compare_steps_per_read": round(cnt["text_compare_steps"] / nreads, 1),
+                 "text_steps_per_read": round(cnt["text_steps"] / nreads, 1),
                  "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
                  "search_ms": round(search_ms_step, 2), "text_ms": round(text_ms / args.steps, 2),
                  "locate_ms": round(locate_ms / args.steps, 2),

@@ -86,6 +86,7 @@ typedef struct sahara_stats {
     uint32_t text_grid;          /* text-kernel workgroups per launch */
     uint32_t pipelined;          /* 1 if FM and text phases of consecutive batches overlapped */
     double   seed_ms;            /* starting cursors (k-mer table lookups) */
+    uint64_t text_steps;         /* text-kernel micro-steps, lane count (count=1) */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

@@ -47,7 +47,7 @@ struct Ctx {
     bool verify = true;
     bool locateSA = true;
     uint32_t split = 1;                   // text-phase threshold (rows per interval)
-    uint32_t textSteps = 8;               // text-phase node expansions per lane per wave iteration
+    uint32_t textSteps = 4;               // text-phase micro-steps per lane per wave iteration
     uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
 
     // work buffers. Batches alternate between two slots so that the FM phase
@@ -65,7 +65,7 @@ struct Ctx {
     size_t pinnedCap = 0;
     bool pipeline = true;
     DevBuf<uint4> stack, seeds;           // FM spill stack; starting cursors (stream st only)
-    DevBuf<uint32_t> seedItem;
+    DevBuf<uint32_t> seedItem, dbg;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> rowOff, k0, k1;
@@ -209,7 +209,9 @@ void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, u
 //       from pos (<= 127) on the same side with u == u[pos] and l <= u[pos]:
 //       a node at pos with e == u[pos] has no error child anywhere in that
 //       run, so the DFS is a forced chain of matches through it;
-//   y = a | b << 12 — pattern positions [a, b) covered before step pos.
+//   y = a | b << 12 | same << 24 — pattern positions [a, b) covered before
+//       step pos; `same` (<= run) positions from pos share pos's l as well,
+//       so a chain of matches through them branches the same way at each.
 void textTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
                const std::vector<uint32_t>& packed, std::vector<uint32_t>& out) {
     out.assign((size_t)ns * m * 2, 0);
@@ -221,12 +223,13 @@ void textTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_
         uint32_t a = P[0], b = P[0];
         for (uint32_t p = 0; p < m; ++p) {
             const uint32_t right = (Q[p] >> 24) & 1u;
-            uint32_t run = 1;
+            uint32_t run = 1, same = 1;
             while (run < 127 && p + run < m && ((Q[p + run] >> 24) & 1u) == right && U[p + run] == U[p] &&
                    L[p + run] <= U[p])
                 ++run;
+            while (same < run && L[p + same] == L[p]) ++same;
             out[((size_t)s * m + p) * 2] = Q[p] | (run << 25);
-            out[((size_t)s * m + p) * 2 + 1] = a | (b << 12);
+            out[((size_t)s * m + p) * 2 + 1] = a | (b << 12) | (same << 24);
             a = std::min(a, P[p]);
             b = std::max(b, P[p] + 1);
         }
@@ -315,7 +318,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const uint32_t sigma = c->I.sigma;
     const size_t lds = (size_t)c->nsearch * c->m * 4;
     int bpc = searchBlocksPerCU(sigma, c->edit, lds);
-    if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(bpc, std::atoi(e)));
+    // Overlapped with the text phase of the previous batch, the FM phase
+    // (memory-latency bound) runs with one workgroup per CU and leaves the
+    // CUs' issue slots to the text phase (ALU bound); alone it takes them all.
+    const uint64_t batchesHere = (c->npat + std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch) - 1) /
+                                 std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
+    if (!serial && batchesHere > 1 && c->verify) bpc = 1;
+    if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     const uint64_t T = (uint64_t)blocks * 256;
     const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
@@ -449,6 +458,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.stackCap = textStack;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
+            c->dbg.reserve(16);
+            t.dbg = c->dbg.ptr;
+            SH_HIP(hipMemsetAsync(c->dbg.ptr, 0, 16 * sizeof(uint32_t), sB));
             launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
         }
@@ -470,7 +482,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
         S.text_ms += ms;
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
-        if (hs[2] & 16u) throw Error("text phase: internal window/stack bound violated");
+        if (hs[2] & 16u) {
+            uint32_t d[16] = {};
+            SH_HIP(hipMemcpy(d, c->dbg.ptr, sizeof(d), hipMemcpyDeviceToHost));
+            std::string st;
+            for (int j = 1; j < 16; ++j) st += " " + std::to_string(d[j]);
+            throw Error("text phase: internal window/stack bound violated (pos e lb ub sp nSurv contM B L run same side"
+                        " Dm Im Sx:" + st + ")");
+        }
         if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
             if (hs[2] & 8u) growCap(c->taskCap, hs[4]);
             if (hs[2] & 2u) growCap(c->hitCap, hs[1]);
@@ -580,6 +599,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         S.text_cycles_step = h[12];
         S.text_cycles_emit = h[13];
         S.text_compare_steps = h[14];
+        S.text_steps = h[15];
     }
 }
 

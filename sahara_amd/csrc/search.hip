@@ -545,24 +545,40 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 // up to 8 forced matches at once: the DFS visits the same chain of nodes,
 // one micro-step per 16 of them.
 
-// 8 consecutive nibbles [o, o+8) of an interleaved word array of `words`
-// words (past the end: garbage, callers bound-check)
-__device__ __forceinline__ uint32_t nib8(const uint32_t* A, uint32_t o, uint32_t words) {
-    const uint32_t i = min(o >> 3, words - 1u);
-    const uint32_t w0 = A[i * 256u], w1 = A[min(i + 1u, words - 1u) * 256u];
-    return __builtin_amdgcn_alignbit(w1, w0, (o & 7u) * 4u);
+
+
+// ---- 16-symbol runs as u64 (symbol j in nibble j) and per-symbol bit masks
+// (bit 4j for symbol j)
+constexpr uint64_t kOnes16 = 0x1111111111111111ull;
+__device__ __forceinline__ uint64_t ones16(uint32_t n) {  // symbols [0, n), n <= 16
+    return n >= 16u ? kOnes16 : kOnes16 & ((1ull << (4u * n)) - 1ull);
 }
-// the pattern run read at position q in direction r (branch-free): right ->
-// [q, q+8); left -> [q-7, q] top-aligned (q in nibble 7, zeros below 0)
-__device__ __forceinline__ uint32_t patRun(const uint32_t* A, uint32_t q, bool r, uint32_t words) {
-    const uint32_t o = r ? q : (q >= 7u ? q - 7u : 0u);
-    const uint32_t v = nib8(A, o, words);
-    return (!r && q < 7u) ? v << (4u * (7u - q)) : v;
+__device__ __forceinline__ uint64_t beyond16(uint32_t n) { return kOnes16 & ~ones16(n); }  // symbols >= n
+__device__ __forceinline__ uint64_t nz16(uint64_t x) { return (x | (x >> 1) | (x >> 2) | (x >> 3)) & kOnes16; }
+__device__ __forceinline__ uint64_t eq16(uint64_t a, uint64_t b) { return ~nz16(a ^ b) & kOnes16; }
+// bit 4j set iff bits 4j .. 4(j+6) are all set (7 consecutive matches from j)
+__device__ __forceinline__ uint64_t run7(uint64_t m) {
+    const uint64_t m2 = m & (m >> 4), m4 = m2 & (m2 >> 8);
+    return m4 & (m2 >> 16) & (m >> 24);
 }
-// the 8 nibbles [end-8, end), zero where end-8+i < 0 (nibble 7 = end-1)
-__device__ __forceinline__ uint32_t left8(const uint32_t* A, uint32_t end, uint32_t words) {
-    const uint32_t v = nib8(A, end >= 8u ? end - 8u : 0u, words);
-    return end >= 8u ? v : (end == 0u ? 0u : v << (32u - 4u * end));
+// nibbles [o, o+16) of an interleaved word array (reads may run past the
+// array into the lane's next region; callers mask)
+__device__ __forceinline__ uint64_t read16(const uint32_t* A, uint32_t o) {
+    const uint32_t i = o >> 3, sh = (o & 7u) * 4u;
+    const uint32_t w0 = A[i * 256u], w1 = A[(i + 1u) * 256u], w2 = A[(i + 2u) * 256u];
+    return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
+}
+// nibbles [end-16, end) (zeros below 0), natural order
+__device__ __forceinline__ uint64_t left16(const uint32_t* A, uint32_t end) {
+    const uint64_t v = read16(A, end >= 16u ? end - 16u : 0u);
+    return end >= 16u ? v : (end == 0u ? 0ull : v << (4u * (16u - end)));
+}
+__device__ __forceinline__ uint32_t revNib32(uint32_t x) {
+    x = __builtin_bswap32(x);
+    return ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+}
+__device__ __forceinline__ uint64_t rev16(uint64_t v) {
+    return (uint64_t)revNib32((uint32_t)(v >> 32)) | ((uint64_t)revNib32((uint32_t)v) << 32);
 }
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -641,7 +657,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     }
     SlotRange hitSlots;
     uint2 cur = make_uint2(0, 0);
-    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0;
+    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
 
     for (;;) {
@@ -730,115 +746,140 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
             const uint32_t e = (cur.y >> 16) & 0xFu;
             const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
-            const uint32_t t0 = SC[sBase + min(pos, m - 1u)].x;       // this step
-            const uint32_t t1 = SC[sBase + min(pos + 1u, m - 1u)].x;  // the next step (children S, I)
+            const uint2 tab = SC[sBase + min(pos, m - 1u)];
+            const uint32_t t0 = tab.x;
             const uint32_t q0 = t0 & 0xFFFFu, lb0 = (t0 >> 16) & 0xFu, ub0 = (t0 >> 20) & 0xFu;
             const bool r0 = (t0 >> 24) & 1u;
-            const uint32_t run0 = t0 >> 25;
-            const uint32_t q1 = t1 & 0xFFFFu, ub1 = (t1 >> 20) & 0xFu;
-            const bool r1 = (t1 >> 24) & 1u;
-            const uint32_t run1 = t1 >> 25;
+            const uint32_t run0 = t0 >> 25, same0 = (tab.y >> 24) & 0x7Fu;
 
-            // ---- reads (8 symbols each): the text on both sides of the span —
-            // TR = t[yo, yo+8), TL = t[xo-8, xo) — and the pattern runs at
-            // pi[pos] and pi[pos+1] in their directions (a left run is read
-            // top-aligned: its first symbol, pi[.], in the top nibble).
-            const uint32_t TR = nib8(W, yo, winWords);
-            const uint32_t TL = left8(W, xo, winWords);
-            const uint32_t P0 = patRun(P, q0, r0, patWords), P1 = patRun(P, q1, r1, patWords);
-            // does the pattern run Pw (k symbols) match the text on side r
-            // beyond the span, after skipping s symbols a sibling consumed?
-            // '$', the text's ends and window padding (0) never match.
-            auto runEq = [&](uint32_t Pw, bool r, uint32_t s, uint32_t k, bool& in) -> bool {
-                in = r ? (yo + s + k <= winLen) : (s + k <= xo);
-                const uint32_t sh = 32u - 4u * k;
-                const uint32_t d = r ? (((TR >> (4u * s)) ^ Pw) << sh) : (((TL << (4u * s)) ^ Pw) >> sh);
-                return in && d == 0u;
-            };
+            // ---- 16 pattern symbols from pi[pos] in this step's direction and
+            // the 16 text symbols beyond the span on that side, both in chain
+            // order (symbol j of the chain in nibble j); text past the window
+            // edge or before the text start reads as 0 and never matches
+            const uint64_t P16 = r0 ? read16(P, q0) : rev16(left16(P, q0 + 1u));
+            const uint64_t T16 = r0 ? read16(W, yo) : rev16(left16(W, xo));
+            const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
+            const uint64_t VT = ones16(min(avail, 16u));
+            const uint64_t E0 = eq16(P16, T16) & VT;                // p_j == t_j     (M chain, S runs)
+            const uint64_t ED = eq16(P16, T16 >> 4) & (VT >> 4);    // p_j == t_{j+1} (D runs)
+            const uint64_t EI = eq16(P16 >> 4, T16) & VT;           // p_{j+1} == t_j (I runs)
+            const uint64_t TZ = nz16(T16) & VT;                     // t_j is a symbol (not '$' / edge)
 
             const bool atLeaf = live && pos == m;
             const bool node = live && pos < m;
-            const bool forced = e == ub0;  // no error child at this position or the rest of its run
-            const bool one = node && !forced;
-
-            // ---- forced node: up to 8 matches at once
-            const uint32_t nF = min(run0, 8u);
-            bool inF;
-            const bool runOK = node && forced && runEq(P0, r0, 0u, nF, inF);
-            bad = bad || (node && forced && !inF && (r0 || wb != 0));
-
-            // ---- branching node: children M/S (the text's symbol), D, I under policy P0
-            const bool in1 = r0 ? (yo < winLen) : (xo > 0u);
-            const uint32_t tc = in1 ? (r0 ? (TR & 0xFu) : (TL >> 28)) : 0u;
-            const uint32_t cq = r0 ? (P0 & 0xFu) : (P0 >> 28);
-            bad = bad || (one && !in1 && (r0 || wb != 0));
-            const uint32_t side = r0 ? lastR : lastL;
-            const bool sym = one && tc != 0u;
-            const bool okM = sym && tc == cq && lb0 <= e && e <= ub0;
+            const bool forced = e == ub0;          // no error child here or in the rest of the run
+            const bool kidsF = e + 1u == ub0;      // the error children are forced nodes
+            const bool mOK = lb0 <= e && e <= ub0;
             const bool misOK = lb0 <= e + 1u && e + 1u <= ub0;
-            bool okS = sym && tc != cq && misOK;
-            bool okD = EDIT && sym && pos > 0u && e + 1u <= ub0 && side != OP_I;
-            bool okI = EDIT && one && misOK && side != OP_D;
-            // An error child whose own position admits no further error starts
-            // a forced run: check it here (up to 7 symbols) and drop the child
-            // if it mismatches, instead of spending a micro-step on it.
-            const uint32_t nD = min(run0, 7u), n1 = min(run1, 7u);
-            const bool fD = okD && e + 1u == ub0;
-            const bool fS = okS && pos + 1u < m && e + 1u == ub1;
-            const bool fI = okI && pos + 1u < m && e + 1u == ub1;
-            bool inD, inS, inI;
-            const bool eqD = runEq(P0, r0, 1u, nD, inD);
-            const bool eqS = runEq(P1, r1, r1 == r0 ? 1u : 0u, n1, inS);
-            const bool eqI = runEq(P1, r1, 0u, n1, inI);
-            bad = bad || (fD && !inD && (r0 || wb != 0)) || (fS && !inS && (r1 || wb != 0)) ||
-                  (fI && !inI && (r1 || wb != 0));
-            okD = okD && (!fD || eqD);
-            okS = okS && (!fS || eqS);
-            okI = okI && (!fI || eqI);
+            const uint32_t side = r0 ? lastR : lastL;
+            // chain budget: a forced node matches up to 16 symbols; a node whose
+            // error children are forced walks up to 8 positions of its match
+            // chain (same direction, l and u), checking every error child's
+            // forced run on the way; any other node is expanded alone
+            const uint32_t B = forced ? min(run0, 16u)
+                                      : (kidsF ? max(1u, min(min(same0, run0 - 1u), 8u)) : 1u);
+            const uint64_t miss = ~E0 & kOnes16;
+            const uint32_t L = mOK ? min(B, miss ? (uint32_t)__builtin_ctzll(miss) >> 2 : 16u) : 0u;
 
-            // ---- children
-            const bool nl = pos == 0u;  // an operation at pos 0 sets both sides
-            const uint32_t keepL = r0 && !nl ? lastL : 0xFFu, keepR = !r0 && !nl ? lastR : 0xFFu;
-            auto sideMeta = [&](uint32_t op) -> uint32_t {
-                return ((keepL == 0xFFu ? op : keepL) << 20) | ((keepR == 0xFFu ? op : keepR) << 22);
+            // ---- error children of the chain nodes i < NN (node L = the mismatch)
+            const uint32_t NN = L < B ? L + 1u : B;
+            const uint64_t nodesM = node && !forced ? ones16(NN) : 0ull;  // leaves / idle lanes: none
+            const uint64_t first = 1ull;  // chain node 0 (= this node)
+            uint64_t Dm = EDIT ? (nodesM & TZ) : 0ull;
+            if (pos == 0u || side == OP_I) Dm &= ~first;
+            uint64_t Im = EDIT && misOK ? nodesM : 0ull;
+            if (side == OP_D) Im &= ~first;
+            // S at the first mismatch (not where M is merely disallowed: l > e)
+            bool Sx = node && !forced && L < B && misOK && ((TZ & ~E0) >> (4u * L)) & 1ull;
+            if (kidsF) {
+                // forced runs: D at i needs p[i..] == t[i+1..], I at i needs
+                // p[i+1..] == t[i..], S at L needs p[L+1..] == t[L+1..], each for
+                // min(7, rest of the run) symbols (positions past the run count as matches)
+                Dm &= run7(ED | beyond16(run0));
+                Im &= run7(EI | beyond16(run0 - 1u));
+                Sx = Sx && ((run7(E0 | beyond16(run0)) >> (4u * (L + 1u))) & 1ull);
+            }
+            const bool contM = node && L >= B;  // the match chain continues at pos + B
+            uint32_t nSurv = (uint32_t)__popcll(Dm) + (uint32_t)__popcll(Im) + (Sx ? 1u : 0u);
+            // the lane continues with one child and stacks the others: a
+            // surviving error child first, the match chain below it
+            uint32_t Bc = B;
+            // Stack invariant (stackCap = 2k + 2): a node that stacks entries
+            // with e errors finds sp <= 2e + 2. One node expanded alone stacks
+            // <= 2; a chain may stack more only while the child it continues
+            // with (e + 1) still finds sp <= 2(e + 1) + 2.
+            if (nSurv && sp + nSurv + (contM ? 1u : 0u) - 1u > 2u * e + 4u) {
+                // not enough stack for this chain: expand its first node only
+                Bc = 1u;
+                Dm &= first;
+                Im &= first;
+                Sx = Sx && L == 0u;
+                nSurv = (uint32_t)__popcll(Dm) + (uint32_t)__popcll(Im) + (Sx ? 1u : 0u);
+            }
+            const bool contM1 = node && L >= Bc;
+            if (node && nSurv && sp + nSurv + (contM1 ? 1u : 0u) - 1u > a.stackCap) {
+                bad = true;
+                if (a.dbg && atomicCAS(a.dbg, 0u, 1u) == 0u) {  // first violation: keep the lane's state
+                    const uint32_t v[15] = {pos, e, lb0, ub0, sp, nSurv, contM1, B, L, run0, same0, side,
+                                            (uint32_t)Dm, (uint32_t)Im, Sx};
+                    for (int j = 0; j < 15; ++j) a.dbg[1 + j] = v[j];
+                }
+            }
+
+            // ---- children as stack entries (x = span, y = meta)
+            auto extend = [&](uint32_t span, uint32_t k) -> uint32_t { return r0 ? span + (k << 16) : span - k; };
+            // side memory after i chain matches, then op at chain node i, then
+            // k forced matches; pos 0 operations set both sides
+            auto metaAt = [&](uint32_t i, uint32_t op, uint32_t k) -> uint32_t {
+                uint32_t ml = lastL, mr = lastR;
+                if (i > 0u) {
+                    if (pos == 0u) ml = mr = OP_MS;
+                    else if (r0) mr = OP_MS;
+                    else ml = OP_MS;
+                }
+                if (pos + i == 0u) ml = mr = op;
+                else if (r0) mr = op;
+                else ml = op;
+                if (k) { if (r0) mr = OP_MS; else ml = OP_MS; }
+                return (ml << 20) | (mr << 22);
             };
-            // after a forced run on side r the last operation there is a match
-            auto runMeta = [&](uint32_t meta, bool r, bool did) -> uint32_t {
-                const uint32_t sh = r ? 22u : 20u;
-                return did ? ((meta & ~(3u << sh)) | (OP_MS << sh)) : meta;
-            };
-            auto extend = [&](uint32_t span, bool r, uint32_t k) -> uint32_t {
-                return r ? span + (k << 16) : span - k;
-            };
-            const uint32_t nspan = extend(cur.x, r0, 1u);  // the text symbol consumed by M/S/D
-            const uint32_t kS = fS ? n1 : 0u, kD = fD ? nD : 0u, kI = fI ? n1 : 0u;
-            const uint2 cM = make_uint2(forced ? extend(cur.x, r0, nF) : nspan,
-                                        (pos + (forced ? nF : 1u)) | (e << 16) | sideMeta(OP_MS));
-            const uint2 cS = make_uint2(extend(nspan, r1, kS),
-                                        (pos + 1u + kS) | ((e + 1u) << 16) | runMeta(sideMeta(OP_MS), r1, fS));
-            const uint2 cD = make_uint2(extend(nspan, r0, kD),
-                                        (pos + kD) | ((e + 1u) << 16) | runMeta(sideMeta(OP_D), r0, fD));
-            const uint2 cI = make_uint2(extend(cur.x, r1, kI),
-                                        (pos + 1u + kI) | ((e + 1u) << 16) | runMeta(sideMeta(OP_I), r1, fI));
-            // match child below its error siblings; continue with the first
-            // error child (I, then S, then D) or, if none, with the match child.
-            // Unconditional stores: slots above the new top are scratch (the
-            // stack never exceeds 2k entries, stackCap = 2k + 2).
-            const uint32_t nErr = (okI ? 1u : 0u) + (okS ? 1u : 0u) + (okD ? 1u : 0u);
-            const uint32_t pa = okM && nErr ? 1u : 0u, pb = okI && okS ? 1u : 0u;
-            const uint32_t pc = (okI || okS) && okD ? 1u : 0u;
-            bad = bad || (sp + pa + pb + pc > a.stackCap);
-            const uint32_t cap1 = a.stackCap - 1u;
-            const uint32_t spw = min(sp, cap1);
-            S[spw * 256u] = cM;
-            S[min(spw + pa, cap1) * 256u] = cS;
-            S[min(spw + pa + pb, cap1) * 256u] = cD;
-            sp = min(sp + pa + pb + pc, a.stackCap);
+            const uint32_t e1 = (e + 1u) << 16;
+            auto runLen = [&](uint32_t i) -> uint32_t { return kidsF ? min(run0 - i, 7u) : 0u; };
+            const uint2 cM = make_uint2(extend(cur.x, Bc), (pos + Bc) | (e << 16) | metaAt(Bc, OP_MS, 0u));
+            if (nSurv) {  // rare: the surviving error children; the last one stays in registers
+                uint32_t spw = sp;
+                uint2 pend = cM;
+                bool hasPend = contM1;
+                auto emit = [&](const uint2& v) {
+                    if (hasPend) S[min(spw++, a.stackCap - 1u) * 256u] = pend;
+                    pend = v;
+                    hasPend = true;
+                };
+                for (uint64_t d = Dm; d; d &= d - 1ull) {
+                    const uint32_t i = (uint32_t)__builtin_ctzll(d) >> 2, k = runLen(i);
+                    emit(make_uint2(extend(cur.x, i + 1u + k), (pos + i + k) | e1 | metaAt(i, OP_D, k)));
+                }
+                for (uint64_t d = Im; d; d &= d - 1ull) {
+                    const uint32_t i = (uint32_t)__builtin_ctzll(d) >> 2, k = i + 1u < run0 ? runLen(i + 1u) : 0u;
+                    emit(make_uint2(extend(cur.x, i + k), (pos + i + 1u + k) | e1 | metaAt(i, OP_I, k)));
+                }
+                if (Sx) {
+                    const uint32_t k = L + 1u < run0 ? runLen(L + 1u) : 0u;
+                    emit(make_uint2(extend(cur.x, L + 1u + k), (pos + L + 1u + k) | e1 | metaAt(L, OP_MS, k)));
+                }
+                sp = min(spw, a.stackCap);
+                cur = pend;
+            } else if (node && contM1) {
+                cur = cM;
+            }
 
             if (atLeaf) { leaf = true; leafStart = xo; leafE = e; }
-            if (node) cur = okI ? cI : (okS ? cS : (okD ? cD : cM));
-            if (live) have = runOK || nErr != 0u || okM;
-            if (COUNT) { cNodes += one ? 1u : 0u; cCmp += (node && forced) ? 1u : 0u; }
+            if (live) have = node && (nSurv || contM1);
+            if (COUNT) {
+                cNodes += forced ? 0u : (node ? NN : 0u);
+                cCmp += (node && forced) ? 1u : 0u;
+                cSteps += node ? 1u : 0u;
+            }
         }
         if (COUNT) {
             const uint64_t t1 = clock64();
@@ -869,6 +910,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             atomicAdd(a.counters + 13, (unsigned long long)cyEmit);
         }
         atomicAdd(a.counters + 14, (unsigned long long)cCmp);
+        atomicAdd(a.counters + 15, (unsigned long long)cSteps);
     }
 }
 

@@ -1,0 +1,77 @@
+"""The text kernel's chain micro-step (modelled in tests/text_model.py) yields
+the same leaf multiset as the plain P0 DFS against the text, from arbitrary
+DFS states, within the 2k + 2 stack bound."""
+import random
+
+import pytest
+
+import oracle
+from text_model import D_, I_, MS, chain, plain, sides
+
+
+def states(P, T, sch, edit, limit=300):
+    """DFS nodes from every start position (what the FM phase could hand over)."""
+    pi, l, u, dirs = sch
+    m = len(pi)
+    out = []
+    for start in range(len(T) + 1):
+        st = [(start, start, 0, 0, 0, 0)]
+        while st and len(out) < limit:
+            node = st.pop()
+            xs, ye, pos, e, lL, lR = node
+            if ye - xs >= 3:
+                out.append(node)
+            if pos == m:
+                continue
+            q, r = pi[pos], dirs[pos]
+            side = lR if r else lL
+            c = (T[ye] if ye < len(T) else 0) if r else (T[xs - 1] if xs > 0 else 0)
+            mOK, misOK = l[pos] <= e <= u[pos], l[pos] <= e + 1 <= u[pos]
+            delOK = edit and pos > 0 and e + 1 <= u[pos] and side != I_
+            insOK = edit and misOK and side != D_
+            a, b = (xs, ye + 1) if r else (xs - 1, ye)
+            if c != 0:
+                if c == P[q]:
+                    if mOK:
+                        st.append((a, b, pos + 1, e) + sides(pos, r, lL, lR, MS))
+                elif misOK:
+                    st.append((a, b, pos + 1, e + 1) + sides(pos, r, lL, lR, MS))
+                if delOK:
+                    st.append((a, b, pos, e + 1) + sides(pos, r, lL, lR, D_))
+            if insOK:
+                st.append((xs, ye, pos + 1, e + 1) + sides(pos, r, lL, lR, I_))
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_chain_step_equals_plain_dfs(seed):
+    rng = random.Random(seed)
+    checked = 0
+    for _ in range(60):
+        m, k = rng.randint(8, 36), rng.randint(1, 3)
+        gen = rng.choice(["h2-k2", "h2-k1", "pigeon", "backtracking", "h2-k3"])
+        ham = rng.random() < 0.3
+        pi, l, u = oracle.scheme(gen, 0, k, m, hamming=ham)
+        s = rng.randrange(len(pi))
+        pi, l, u = [int(v) for v in pi[s]], [int(v) for v in l[s]], [int(v) for v in u[s]]
+        dirs = [pi[p] > pi[p - 1] if p else (pi[1] > pi[0] if m > 1 else True) for p in range(m)]
+        sig = rng.choice([2, 3, 4])  # small alphabets: repeats, many surviving children
+        P = [rng.randint(1, sig) for _ in range(m)]
+        T = [rng.randint(1, sig) for _ in range(8)] + P[:] + [rng.randint(1, sig) for _ in range(8)]
+        for _ in range(rng.randint(0, 3)):
+            T[rng.randrange(8, 8 + m)] = rng.randint(1, sig)
+        for _ in range(rng.randint(0, 2)):
+            j = rng.randrange(8, 8 + m)
+            if rng.random() < 0.5:
+                del T[j]
+            else:
+                T.insert(j, rng.randint(1, sig))
+        if rng.random() < 0.2:
+            T[rng.randrange(len(T))] = 0  # a delimiter
+        edit = not ham
+        cap = 2 * max(max(u), 1) + 2
+        nodes = states(P, T, (pi, l, u, dirs), edit)
+        for task in rng.sample(nodes, min(5, len(nodes))):
+            assert chain(P, T, task, (pi, l, u, dirs), edit, cap=cap) == plain(P, T, task, (pi, l, u, dirs), edit)
+            checked += 1
+    assert checked > 100
