@@ -568,11 +568,6 @@ __device__ __forceinline__ uint64_t read16(const uint32_t* A, uint32_t o) {
     const uint32_t w0 = A[i * 256u], w1 = A[(i + 1u) * 256u], w2 = A[(i + 2u) * 256u];
     return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
 }
-// nibbles [end-16, end) (zeros below 0), natural order
-__device__ __forceinline__ uint64_t left16(const uint32_t* A, uint32_t end) {
-    const uint64_t v = read16(A, end >= 16u ? end - 16u : 0u);
-    return end >= 16u ? v : (end == 0u ? 0ull : v << (4u * (16u - end)));
-}
 __device__ __forceinline__ uint32_t revNib32(uint32_t x) {
     x = __builtin_bswap32(x);
     return ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
@@ -756,8 +751,16 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             // the 16 text symbols beyond the span on that side, both in chain
             // order (symbol j of the chain in nibble j); text past the window
             // edge or before the text start reads as 0 and never matches
-            const uint64_t P16 = r0 ? read16(P, q0) : rev16(left16(P, q0 + 1u));
-            const uint64_t T16 = r0 ? read16(W, yo) : rev16(left16(W, xo));
+            // one read each at a side-dependent offset (a left run ends at the
+            // position and is reversed), so the lanes of both sides share it
+            const uint32_t pOff = r0 ? q0 : (q0 >= 15u ? q0 - 15u : 0u);
+            const uint32_t tOff = r0 ? yo : (xo >= 16u ? xo - 16u : 0u);
+            const uint64_t pr = read16(P, pOff), tr = read16(W, tOff);
+            const uint32_t pSh = !r0 && q0 < 15u ? 4u * (15u - q0) : 0u;
+            const uint32_t tSh = !r0 && xo < 16u ? 4u * (16u - xo) : 0u;
+            const uint64_t pa = pr << pSh, ta = tSh >= 64u ? 0ull : tr << tSh;
+            const uint64_t P16 = r0 ? pa : rev16(pa);
+            const uint64_t T16 = r0 ? ta : rev16(ta);
             const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
             const uint64_t VT = ones16(min(avail, 16u));
             const uint64_t E0 = eq16(P16, T16) & VT;                // p_j == t_j     (M chain, S runs)
