@@ -33,6 +33,16 @@
 
 using namespace sahara_cli;
 
+namespace sahara_cli {
+struct ReadSimulatorArgs {
+    std::string input, output;
+    size_t lineLength = 80, readLength = 150, nreads = 1000, sub = 0, ins = 0, del = 0, errors = 0;
+    uint32_t seed = 0;
+    bool haveInput = false;
+};
+int runReadSimulator(const ReadSimulatorArgs& a);  // read_simulator.cpp
+}  // namespace sahara_cli
+
 namespace {
 
 struct CliError : std::runtime_error {
@@ -438,6 +448,32 @@ int cmdSearch(int argc, char** argv) {
     return 0;
 }
 
+// `sahara read_simulator` (src/sahara/read_simulator.cpp:13-82)
+int cmdReadSimulator(int argc, char** argv) {
+    Opt input{{"-i", "--input"}}, output{{"-o", "--output"}}, width{{"--fasta_line_length"}, false, "80"};
+    Opt len{{"-l", "--read_length"}, false, "150"}, n{{"-n", "--number_of_reads"}, false, "1000"};
+    Opt sub{{"--substitution_errors"}, false, "0"}, ins{{"--insertion_errors"}, false, "0"};
+    Opt del{{"--deletion_errors"}, false, "0"}, err{{"-e", "--errors"}, false, "0"}, seed{{"--seed"}, false, "0"};
+    Parser p;
+    for (Opt* o : {&input, &output, &width, &len, &n, &sub, &ins, &del, &err, &seed}) p.add(*o);
+    p.parse(argc, argv, 2);
+    if (!p.positional.empty()) throw CliError("unexpected argument " + p.positional[0]);
+    if (!output.given) throw CliError("option -o/--output is required");
+    ReadSimulatorArgs a;
+    a.haveInput = input.given;
+    a.input = input.value;
+    a.output = output.value;
+    a.lineLength = toU64(width.value, "--fasta_line_length");
+    a.readLength = toU64(len.value, "--read_length");
+    a.nreads = toU64(n.value, "--number_of_reads");
+    a.sub = toU64(sub.value, "--substitution_errors");
+    a.ins = toU64(ins.value, "--insertion_errors");
+    a.del = toU64(del.value, "--deletion_errors");
+    a.errors = toU64(err.value, "--errors");
+    a.seed = (uint32_t)toU64(seed.value, "--seed");
+    return runReadSimulator(a);
+}
+
 void help() {
     std::printf(
         "sahara - readmapper (MI355X build)\n"
@@ -445,6 +481,9 @@ void help() {
         "  sahara search -q <fasta> -i <index> [-o <out>] [-g <generator>] [-e <k>] [--no-reverse]\n"
         "                [-m all|besthits] [-d ham|lev] [--max_hits <n>] [--limit_queries <n>]\n"
         "                [--gpus <N>] [--emit-errors] [--fm-only]\n"
+        "  sahara read_simulator -o <fasta> [-i <reference>] [-l <len>] [-n <reads>] [-e <errors>]\n"
+        "                [--substitution_errors n] [--insertion_errors n] [--deletion_errors n]\n"
+        "                [--fasta_line_length n] [--seed s]\n"
         "  sahara search_scheme list-generators\n");
 }
 
@@ -459,6 +498,7 @@ int main(int argc, char** argv) {
         const std::string cmd = argv[1];
         if (cmd == "index") return cmdIndex(argc, argv);
         if (cmd == "search") return cmdSearch(argc, argv);
+        if (cmd == "read_simulator") return cmdReadSimulator(argc, argv);
         if (cmd == "search_scheme" && argc >= 3 && std::string(argv[2]) == "list-generators") {
             const char* names[64];
             const char* descs[64];

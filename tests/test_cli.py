@@ -181,3 +181,93 @@ def test_cli_errors_after_index_load(tmp_path, gpu_device):
     rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
                      "-g", "nope")
     assert rc == 1 and 'unknown search scheme generetaror "nope"' in err
+
+
+# ------------------------------------------------------- read_simulator ----
+
+def parse_sim(path):
+    recs, head = [], None
+    for line in open(path):
+        line = line.rstrip("\n")
+        if line.startswith(">"):
+            head = line[1:]
+            recs.append([head, ""])
+        else:
+            recs[-1][1] += line
+    return recs
+
+
+def apply_transcript(ref, pos, trans, read):
+    """The read_simulator.cpp:204-231 semantics, checked against its output."""
+    p = j = 0
+    for t in trans:
+        if t == "M":
+            assert read[j] == ref[pos + p]
+            p += 1
+            j += 1
+        elif t == "S":
+            assert read[j] != ref[pos + p]
+            p += 1
+            j += 1
+        elif t == "I":
+            j += 1
+        elif t == "D":
+            p += 1
+    assert j == len(read)
+
+
+def test_read_simulator_transcripts_and_determinism(tmp_path):
+    ref = os.path.join(GOLD, "ref_b.fa")  # ACGT only
+    seq = "".join(l.strip() for l in open(ref) if not l.startswith(">"))
+    args = ["read_simulator", "-i", ref, "-l", 60, "-n", 50, "-e", 3, "--seed", 5, "--fasta_line_length", 25]
+    rc, out, err = run(*args, "-o", tmp_path / "a.fa")
+    assert rc == 0, err
+    assert out == "loaded fasta file - start simulating\n"
+    assert run(*args, "-o", tmp_path / "b.fa")[0] == 0
+    assert (tmp_path / "a.fa").read_bytes() == (tmp_path / "b.fa").read_bytes()
+    lines = open(tmp_path / "a.fa").read().splitlines()
+    assert all(len(l) <= 25 for l in lines if not l.startswith(">"))
+    recs = parse_sim(tmp_path / "a.fa")
+    assert len(recs) == 50
+    for i, (head, read) in enumerate(recs):
+        m = __import__("re").fullmatch(r"simulated-(\d+) \(seqid:(\d+), pos:(\d+), trans:([MSID]+)\)", head)
+        assert m and int(m.group(1)) == i and int(m.group(2)) == 0
+        trans = m.group(4)
+        assert len(read) == 60 and sum(c != "M" for c in trans) == 3
+        apply_transcript(seq, int(m.group(3)), trans, read)
+    rc, _, _ = run("read_simulator", "-i", ref, "-l", 60, "-n", 50, "-e", 3, "--seed", 6, "-o", tmp_path / "c.fa")
+    assert rc == 0 and (tmp_path / "c.fa").read_bytes() != (tmp_path / "a.fa").read_bytes()
+
+
+def test_read_simulator_random_mode_and_errors(tmp_path):
+    rc, out, _ = run("read_simulator", "-l", 33, "-n", 7, "-o", tmp_path / "r.fa")
+    assert rc == 0 and out.startswith("no fasta file")
+    recs = parse_sim(tmp_path / "r.fa")
+    assert [h for h, _ in recs] == [f"simulated-{i}" for i in range(7)]
+    assert all(len(s) == 33 and set(s) <= set("ACGT") for _, s in recs)
+    assert run("read_simulator", "-n", 3)[0] == 1  # -o is required
+    # more substitutions than positions: the reference's transcript error
+    rc, _, err = run("read_simulator", "-i", os.path.join(GOLD, "ref_b.fa"), "-l", 4,
+                     "--substitution_errors", 5, "-o", tmp_path / "x.fa")
+    assert rc == 1 and "no more matches" in err
+
+
+@pytest.mark.gpu
+def test_cli_simulated_reads_are_found(tmp_path, gpu_device):
+    """read_simulator -> search: every read's simulated origin is among its hits."""
+    ref = os.path.join(GOLD, "ref_b.fa")  # ACGT only: the simulator's reference equals the index's
+    rc, _, err = run("read_simulator", "-i", ref, "-l", 50, "-n", 200, "-e", 2, "-o", tmp_path / "r.fa")
+    assert rc == 0, err
+    out = tmp_path / "h.txt"
+    rc, _, err = run("search", "-q", tmp_path / "r.fa", "-i", os.path.join(GOLD, IDX["b"]), "-e", 2, "-o", out)
+    assert rc == 0, err
+    hits = read_hits(out, 3)
+    found = {(int(q), int(s), int(p)) for q, s, p in hits.tolist()}
+    import re
+    for i, (head, _) in enumerate(parse_sim(tmp_path / "r.fa")):
+        m = re.search(r"seqid:(\d+), pos:(\d+), trans:([MSID]+)", head)
+        seqid, pos, trans = int(m.group(1)), int(m.group(2)), m.group(3)
+        lead_d = len(trans) - len(trans.lstrip("D"))  # leading deletions shift the start (policy P0)
+        lead_i = len(trans) - len(trans.lstrip("I"))
+        starts = {pos + k for k in range(0, lead_d + 1)} | {pos}
+        assert any((2 * i, seqid, p) in found for p in starts) or lead_i > 0, (i, head)
