@@ -168,6 +168,14 @@ int  sahara_scheme_generators(const char** names, const char** descs, int cap);
  * -2 capacity, -3 len shorter than the number of parts. */
 int  sahara_scheme(const char* generator, int min_k, int max_k, uint32_t len, int hamming,
                    uint32_t* pi, uint32_t* l, uint32_t* u, int max_searches);
+/* --dynamic_generator (expandByWNCTopDown, search.cpp:192-195, 202-205):
+ * like sahara_scheme, but the part sizes (written to part_sizes, one per part)
+ * minimise the summed weighted node count for `sigma` and a text of text_len
+ * symbols (edit != 0: counted with I/D edges). Returns the number of
+ * searches; -1 unknown generator, -2 capacity, -3 len < parts. */
+int  sahara_scheme_dynamic(const char* generator, int min_k, int max_k, uint32_t len, int hamming, int edit,
+                           int sigma, double text_len, uint32_t* part_sizes, int max_parts, uint32_t* pi,
+                           uint32_t* l, uint32_t* u, int max_searches);
 /* Part-level (unexpanded) scheme: *parts = number of parts P; n_searches*P
  * entries per array. Returns the number of searches. */
 int  sahara_scheme_parts(const char* generator, int min_k, int max_k, int* parts, int* pi, int* l, int* u,

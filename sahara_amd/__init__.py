@@ -96,6 +96,8 @@ EXPORTED = {
     "sahara_scheme_generators": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int]),
     "sahara_scheme": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_int, u32p, u32p, u32p,
                                 C.c_int]),
+    "sahara_scheme_dynamic": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                        C.c_double, u32p, C.c_int, u32p, u32p, u32p, C.c_int]),
     "sahara_scheme_parts": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_int),
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                       C.c_int]),
@@ -345,6 +347,25 @@ def search_scheme(generator, min_k, max_k, length, hamming=False):
     if rc != n:
         raise SaharaError(f"cannot expand scheme {generator} to length {length} (rc={rc})")
     return pi, l, u
+
+
+def search_scheme_dynamic(generator, min_k, max_k, length, hamming=False, edit=True, sigma=6, text_len=3e9):
+    """--dynamic_generator: expanded scheme with WNC-optimised part sizes -> ((pi, l, u), sizes)."""
+    L = lib()
+    n = L.sahara_scheme_dynamic(generator.encode(), min_k, max_k, length, int(hamming), int(edit), sigma,
+                                float(text_len), None, 0, None, None, None, 0)
+    if n < 0:
+        raise SaharaError(f"unknown search scheme generator {generator!r}")
+    sizes = np.zeros(64, np.uint32)
+    pi = np.zeros((n, length), np.uint32)
+    l = np.zeros((n, length), np.uint32)
+    u = np.zeros((n, length), np.uint32)
+    rc = L.sahara_scheme_dynamic(generator.encode(), min_k, max_k, length, int(hamming), int(edit), sigma,
+                                 float(text_len), _p(sizes, u32p), 64, _p(pi, u32p), _p(l, u32p), _p(u, u32p), n)
+    if rc != n:
+        raise SaharaError(f"cannot expand scheme {generator} to length {length} (rc={rc})")
+    P = scheme_parts(generator, min_k, max_k)[0].shape[1]
+    return (pi, l, u), sizes[:P].copy()
 
 
 def scheme_parts(generator, min_k, max_k):

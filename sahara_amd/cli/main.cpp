@@ -354,7 +354,6 @@ int cmdSearch(int argc, char** argv) {
         if (!known)
             throw CliError("unknown search scheme generetaror \"" + gen.value + "\", valid generators are: " + all);
     }
-    if (dyn.given) throw CliError("--dynamic_generator (expandByWNCTopDown) is not supported by this build");
     const uint32_t len = (uint32_t)queries[0].size();
     for (size_t i = 0; i < queries.size(); ++i)
         if (queries[i].size() != len)
@@ -368,15 +367,40 @@ int cmdSearch(int argc, char** argv) {
     std::vector<std::vector<uint8_t>>().swap(queries);
 
     std::vector<Scheme> schemes;  // all: [0..k]; besthits: one per exact error count j
-    if (!besthits) schemes.push_back(makeScheme(gen.value, 0, k, len, !edit));
-    else
-        for (int j = 0; j <= k; ++j) schemes.push_back(makeScheme(gen.value, j, j, len, false));
-    for (auto& s : schemes) {
+    // --dynamic_generator: part sizes by weighted node count (search.cpp:192-195, 202-205)
+    auto build = [&](int minK, int maxK, bool hamming) {
+        if (!dyn.given) return makeScheme(gen.value, minK, maxK, len, hamming);
+        Scheme s;
+        const int n = sahara_scheme_dynamic(gen.value.c_str(), minK, maxK, len, 0, edit ? 1 : 0, (int)sigma,
+                                            (double)info.n, nullptr, 0, nullptr, nullptr, nullptr, 0);
+        if (n < 0) throw CliError("cannot expand search scheme " + gen.value);
+        std::vector<uint32_t> sizes(64);
+        s.n = (uint32_t)n;
+        s.pi.resize((size_t)n * len);
+        s.l.resize((size_t)n * len);
+        s.u.resize((size_t)n * len);
+        if (sahara_scheme_dynamic(gen.value.c_str(), minK, maxK, len, hamming ? 1 : 0, edit ? 1 : 0, (int)sigma,
+                                  (double)info.n, sizes.data(), 64, s.pi.data(), s.l.data(), s.u.data(), n) != n)
+            throw CliError("cannot expand search scheme " + gen.value + " to length " + std::to_string(len));
+        int P = 0;
+        sahara_scheme_parts(gen.value.c_str(), minK, maxK, &P, nullptr, nullptr, nullptr, 0);
+        std::string part = "[";
+        for (int t = 0; t < P; ++t) part += (t ? ", " : "") + std::to_string(sizes[t]);
+        std::printf("partition: %s]\n", part.c_str());
+        return s;
+    };
+    // each scheme's node counts right after it, as loadSearchScheme prints them (search.cpp:186-212)
+    auto add = [&](Scheme sch) {
         double nc = 0, wnc = 0;
-        sahara_scheme_counts(s.l.data(), s.u.data(), s.n, len, edit ? 1 : 0, (int)sigma, (double)info.n, &nc, &wnc);
+        sahara_scheme_counts(sch.l.data(), sch.u.data(), sch.n, len, edit ? 1 : 0, (int)sigma, (double)info.n, &nc,
+                             &wnc);
         std::printf("node count: %s\n", shortest(nc).c_str());
         std::printf("weighted node count: %s\n", shortest(wnc).c_str());
-    }
+        schemes.push_back(std::move(sch));
+    };
+    if (!besthits) add(build(0, k, !edit));
+    else
+        for (int j = 0; j <= k; ++j) add(build(j, j, false));
     timing.emplace_back("searchScheme", sw.reset());
 
     // search + locate (search.cpp:218-250), queries sharded over the devices

@@ -133,15 +133,18 @@ const char* kDescs[] = {"single part, errors anywhere",
                         "k+2 parts, greedy-box optimum-style scheme (default)",
                         "k+3 parts, greedy-box optimum-style scheme"};
 
-// expand(oss, len): parts of len/P (+1 for the first len%P parts); inside a
-// part the order follows the search direction; upper bounds hold for the
-// whole part, lower bounds apply at the part's last position.
-bool expand(const Part& s, unsigned len, std::vector<unsigned>& pi, std::vector<unsigned>& l,
-            std::vector<unsigned>& u) {
+// expand(oss, len) with explicit part sizes: inside a part the order follows
+// the search direction; upper bounds hold for the whole part, lower bounds
+// apply at the part's last position.
+bool expandSizes(const Part& s, const std::vector<unsigned>& sizes, std::vector<unsigned>& pi,
+                 std::vector<unsigned>& l, std::vector<unsigned>& u) {
     const unsigned P = (unsigned)s.pi.size();
-    if (len < P) return false;
+    if (sizes.size() != P) return false;
     std::vector<unsigned> first(P + 1, 0);
-    for (unsigned t = 0; t < P; ++t) first[t + 1] = first[t] + len / P + (t < len % P ? 1u : 0u);
+    for (unsigned t = 0; t < P; ++t) {
+        if (sizes[t] == 0) return false;
+        first[t + 1] = first[t] + sizes[t];
+    }
     pi.clear(); l.clear(); u.clear();
     for (unsigned i = 0; i < P; ++i) {
         const unsigned t = (unsigned)s.pi[i];
@@ -154,6 +157,20 @@ bool expand(const Part& s, unsigned len, std::vector<unsigned>& pi, std::vector<
         }
     }
     return true;
+}
+
+// uniform part sizes: len/P, +1 for the first len%P parts
+std::vector<unsigned> uniformSizes(unsigned P, unsigned len) {
+    std::vector<unsigned> z(P);
+    for (unsigned t = 0; t < P; ++t) z[t] = len / P + (t < len % P ? 1u : 0u);
+    return z;
+}
+
+bool expand(const Part& s, unsigned len, std::vector<unsigned>& pi, std::vector<unsigned>& l,
+            std::vector<unsigned>& u) {
+    const unsigned P = (unsigned)s.pi.size();
+    if (len < P) return false;
+    return expandSizes(s, uniformSizes(P, len), pi, l, u);
 }
 
 void toHamming(std::vector<unsigned>& l, std::vector<unsigned>& u) {
@@ -209,9 +226,76 @@ void counts(const std::vector<unsigned>& l, const std::vector<unsigned>& u, bool
     for (double c : cur) nodes += c;  // leaves
 }
 
+// --dynamic_generator (expandByWNCTopDown, search.cpp:192-195,202-205): part
+// sizes chosen to minimise the summed weighted node count of the scheme.
+// The upstream optimiser is not in the container; this one starts
+// from the uniform split and moves part boundaries (by 8, 4, 2, 1 positions)
+// while the weighted node count drops. Hits do not depend on the sizes.
+std::vector<unsigned> optimizeSizes(const std::vector<Part>& parts, unsigned len, bool edit, int sigma, double N) {
+    const unsigned P = (unsigned)parts[0].pi.size();
+    std::vector<unsigned> z = uniformSizes(P, len);
+    auto cost = [&](const std::vector<unsigned>& sz) {
+        double total = 0;
+        std::vector<unsigned> pi, l, u;
+        for (const Part& s : parts) {
+            if (!expandSizes(s, sz, pi, l, u)) return 1e300;
+            double a = 0, b = 0;
+            counts(l, u, edit, sigma, N, a, b);
+            total += b;
+        }
+        return total;
+    };
+    double best = cost(z);
+    for (unsigned step : {8u, 4u, 2u, 1u}) {
+        for (int iter = 0; iter < 4 * (int)len; ++iter) {
+            double bestMove = best;
+            std::vector<unsigned> bestZ;
+            for (unsigned b = 0; b + 1 < P; ++b)
+                for (int dir : {-1, 1}) {
+                    std::vector<unsigned> t = z;
+                    const unsigned from = dir > 0 ? b : b + 1, to = dir > 0 ? b + 1 : b;
+                    if (t[from] <= step) continue;
+                    t[from] -= step;
+                    t[to] += step;
+                    const double c = cost(t);
+                    if (c < bestMove * (1 - 1e-6)) { bestMove = c; bestZ = t; }  // real gains only
+                }
+            if (bestZ.empty()) break;
+            z = bestZ;
+            best = bestMove;
+        }
+    }
+    return z;
+}
+
 }  // namespace
 
 extern "C" {
+
+int sahara_scheme_dynamic(const char* generator, int min_k, int max_k, uint32_t len, int hamming, int edit,
+                          int sigma, double text_len, uint32_t* part_sizes, int max_parts, uint32_t* pi,
+                          uint32_t* l, uint32_t* u, int max_searches) {
+    std::vector<Part> parts;
+    if (!generator || !generate(generator, min_k, max_k, parts)) return -1;
+    const int P = (int)parts[0].pi.size();
+    if (!pi) return (int)parts.size();
+    if ((int)parts.size() > max_searches || P > max_parts) return -2;
+    if (len < (uint32_t)P) return -3;
+    const std::vector<unsigned> z = optimizeSizes(parts, len, edit != 0, sigma, text_len);
+    for (int t = 0; t < P; ++t) part_sizes[t] = z[t];
+    std::vector<unsigned> PI, L, U;
+    for (size_t s = 0; s < parts.size(); ++s) {
+        if (!expandSizes(parts[s], z, PI, L, U)) return -3;
+        if (hamming) toHamming(L, U);
+        for (uint32_t j = 0; j < len; ++j) {
+            pi[s * len + j] = PI[j];
+            l[s * len + j] = L[j];
+            u[s * len + j] = U[j];
+        }
+    }
+    return (int)parts.size();
+}
+
 
 int sahara_scheme_generators(const char** names, const char** descs, int cap) {
     const int n = (int)(sizeof(kNames) / sizeof(kNames[0]));

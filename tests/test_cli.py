@@ -271,3 +271,17 @@ def test_cli_simulated_reads_are_found(tmp_path, gpu_device):
         lead_i = len(trans) - len(trans.lstrip("I"))
         starts = {pos + k for k in range(0, lead_d + 1)} | {pos}
         assert any((2 * i, seqid, p) in found for p in starts) or lead_i > 0, (i, head)
+
+
+@pytest.mark.gpu
+def test_cli_dynamic_generator(tmp_path, gpu_device):
+    """--dynamic_generator prints the partition and finds the golden hit set."""
+    out = tmp_path / "h.txt"
+    rc, so, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                      "-e", 2, "--dynamic_generator", "--emit-errors", "-o", out)
+    assert rc == 0, err
+    assert "  dynamic expansion:   true" in so
+    part = [l for l in so.splitlines() if l.startswith("partition: [")]
+    assert len(part) == 1 and sum(map(int, part[0][12:-1].split(","))) == 40
+    from helpers import pset
+    assert pset(hits_as_rows(read_hits(out, 4))) == pset(expected("a_lev_k2"))

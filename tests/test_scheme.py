@@ -85,3 +85,26 @@ def test_counts_monotone_in_k():
         nc, wnc = sa.scheme_counts(sa.search_scheme("h2-k2", 0, k, 100), True, 6, 3e9)
         assert nc > prev and wnc > 0
         prev = nc
+
+
+@pytest.mark.parametrize("gen,k,m,n", [("h2-k2", 2, 40, 5e3), ("h2-k1", 1, 30, 2e3), ("pigeon", 2, 36, 1e4),
+                                       ("h2-k3", 3, 48, 3e3), ("h2-k2", 2, 100, 3e9)])
+def test_dynamic_partition(gen, k, m, n):
+    """--dynamic_generator: sizes sum to m, no empty part, WNC never above the uniform split,
+    and the hit set equals brute force (the sizes only move the search effort)."""
+    import numpy as np
+    import oracle
+    import sahara_amd as sa
+    from helpers import mutate_reads, pset, random_records
+    (pi, l, u), sizes = sa.search_scheme_dynamic(gen, 0, k, m, text_len=n)
+    assert sizes.sum() == m and sizes.min() >= 1
+    wd = sa.scheme_counts((pi, l, u), True, 6, n)[1]
+    wu = sa.scheme_counts(sa.search_scheme(gen, 0, k, m), True, 6, n)[1]
+    assert wd <= wu * (1 + 1e-9)
+    if n < 1e6:
+        rng = np.random.default_rng(m)
+        recs = random_records(rng, [int(n) // 2, int(n) // 2], 6, repeats=True)
+        pats = mutate_reads(rng, recs, 40, m, k)
+        I = oracle.Index.build(recs, 6)
+        h, _ = I.search(pats, (pi, l, u), edit=True)
+        assert pset(h) == pset(oracle.bruteforce(recs, pats, k, edit=True))
