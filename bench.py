@@ -124,7 +124,10 @@ def main():
     log(f"rank {rank}: GPU index built in {build_s:.1f}s, {info['device_bytes']/1e9:.2f} GB resident")
 
     t = time.time()
-    reads = sa.synth_reads(flat, lens, nreads, rlen, k, sigma=sigma, seed=7 + 1000003 * rank)
+    # exactly k errors per read, of uniform type S/I/D for edit
+    # distance and substitutions for Hamming (C2)
+    reads = sa.synth_reads(flat, lens, nreads, rlen, k if edit else 0, sigma=sigma, seed=7 + 1000003 * rank,
+                           substitutions=0 if edit else k)
     pats = sa.interleave_rc(reads, sigma)
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
     idx.stage(pats, scheme, edit=edit)

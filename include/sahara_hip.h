@@ -196,6 +196,12 @@ int  sahara_synth_reference(uint64_t seed, uint32_t sigma, const uint64_t* rec_l
 int  sahara_synth_reads(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
                         uint64_t n_reads, uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out,
                         uint64_t* origin);
+/* The same with the error types given as in `sahara read_simulator`
+ * (--substitution_errors, --insertion_errors, --deletion_errors, -e):
+ * fixed counts of S, I, D plus `errors` of uniformly chosen type. */
+int  sahara_synth_reads_typed(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
+                              uint64_t n_reads, uint32_t len, uint32_t substitutions, uint32_t insertions,
+                              uint32_t deletions, uint32_t errors, uint64_t seed, uint8_t* out, uint64_t* origin);
 /* Reverse complement interleave of search.cpp:121-123: out[2i] = read i,
  * out[2i+1] = its reverse complement (A<->T, C<->G, N->N). */
 int  sahara_interleave_rc(const uint8_t* reads, uint64_t n_reads, uint32_t len, uint32_t sigma, uint8_t* out);

@@ -106,6 +106,8 @@ EXPORTED = {
     "sahara_synth_reference": (C.c_int, [C.c_uint64, C.c_uint32, u64p, C.c_uint64, u8p]),
     "sahara_synth_reads": (C.c_int, [u8p, u64p, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
                                      C.c_uint32, C.c_uint64, u8p, u64p]),
+    "sahara_synth_reads_typed": (C.c_int, [u8p, u64p, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
+                                           C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, u8p, u64p]),
     "sahara_interleave_rc": (C.c_int, [u8p, C.c_uint64, C.c_uint32, C.c_uint32, u8p]),
 }
 
@@ -398,13 +400,17 @@ def synth_reference(lengths, sigma=6, seed=42):
     return out, lens
 
 
-def synth_reads(flat, rec_lens, n_reads, length, errors, sigma=6, seed=7, with_origin=False):
+def synth_reads(flat, rec_lens, n_reads, length, errors, sigma=6, seed=7, with_origin=False, substitutions=0,
+                insertions=0, deletions=0):
+    """Reads with `errors` transcript errors of uniform type S/I/D, plus fixed numbers of each type
+    (read_simulator.cpp semantics)."""
     flat = np.ascontiguousarray(flat, dtype=np.uint8)
     lens = np.ascontiguousarray(rec_lens, dtype=np.uint64)
     out = np.zeros((n_reads, length), np.uint8)
     origin = np.zeros((n_reads, 2), np.uint64) if with_origin else None
-    _check(lib().sahara_synth_reads(_p(flat, u8p), _p(lens, u64p), len(lens), sigma, n_reads, length,
-                                    errors, seed, _p(out, u8p), _p(origin, u64p)))
+    _check(lib().sahara_synth_reads_typed(_p(flat, u8p), _p(lens, u64p), len(lens), sigma, n_reads, length,
+                                          substitutions, insertions, deletions, errors, seed, _p(out, u8p),
+                                          _p(origin, u64p)))
     return (out, origin) if with_origin else out
 
 

@@ -850,7 +850,16 @@ int sahara_synth_reference(uint64_t seed, uint32_t sigma, const uint64_t* rec_le
 int sahara_synth_reads(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
                        uint64_t n_reads, uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out,
                        uint64_t* origin) {
-    return guarded([&] { synthReads(ranks, rec_lens, n_records, sigma, n_reads, len, errors, seed, out, origin); });
+    return guarded([&] { synthReads(ranks, rec_lens, n_records, sigma, n_reads, len, 0, 0, 0, errors, seed, out, origin); });
+}
+
+int sahara_synth_reads_typed(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
+                             uint64_t n_reads, uint32_t len, uint32_t substitutions, uint32_t insertions,
+                             uint32_t deletions, uint32_t errors, uint64_t seed, uint8_t* out, uint64_t* origin) {
+    return guarded([&] {
+        synthReads(ranks, rec_lens, n_records, sigma, n_reads, len, substitutions, insertions, deletions, errors, seed,
+                   out, origin);
+    });
 }
 
 int sahara_interleave_rc(const uint8_t* reads, uint64_t n_reads, uint32_t len, uint32_t sigma, uint8_t* out) {

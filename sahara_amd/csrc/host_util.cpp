@@ -129,7 +129,8 @@ struct Xoshiro {
 }  // namespace
 
 void synthReads(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma, uint64_t nreads,
-                uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out, uint64_t* origin) {
+                uint32_t len, uint32_t subs, uint32_t ins, uint32_t dels, uint32_t errors, uint64_t seed, uint8_t* out,
+                uint64_t* origin) {
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 or 6");
     if (len == 0) throw Error("read length must be > 0");
     const uint8_t code[4] = {1, 2, 3, (uint8_t)(sigma == 6 ? 5 : 4)};
@@ -146,7 +147,7 @@ void synthReads(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec, ui
             std::vector<char> tr;
             for (uint64_t i = nreads * t / nth; i < nreads * (t + 1) / nth; ++i) {
                 Xoshiro g(seed * 0x100000001b3ull + i);
-                uint32_t ns = 0, ni = 0, nd = 0;
+                uint32_t ns = subs, ni = ins, nd = dels;
                 for (uint32_t e = 0; e < errors; ++e) {
                     const uint64_t k = g.below(3);
                     ns += k == 0; ni += k == 1; nd += k == 2;

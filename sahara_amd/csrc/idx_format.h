@@ -42,6 +42,7 @@ void writeIdx(const std::string& path, const IdxParts& p);
 uint64_t readIdxSigma(const std::string& path);         // search.cpp:278-283
 
 void synthReads(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma, uint64_t nreads,
-                uint32_t len, uint32_t errors, uint64_t seed, uint8_t* out, uint64_t* origin);
+                uint32_t len, uint32_t subs, uint32_t ins, uint32_t dels, uint32_t errors, uint64_t seed, uint8_t* out,
+                uint64_t* origin);
 
 }  // namespace sahara

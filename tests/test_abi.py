@@ -66,6 +66,17 @@ def test_synth_reads_follow_transcript_semantics():
         assert best <= 2
 
 
+def test_synth_reads_substitutions_only():
+    # Hamming workloads (C2): exactly k substitutions, no indels
+    flat, lens = sa.synth_reference([3000, 2000], sigma=6, seed=42)
+    reads, origin = sa.synth_reads(flat, lens, 300, 40, 0, sigma=6, seed=9, with_origin=True, substitutions=2)
+    starts = [0] + np.cumsum(lens.astype(np.int64))[:-1].tolist()
+    for i in range(300):
+        rec, pos = int(origin[i, 0]), int(origin[i, 1])
+        ref = flat[starts[rec] + pos: starts[rec] + pos + 40]
+        assert int(np.count_nonzero(ref != reads[i])) == 2
+
+
 def test_interleave_rc():
     r = np.array([[1, 2, 3, 5, 4], [5, 5, 1, 2, 2]], np.uint8)
     out = sa.interleave_rc(r, sigma=6)
