@@ -89,8 +89,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_c3.json"),
-                    help="measured HBM bytes per launch per kernel (tools/profile.sh + tools/pmc_summary.py)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="measured HBM bytes per launch per kernel (tools/traffic.sh + tools/traffic_summary.py); "
+                         "default profiles/traffic_<config>.json when it exists")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,12 +200,13 @@ def main():
         roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": round(kern[dom]["bytes"] / per_launch)}
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            tr = json.load(open(args.traffic_json)).get(dom)
+        tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        if os.path.exists(tj):
+            tr = json.load(open(tj)).get(dom)
             if tr:  # HBM bytes per launch from the committed PMC pass (FETCH_SIZE, calibrated)
                 roofline["traffic"] = tr["bytes_per_launch"]
                 roofline["traffic_GBs"] = tr["traffic_GBs"]
-                roofline["traffic_source"] = os.path.relpath(args.traffic_json, ROOT)
+                roofline["traffic_source"] = os.path.relpath(tj, ROOT)
         extra = {"bytes_per_read": round((search_bytes + text_bytes + locate_bytes) / nreads, 1),
                  "kernels": {n: {"ms": v["ms"], "algorithmic_GBs": v["GBs"],
                                  "bytes_per_read": round(v["bytes"] / nreads, 1)} for n, v in kern.items()},

@@ -50,17 +50,18 @@ struct Ctx {
     uint32_t textSteps = 4;               // text-phase micro-steps per lane per wave iteration
     uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
 
-    // work buffers. Batches alternate between two slots so that the FM phase
-    // of batch i+1 (stream `st`) runs while batch i finishes its text phase,
-    // locate and sort (stream `stB`).
+    // work buffers. Batches rotate over three slots so that the FM phase runs
+    // up to two batches ahead (stream `st`) of the text phase (stream `stB`),
+    // while batch i-1 runs its locate and sort (stream `stC`).
+    static constexpr int kSlots = 3;
     struct Slot {
         DevBuf<uint4> hits, tasks;
         DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, -, seedCount
         DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512)
         hipEvent_t fmStart = nullptr, seedDone = nullptr, fmDone = nullptr, textStart = nullptr, textDone = nullptr,
                    free = nullptr;
-    } slot[2];
-    hipStream_t stB = nullptr;
+    } slot[kSlots];
+    hipStream_t stB = nullptr, stC = nullptr;
     uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
     size_t pinnedCap = 0;
     bool pipeline = true;
@@ -68,7 +69,9 @@ struct Ctx {
     DevBuf<uint32_t> seedItem, dbg;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
-    DevBuf<uint64_t> rowOff, k0, k1;
+    DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
+    DevBuf<uint64_t> partial;             // tile sums of the segment scan
+    DevBuf<uint32_t> qcnt, big;           // per-query row counts (zero between batches); long segments
     DevBuf<char> tmp;
     DevBuf<sahara_hit> out;
     uint64_t nout = 0;
@@ -84,6 +87,7 @@ struct Ctx {
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
         if (stB) (void)hipStreamDestroy(stB);
+        if (stC) (void)hipStreamDestroy(stC);
         if (st) (void)hipStreamDestroy(st);
     }
 };
@@ -155,6 +159,7 @@ Ctx* newCtx(int device) {
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
@@ -283,10 +288,14 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
 
 
 // One pass over the staged patterns in batches of <= 4M. Per batch:
-//   stream st : kSearchFM                              -> hits, tasks of its slot
-//   stream stB: kResolveTasks, kSearchText, locate, sort, decode
-// Two slots alternate, so the FM phase of batch i+1 (memory-latency bound)
-// overlaps the text phase of batch i (ALU bound). Buffer overflow is detected
+//   stream st : kSeedItems, kSearchFM        -> hits, tasks of its slot
+//   stream stB: kResolveTasks, kSearchText   -> hits of its slot
+//   stream stC: row offsets, locate, sort, decode
+// Three slots rotate, so the FM phase of batches i+1, i+2 (memory-latency
+// bound) overlaps the text phase of batch i (ALU bound), and both phases run
+// back to back while locate and sort of batch i-1 fill the gaps on stream
+// stC. Host order: finish(i-3), FM(i), text(i) — FM(i) reuses the slot that
+// locate(i-3) frees. Buffer overflow is detected
 // after the fact from each batch's flags; the whole pass is then redone on one
 // stream with grown buffers (`serial`), re-running a batch until it fits.
 void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
@@ -317,16 +326,22 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     S.patterns = c->npat;
     const uint32_t sigma = c->I.sigma;
     const size_t lds = (size_t)c->nsearch * c->m * 4;
-    int bpc = searchBlocksPerCU(sigma, c->edit, lds);
+    const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
+    int bpc = fullBpc;
     // Overlapped with the text phase of the previous batch, the FM phase
     // (memory-latency bound) runs with one workgroup per CU and leaves the
     // CUs' issue slots to the text phase (ALU bound); alone it takes them all.
-    const uint64_t batchesHere = (c->npat + std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch) - 1) /
-                                 std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
+    // patterns per batch: 4M, fewer for schemes with many searches (work
+    // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
+    uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
+    if (const char* e = std::getenv("SAHARA_BATCH")) maxBatch = std::max<uint64_t>(1, std::min<uint64_t>(maxBatch, std::atoll(e)));
+    const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
     if (!serial && batchesHere > 1 && c->verify) bpc = 1;
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
-    const uint64_t T = (uint64_t)blocks * 256;
+    // the first batch's FM phase has nothing to overlap with: full occupancy
+    const uint32_t firstBlocks = std::getenv("SAHARA_FM_BPC") ? blocks : (uint32_t)(c->numCU * fullBpc);
+    const uint64_t T = (uint64_t)std::max(blocks, firstBlocks) * 256;
     const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
     c->stack.reserve((size_t)std::max<uint32_t>(stackCap, 5) * T);  // levels beyond the LDS part
     S.search_grid = blocks;
@@ -349,7 +364,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
 
-    const uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (c->hitCap == 0) {
         c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (const char* e = std::getenv("SAHARA_HITCAP")) c->hitCap = (uint32_t)std::max(1L, std::atol(e));
@@ -358,28 +372,63 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
     }
-    const uint64_t nbatch = (c->npat + maxBatch - 1) / maxBatch;
+    // batch boundaries. SAHARA_RAMP (pipelined only): 1 makes the first two
+    // batches smaller (1/4, 1/2 of the others) so that the FM phase of the
+    // first, which overlaps nothing, is short; 2 also the last two
+    std::vector<uint64_t> bstart{0};
+    {
+        const int rampMode = std::getenv("SAHARA_RAMP") ? std::atoi(std::getenv("SAHARA_RAMP")) : 0;
+        const bool up = !serial && rampMode >= 1 && c->npat > 3 * maxBatch;
+        const bool down = up && rampMode >= 2;
+        const uint64_t edge[2] = {std::max<uint64_t>(maxBatch / 4, 1), std::max<uint64_t>(maxBatch / 2, 1)};
+        const uint64_t mid = c->npat - (up ? edge[0] + edge[1] : 0) - (down ? edge[0] + edge[1] : 0);
+        if (up) {
+            bstart.push_back(edge[0]);
+            bstart.push_back(edge[0] + edge[1]);
+        }
+        const uint64_t nmid = (mid + maxBatch - 1) / maxBatch, q0 = bstart.back();
+        for (uint64_t i = 1; i <= nmid; ++i) bstart.push_back(q0 + mid * i / nmid);
+        if (down) {
+            bstart.push_back(bstart.back() + edge[1]);
+            bstart.push_back(bstart.back() + edge[0]);
+        }
+    }
+    const uint64_t nbatch = bstart.size() - 1;
     if (c->pinnedCap < nbatch * 8) {
         if (c->pinned) SH_HIP(hipHostFree(c->pinned));
         c->pinned = nullptr;
         SH_HIP(hipHostMalloc(&c->pinned, nbatch * 8 * sizeof(uint32_t)));
         c->pinnedCap = nbatch * 8;
     }
-    hipStream_t sA = c->st, sB = serial ? c->st : c->stB;
+    if (c->qcnt.cap < maxBatch + 1) {
+        c->qcnt.reserve(maxBatch + 1);
+        c->qoff.reserve(maxBatch + 1);
+        c->big.reserve(maxBatch);
+    }
+    SH_HIP(hipMemsetAsync(c->qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
+    hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC;
     SH_HIP(hipStreamSynchronize(c->st));
     SH_HIP(hipStreamSynchronize(c->stB));
+    SH_HIP(hipStreamSynchronize(c->stC));
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
-    for (auto& sl : c->slot) SH_HIP(hipEventRecord(sl.free, sA));
+    c->dbg.reserve(16);
+    SH_HIP(hipMemsetAsync(c->dbg.ptr, 0, 16 * sizeof(uint32_t), sA));
+    // a slot's counters and queues are zero when its `free` event fires:
+    // here for the first use, after its locate (finish) for the next
+    auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
+        SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), s));
+        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 512 * sizeof(uint32_t), s));
+        SH_HIP(hipEventRecord(sl.free, s));
+    };
+    for (auto& sl : c->slot) resetSlot(sl, sA);
 
     auto issueFM = [&](uint64_t b) {
-        Ctx::Slot& sl = c->slot[b & 1];
-        const uint64_t q0 = b * maxBatch, nb = std::min<uint64_t>(maxBatch, c->npat - q0);
+        Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
+        const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
         sl.hits.reserve((size_t)c->hitCap + 1);
         sl.tasks.reserve((size_t)c->taskCap);
         SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
-        SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), sA));
-        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 512 * sizeof(uint32_t), sA));
         SearchArgs a{};
         a.occF = c->I.occF.ptr;
         a.occR = c->I.occR.ptr;
@@ -426,13 +475,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(sl.fmStart, sA));
         launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sA);
         SH_HIP(hipEventRecord(sl.seedDone, sA));
-        launchSearch(a, sigma, c->edit, count, blocks, lds, sA);
+        launchSearch(a, sigma, c->edit, count, b == 0 ? firstBlocks : blocks, lds, sA);
         SH_HIP(hipEventRecord(sl.fmDone, sA));
         ++S.search_launches;
     };
     auto issueText = [&](uint64_t b) {
-        Ctx::Slot& sl = c->slot[b & 1];
-        const uint64_t q0 = b * maxBatch;
+        Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
+        const uint64_t q0 = bstart[b];
         SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
         SH_HIP(hipEventRecord(sl.textStart, sB));
         if (split) {
@@ -458,21 +507,25 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.stackCap = textStack;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
-            c->dbg.reserve(16);
             t.dbg = c->dbg.ptr;
-            SH_HIP(hipMemsetAsync(c->dbg.ptr, 0, 16 * sizeof(uint32_t), sB));
             launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));
-        SH_HIP(hipMemcpyAsync(c->pinned + b * 8, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sB));
     };
     // locate: row offsets (exclusive scan of len), SA / LF locate, canonical
-    // sort, decode into the device-resident output. Needs the batch's counts.
+    // sort, decode into the device-resident output, on stream sC. Needs the
+    // batch's counts (host waits for its text phase). Returns false on
+    // overflow; `finishCheck` then reads the locate flags and timings.
     auto finish = [&](uint64_t b) {
-        Ctx::Slot& sl = c->slot[b & 1];
-        const uint64_t q0 = b * maxBatch, nb = std::min<uint64_t>(maxBatch, c->npat - q0);
-        SH_HIP(hipStreamSynchronize(sB));
+        Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
+        const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
+        // the batch's counters, copied on sC (a copy on sB would wait for CU
+        // slots between two text phases)
+        SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 8, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipEventRecord(c->ev[6], sC));
+        SH_HIP(hipEventSynchronize(c->ev[6]));
         const uint32_t* hs = c->pinned + b * 8;
         float ms = 0;
         SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
@@ -494,28 +547,31 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             if (hs[2] & 8u) growCap(c->taskCap, hs[4]);
             if (hs[2] & 2u) growCap(c->hitCap, hs[1]);
             overflow = true;
-            SH_HIP(hipEventRecord(sl.free, sB));
+            resetSlot(sl, sC);
             return false;
         }
         // reserved slots incl. len-0 holes; a wave's last range may reach past
         // the capacity without having written there (no overflow flag)
         const uint64_t nh = std::min<uint64_t>(hs[1], c->hitCap);
         S.cursors += hs[3];
-        SH_HIP(hipEventRecord(c->ev[2], sB));
-        SH_HIP(hipMemsetAsync(sl.hits.ptr + nh, 0, sizeof(uint4), sB));
-        c->rowOff.reserve(nh + 1);
-        const size_t scanBytes = rowOffsetsTempBytes(nh);
-        c->tmp.reserve(scanBytes + 256);
-        rowOffsets(sl.hits.ptr, nh, c->rowOff.ptr, c->tmp.ptr, c->tmp.cap, sB);
+        SH_HIP(hipEventRecord(c->ev[2], sC));
+        SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
+        c->partial.reserve(scanTiles((uint32_t)nb));
+        querySegments(sl.hits.ptr, nh, c->qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr,
+                      c->small.ptr + 4, sC);
         uint64_t rows = 0;
-        SH_HIP(hipMemcpyAsync(&rows, c->rowOff.ptr + nh, 8, hipMemcpyDeviceToHost, sB));
-        SH_HIP(hipStreamSynchronize(sB));
+        uint32_t nbig = 0;
+        SH_HIP(hipMemcpyAsync(&rows, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipMemcpyAsync(&nbig, c->small.ptr + 4, 4, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipStreamSynchronize(sC));
+        if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
         c->k0.reserve(std::max<uint64_t>(rows, 1));
-        c->k1.reserve(std::max<uint64_t>(rows, 1));
+        if (nbig) c->k1.reserve(std::max<uint64_t>(rows, 1));
         LocateArgs la{};
         la.hits = sl.hits.ptr;
         la.nhits = nh;
-        la.rowOff = c->rowOff.ptr;
+        la.qoff = c->qoff.ptr;
+        la.qcnt = c->qcnt.ptr;
         la.occF = c->I.occF.ptr;
         for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
         la.samples = c->I.samples.ptr;
@@ -525,49 +581,61 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         la.counters = c->counters.ptr + 3;
         la.sa = c->I.saFull.ptr;
         la.useSA = c->locateSA ? 1u : 0u;
-        SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sB));
-        launchLocate(la, count, sB);
-        SH_HIP(hipEventRecord(sl.free, sB));  // the slot's hits are consumed
-        SH_HIP(hipEventRecord(c->ev[3], sB));
-        unsigned endBit = 36;
-        while ((1ull << (endBit - 36)) < nb) ++endBit;
-        const size_t sbytes = sortTempBytes(rows);
-        c->tmp.reserve(sbytes + 256);
-        uint64_t* sorted = sortKeys(c->k0.ptr, c->k1.ptr, rows, std::min(endBit, 64u), c->tmp.ptr, c->tmp.cap, sB);
+        launchLocate(la, count, sC);
+        SH_HIP(hipEventRecord(c->ev[3], sC));
+        resetSlot(sl, sC);  // the slot's hits are consumed
+        if (nbig) c->tmp.reserve(bigSortTempBytes(rows, nbig) + 256);
         if (c->nout + rows > c->out.cap) {  // grow the device-resident output
             const size_t want = std::max<size_t>((c->nout + rows) + (c->nout + rows) / 2, 1024);
             sahara_hit* np = nullptr;
             SH_HIP(hipMalloc(&np, want * sizeof(sahara_hit)));
-            if (c->nout) SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, sB));
-            SH_HIP(hipStreamSynchronize(sB));
+            if (c->nout) SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, sC));
+            SH_HIP(hipStreamSynchronize(sC));
             c->out.release();
             c->out.ptr = np;
             c->out.cap = want;
         }
-        launchDecode(sorted, rows, q0, c->I.dRecStarts.ptr, (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, sB);
-        SH_HIP(hipEventRecord(c->ev[4], sB));
-        uint32_t lflags = 0;
-        SH_HIP(hipMemcpyAsync(&lflags, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sB));
-        SH_HIP(hipStreamSynchronize(sB));
-        if (lflags & 4u) throw Error("locate walked off the SA samples (corrupt index)");
-        SH_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-        S.locate_ms += ms;
-        SH_HIP(hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
-        S.sort_ms += ms;
+        sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, q0, c->I.dRecStarts.ptr,
+                   (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, c->tmp.ptr, c->tmp.cap, sC);
+        SH_HIP(hipEventRecord(c->ev[4], sC));
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 8 + 7, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipEventRecord(c->ev[5], sC));
         c->nout += rows;
         S.hits += rows;
         return true;
     };
+    auto finishCheck = [&](uint64_t b) {
+        SH_HIP(hipEventSynchronize(c->ev[5]));
+        if (c->pinned[b * 8 + 7] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
+        float ms = 0;
+        SH_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        S.locate_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
+        S.sort_ms += ms;
+    };
 
     if (!serial) {
-        issueFM(0);
+        // FM(b) and text(b) are enqueued as soon as the slot of batch b-3 is
+        // released by its locate, so both streams always have work queued
+        // while the host waits for a text phase to finish.
+        bool pending = false;  // finishCheck owed for batch `owed`
+        uint64_t owed = 0;
+        auto drain = [&](uint64_t f) {
+            if (pending) finishCheck(owed);
+            pending = finish(f);
+            owed = f;
+        };
         for (uint64_t b = 0; b < nbatch; ++b) {
-            if (b + 1 < nbatch) issueFM(b + 1);
+            if (b >= (uint64_t)Ctx::kSlots) drain(b - Ctx::kSlots);
+            issueFM(b);
             issueText(b);
             ++S.batches;
-            finish(b);
         }
+        for (uint64_t f = nbatch > (uint64_t)Ctx::kSlots ? nbatch - Ctx::kSlots : 0; f < nbatch; ++f) drain(f);
+        if (pending) finishCheck(owed);
         SH_HIP(hipStreamSynchronize(sA));
+        SH_HIP(hipStreamSynchronize(sB));
+        SH_HIP(hipStreamSynchronize(sC));
         if (overflow) return;  // the caller redoes the pass serially with the grown buffers
     } else {
         for (uint64_t b = 0; b < nbatch; ++b) {
@@ -576,15 +644,18 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                 overflow = false;
                 issueFM(b);
                 issueText(b);
-                if (finish(b)) break;
+                if (finish(b)) {
+                    finishCheck(b);
+                    break;
+                }
             }
         }
         overflow = false;
     }
     if (count) {
         unsigned long long h[16];
-        SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, sB));
-        SH_HIP(hipStreamSynchronize(sB));
+        SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipStreamSynchronize(sC));
         S.nodes = h[0];
         S.rank_nodes = h[1];
         S.ext_lines = h[2];

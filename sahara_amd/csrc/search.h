@@ -80,7 +80,8 @@ struct TextArgs {
 struct LocateArgs {
     const uint4* hits;
     uint64_t nhits;
-    const uint64_t* rowOff;
+    const uint64_t* qoff;          // per-query row segments (querySegments)
+    uint32_t* qcnt;                // per-query row counts, counted back to 0
     const OccLine* occF;
     uint32_t C[8];
     const uint32_t* samples;
@@ -103,14 +104,18 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
                         hipStream_t st);
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                   hipStream_t st);
-size_t rowOffsetsTempBytes(uint64_t nhits);
-void rowOffsets(const uint4* hits, uint64_t nhits, uint64_t* off, void* tmp, size_t tmpBytes, hipStream_t st);
+// locate + canonical order, per batch: querySegments (rows per query ->
+// segments; long segments listed in big, their count in *nbig, read back by
+// the host), launchLocate (keys into the segments), sortDecode (short
+// segments in registers, medium across a wave, long by segmented radix sort).
+uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
+void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
+                   uint32_t* big, uint32_t* nbig, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
-size_t sortTempBytes(uint64_t n);
-uint64_t* sortKeys(uint64_t* k0, uint64_t* k1, uint64_t n, unsigned endBit, void* tmp, size_t tmpBytes,
-                   hipStream_t st);
-void launchDecode(const uint64_t* keys, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint32_t nrec,
-                  sahara_hit* out, hipStream_t st);
+size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
+void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff, uint32_t nq, const uint32_t* big,
+                uint32_t nbig, uint64_t qidBase, const uint64_t* starts, uint32_t nrec, sahara_hit* out, void* tmp,
+                size_t tmpBytes, hipStream_t st);
 void launchDigest(const sahara_hit* h, uint64_t n, unsigned long long* out, hipStream_t st);
 
 }  // namespace sahara

@@ -39,9 +39,11 @@
 // any buffer is flagged; the host re-runs the batch with a larger buffer.
 //
 // Locate: FM leaves resolve rows through the resident full SA (one read per
-// row) or, in the reference mode, by LF walks to the SA samples. Records are
-// packed into u64 keys (qid, text position, e) and radix-sorted for the
-// canonical (qid, seq_id, pos, e) order.
+// row) or, in the reference mode, by LF walks to the SA samples, straight
+// into per-query segments (counting sort by qid: row counts, exclusive scan).
+// Keys text position << 4 | e are then sorted within each segment — in
+// registers for the usual <= 8 rows, by a segmented radix sort for longer
+// segments — for the canonical (qid, seq_id, pos, e) order.
 
 #include <hip/hip_runtime.h>
 
@@ -919,22 +921,128 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
 
 // ================================================================ locate ====
 
-// One lane per reported cursor: locate every row of [lb, lb+len).
+// Rows per query: qcnt[qid] += len for every reported cursor. qcnt is all
+// zero between batches (kLocate counts it back down).
+__global__ void kCountRows(const uint4* __restrict__ hits, uint64_t nhits, uint32_t* __restrict__ qcnt) {
+    for (uint64_t h = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; h < nhits;
+         h += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 hit = hits[h];
+        if (hit.z) atomicAdd(qcnt + hit.x, hit.z);
+    }
+}
+
+// Segment tiers: <= kSmallSeg rows sorted in a lane's registers,
+// <= kMediumSeg by a wave (one key per lane, bitonic over shuffles), longer
+// ones by the segmented radix sort.
+constexpr uint32_t kSmallSeg = 8;
+constexpr uint32_t kMediumSeg = 64;
+
+// Exclusive scan of the per-query row counts (n = queries + 1 entries, the
+// last one 0) into u64 segment offsets, reduce-then-scan over tiles of
+// kScanTile: no inter-block waiting, so it keeps its pace next to the
+// persistent search kernels. The tile pass also lists the long segments
+// (> kMediumSeg rows; one global atomic per tile).
+constexpr uint32_t kScanTile = 4096;
+
+// exclusive scan of one value per thread over a 256-thread block
+__device__ __forceinline__ uint64_t blockExclusiveScan(uint64_t v, uint64_t& total, uint64_t* wsum) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint64_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint64_t pre = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint64_t t = wsum[i];
+        pre += i < w ? t : 0;
+        total += t;
+    }
+    __syncthreads();
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(256) void kTileSums(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                uint64_t* __restrict__ partial) {
+    __shared__ uint64_t wsum[4];
+    const uint32_t base = blockIdx.x * kScanTile;
+    uint64_t acc = 0;
+    for (uint32_t i = threadIdx.x; i < kScanTile && base + i < n; i += 256) acc += cnt[base + i];
+    for (uint32_t off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+    if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(256) void kScanPartials(uint64_t* __restrict__ partial, uint32_t ntiles) {
+    __shared__ uint64_t wsum[4];
+    uint64_t carry = 0;
+    for (uint32_t b = 0; b < ntiles; b += 256) {
+        const uint32_t i = b + threadIdx.x;
+        const uint64_t v = i < ntiles ? partial[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = blockExclusiveScan(v, tot, wsum);
+        if (i < ntiles) partial[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void kScanTiles(const uint32_t* __restrict__ cnt, uint32_t n,
+                                                 const uint64_t* __restrict__ partial, uint64_t* __restrict__ off,
+                                                 uint32_t* __restrict__ list, uint32_t* __restrict__ nlist) {
+    __shared__ uint64_t wsum[4];
+    __shared__ uint32_t llist[kScanTile];
+    __shared__ uint32_t lcnt, lbase;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (threadIdx.x == 0) lcnt = 0;
+    const uint32_t base = blockIdx.x * kScanTile;
+    uint64_t carry = partial[blockIdx.x];
+    for (uint32_t c = 0; c < kScanTile; c += 256) {  // uniform trip count: block scans inside
+        const uint32_t i = base + c + threadIdx.x;
+        const uint32_t v = i < n ? cnt[i] : 0u;
+        uint64_t tot;
+        const uint64_t ex = blockExclusiveScan(v, tot, wsum);
+        if (i < n) off[i] = carry + ex;
+        carry += tot;
+        const uint64_t m = __ballot(v > kMediumSeg);
+        if (m) {
+            uint32_t wb = 0;
+            const int leader = __ffsll((long long)m) - 1;
+            if ((int)lane == leader) wb = atomicAdd(&lcnt, (uint32_t)__popcll(m));
+            wb = __shfl(wb, leader);
+            if (v > kMediumSeg) llist[wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) lbase = lcnt ? atomicAdd(nlist, lcnt) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < lcnt; i += 256) list[lbase + i] = llist[i];
+}
+
+// One lane per reported cursor: locate every row of [lb, lb+len) into the
+// query's segment [qoff[qid], qoff[qid+1]) of the key array (key = text
+// position << 4 | e); the slot within the segment comes from counting
+// qcnt[qid] back down, which leaves qcnt zero for the next batch.
 template <bool COUNT>
 __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
     uint64_t steps = 0;
     for (uint64_t h = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; h < a.nhits;
          h += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 hit = a.hits[h];
-        const uint64_t out = a.rowOff[h];
+        if (hit.z == 0) continue;  // reserved hole
+        const uint64_t out = a.qoff[hit.x] + (atomicSub(a.qcnt + hit.x, hit.z) - hit.z);
         const uint64_t e = hit.w & 0xFu;
         if (hit.w & kPosKnown) {  // resolved by the text phase
-            a.keys[out] = ((uint64_t)hit.x << 36) | ((uint64_t)hit.y << 4) | e;
+            a.keys[out] = ((uint64_t)hit.y << 4) | e;
             continue;
         }
         if (a.useSA) {  // full SA resident: one read per row
-            for (uint32_t j = 0; j < hit.z; ++j)
-                a.keys[out + j] = ((uint64_t)hit.x << 36) | ((uint64_t)a.sa[hit.y + j] << 4) | e;
+            for (uint32_t j = 0; j < hit.z; ++j) a.keys[out + j] = ((uint64_t)a.sa[hit.y + j] << 4) | e;
             continue;
         }
         for (uint32_t j = 0; j < hit.z; ++j) {  // fmc::LocateLinear: LF walk to a sample
@@ -964,29 +1072,97 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
                 ++st;
             }
             if (COUNT) steps += st;
-            a.keys[out + j] = ((uint64_t)hit.x << 36) | (gpos << 4) | e;
+            a.keys[out + j] = (gpos << 4) | e;
         }
     }
     if (COUNT && steps) atomicAdd(a.counters, (unsigned long long)steps);
 }
 
-__global__ void kDecode(const uint64_t* __restrict__ keys, uint64_t n, uint64_t qidBase,
-                        const uint64_t* __restrict__ starts, uint32_t nrec, sahara_hit* __restrict__ out) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = keys[i];
-        const uint64_t gpos = (k >> 4) & 0xFFFFFFFFull;
-        uint32_t lo = 0, hi = nrec;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (starts[mid] <= gpos) lo = mid; else hi = mid;
+__device__ __forceinline__ sahara_hit decodeKey(uint64_t k, uint64_t qid, const uint64_t* __restrict__ starts,
+                                                uint32_t nrec) {
+    const uint64_t gpos = k >> 4;
+    uint32_t lo = 0, hi = nrec;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (starts[mid] <= gpos) lo = mid; else hi = mid;
+    }
+    sahara_hit h;
+    h.qid = qid;
+    h.seq_id = lo;
+    h.err = (uint32_t)(k & 15u);
+    h.pos = gpos - starts[lo];
+    return h;
+}
+
+__device__ __forceinline__ void cswap(uint64_t& a, uint64_t& b) {
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// Sort + decode of the short and medium segments, one lane per query: a
+// segment of <= kSmallSeg rows is sorted in the lane's registers
+// (odd-even transposition, padded with ~0); the wave then takes its medium
+// segments one by one, one key per lane, bitonic-sorted over shuffles.
+// Long segments are left to the segmented radix sort.
+__global__ __launch_bounds__(256) void kSortDecode(const uint64_t* __restrict__ keys,
+                                                  const uint64_t* __restrict__ qoff, uint32_t nq, uint64_t qidBase,
+                                                  const uint64_t* __restrict__ starts, uint32_t nrec,
+                                                  sahara_hit* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t q0 = blockIdx.x * blockDim.x; q0 < nq; q0 += gridDim.x * blockDim.x) {
+        const uint32_t q = q0 + threadIdx.x;
+        uint64_t b = 0;
+        uint32_t n = 0;
+        if (q < nq) {
+            b = qoff[q];
+            n = (uint32_t)(qoff[q + 1] - b);
         }
-        sahara_hit h;
-        h.qid = qidBase + (k >> 36);
-        h.seq_id = lo;
-        h.err = (uint32_t)(k & 15u);
-        h.pos = gpos - starts[lo];
-        out[i] = h;
+        if (n && n <= kSmallSeg) {
+            uint64_t v[kSmallSeg];
+#pragma unroll
+            for (uint32_t i = 0; i < kSmallSeg; ++i) v[i] = i < n ? keys[b + i] : ~0ull;
+            // n rounds sort the n keys (the ~0 padding never moves)
+#pragma unroll
+            for (uint32_t r = 0; r < kSmallSeg; ++r) {
+                if (r >= n) break;
+#pragma unroll
+                for (uint32_t i = r & 1u; i + 1 < kSmallSeg; i += 2) cswap(v[i], v[i + 1]);
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kSmallSeg; ++i)
+                if (i < n) out[b + i] = decodeKey(v[i], qidBase + q, starts, nrec);
+        }
+        uint64_t med = __ballot(n > kSmallSeg && n <= kMediumSeg);
+        while (med) {
+            const int src = __ffsll((long long)med) - 1;
+            med &= med - 1;
+            const uint32_t sq = (uint32_t)__shfl((int)q, src), sn = (uint32_t)__shfl((int)n, src);
+            const uint64_t sb = __shfl(b, src);
+            uint64_t v = lane < sn ? keys[sb + lane] : ~0ull;
+#pragma unroll
+            for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    const uint64_t o = __shfl_xor(v, j);
+                    const bool keepMin = ((lane & j) == 0) == ((lane & k) == 0);
+                    v = keepMin ? (v < o ? v : o) : (v < o ? o : v);
+                }
+            }
+            if (lane < sn) out[sb + lane] = decodeKey(v, qidBase + sq, starts, nrec);
+        }
+    }
+}
+
+// One workgroup per long segment (already sorted): decode.
+__global__ __launch_bounds__(256) void kDecodeBig(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ qoff,
+                                                 const uint32_t* __restrict__ big, uint32_t nbig, uint64_t qidBase,
+                                                 const uint64_t* __restrict__ starts, uint32_t nrec,
+                                                 sahara_hit* __restrict__ out) {
+    for (uint32_t s = blockIdx.x; s < nbig; s += gridDim.x) {
+        const uint32_t q = big[s];
+        const uint64_t b = qoff[q], e = qoff[q + 1];
+        for (uint64_t i = b + threadIdx.x; i < e; i += blockDim.x) out[i] = decodeKey(keys[i], qidBase + q, starts, nrec);
     }
 }
 
@@ -1023,8 +1199,10 @@ __global__ void kPackPatterns(const uint8_t* __restrict__ src, uint64_t npat, ui
     }
 }
 
-struct HitLen {
-    __host__ __device__ uint64_t operator()(const uint4& h) const { return (uint64_t)h.z; }
+struct SegOff {  // begin (d = 0) / end (d = 1) of a listed query's segment
+    const uint64_t* qoff;
+    uint32_t d;
+    __host__ __device__ uint32_t operator()(const uint32_t& q) const { return (uint32_t)qoff[q + d]; }
 };
 
 template <int SIGMA>
@@ -1103,21 +1281,22 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
     SH_HIP(hipGetLastError());
 }
 
-size_t rowOffsetsTempBytes(uint64_t nhits) {
-    size_t tb = 0;
-    rocprim::transform_iterator<const uint4*, HitLen, uint64_t> it(nullptr, HitLen());
-    SH_HIP(rocprim::exclusive_scan(nullptr, tb, it, (uint64_t*)nullptr, (uint64_t)0, (size_t)nhits + 1,
-                                   rocprim::plus<uint64_t>(), (hipStream_t)0));
-    return tb;
+void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
+                   uint32_t* big, uint32_t* nbig, hipStream_t st) {
+    // qcnt[nq] stays 0, so qoff[nq] = total rows
+    if (nhits) {
+        const uint64_t blocks = std::min<uint64_t>((nhits + 255) / 256, 65536);
+        hipLaunchKernelGGL(kCountRows, dim3((unsigned)blocks), dim3(256), 0, st, hits, nhits, qcnt);
+        SH_HIP(hipGetLastError());
+    }
+    const uint32_t n = nq + 1, tiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, n, partial);
+    hipLaunchKernelGGL(kScanPartials, dim3(1), dim3(256), 0, st, partial, tiles);
+    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, n, partial, qoff, big, nbig);
+    SH_HIP(hipGetLastError());
 }
 
-void rowOffsets(const uint4* hits, uint64_t nhits, uint64_t* off, void* tmp, size_t tmpBytes, hipStream_t st) {
-    // off[nhits] = total rows (hits[nhits] must be readable: caller zeroes it)
-    rocprim::transform_iterator<const uint4*, HitLen, uint64_t> it(hits, HitLen());
-    size_t tb = tmpBytes;
-    SH_HIP(rocprim::exclusive_scan(tmp, tb, it, off, (uint64_t)0, (size_t)nhits + 1, rocprim::plus<uint64_t>(),
-                                   st));
-}
+uint32_t scanTiles(uint32_t nq) { return (nq + 1 + kScanTile - 1) / kScanTile; }
 
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st) {
     if (a.nhits == 0) return;
@@ -1127,27 +1306,30 @@ void launchLocate(const LocateArgs& a, bool count, hipStream_t st) {
     SH_HIP(hipGetLastError());
 }
 
-size_t sortTempBytes(uint64_t n) {
+size_t bigSortTempBytes(uint64_t rows, uint32_t nbig) {
     size_t tb = 0;
-    rocprim::double_buffer<uint64_t> kb(nullptr, nullptr);
-    SH_HIP(rocprim::radix_sort_keys(nullptr, tb, kb, (size_t)n, 0, 64, (hipStream_t)0));
+    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> bi(nullptr, SegOff{nullptr, 0});
+    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> ei(nullptr, SegOff{nullptr, 1});
+    SH_HIP(rocprim::segmented_radix_sort_keys(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                              (unsigned)rows, nbig, bi, ei, 0, 36, (hipStream_t)0));
     return tb;
 }
 
-uint64_t* sortKeys(uint64_t* k0, uint64_t* k1, uint64_t n, unsigned endBit, void* tmp, size_t tmpBytes,
-                   hipStream_t st) {
-    if (n == 0) return k0;
-    rocprim::double_buffer<uint64_t> kb(k0, k1);
+void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff, uint32_t nq, const uint32_t* big,
+                uint32_t nbig, uint64_t qidBase, const uint64_t* starts, uint32_t nrec, sahara_hit* out, void* tmp,
+                size_t tmpBytes, hipStream_t st) {
+    if (rows == 0) return;
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((nq + 255) / 256, 65536));
+    hipLaunchKernelGGL(kSortDecode, dim3(blocks), dim3(256), 0, st, k0, qoff, nq, qidBase, starts, nrec, out);
+    SH_HIP(hipGetLastError());
+    if (nbig == 0) return;
+    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> bi(big, SegOff{qoff, 0});
+    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> ei(big, SegOff{qoff, 1});
     size_t tb = tmpBytes;
-    SH_HIP(rocprim::radix_sort_keys(tmp, tb, kb, (size_t)n, 0, endBit, st));
-    return kb.current();
-}
-
-void launchDecode(const uint64_t* keys, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint32_t nrec,
-                  sahara_hit* out, hipStream_t st) {
-    if (n == 0) return;
-    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 65536);
-    hipLaunchKernelGGL(kDecode, dim3((unsigned)blocks), dim3(256), 0, st, keys, n, qidBase, starts, nrec, out);
+    SH_HIP(rocprim::segmented_radix_sort_keys(tmp, tb, (const uint64_t*)k0, k1, (unsigned)rows, nbig, bi, ei, 0, 36,
+                                              st));
+    hipLaunchKernelGGL(kDecodeBig, dim3(std::min<uint32_t>(nbig, 65536)), dim3(256), 0, st, k1, qoff, big, nbig, qidBase,
+                       starts, nrec, out);
     SH_HIP(hipGetLastError());
 }
 

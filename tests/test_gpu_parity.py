@@ -221,3 +221,33 @@ def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch):
         for verify, locate_sa in MODES:
             gpu.set_mode(verify, locate_sa)
             assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (k, verify, locate_sa)
+
+
+@pytest.mark.parametrize("batch", ["97", "1000000"])
+def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch):
+    """Per-query segments of every length: reads from a 40-fold repeated unit
+    have > 8 located rows (segmented radix sort), unique reads 1-2 (register
+    sort), random reads none. SAHARA_BATCH=97 runs many batches through the
+    three-stream pipeline, with the per-query counters reused between them."""
+    monkeypatch.setenv("SAHARA_BATCH", batch)
+    rng = np.random.default_rng(5)
+    unit = random_records(rng, [400], 6)[0]
+    parts = []
+    for i in range(40):
+        u = unit.copy()
+        u[rng.integers(0, 400, size=i % 3)] = 1  # near-identical copies: varying error counts
+        parts += [u, random_records(rng, [rng.integers(50, 300)], 6)[0]]
+    recs = [np.concatenate(parts[:40]), np.concatenate(parts[40:]), random_records(rng, [5000], 6)[0]]
+    m, k = 40, 2
+    reads = np.vstack([mutate_reads(rng, [unit], 150, m, k), mutate_reads(rng, recs[2:], 150, m, k),
+                       random_records(rng, [m] * 40, 6)])
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme("h2-k2", 0, k, m)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch, nthreads=8)[0])
+    per_q = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
+    assert per_q.max() > 8 and ((per_q >= 1) & (per_q <= 8)).any() and (per_q == 0).any()
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    for verify, locate_sa in MODES:
+        gpu.set_mode(verify, locate_sa)
+        for _ in range(2):
+            assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
