@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host buffers) pass")
     ap.add_argument("--traffic-json", default=None,
                     help="measured HBM bytes per launch per kernel (tools/traffic.sh + tools/traffic_summary.py); "
                          "default profiles/traffic_<config>.json when it exists")
@@ -231,6 +232,20 @@ def main():
                  "search_grid": cnt["search_grid"], "text_grid": cnt["text_grid"],
                  "pipelined": bool(cnt["pipelined"]),
                  }
+
+    # PCIe-inclusive rate (SURVEY §8(d)'s definition; not `value`): host ranks
+    # in, located hits in host memory, through sahara_gpu_search
+    if rank == 0 and not args.no_e2e:
+        t = time.perf_counter()
+        h = sa.search(idx, pats, scheme, edit=edit)
+        dt = time.perf_counter() - t
+        st = idx.stats()
+        extra["pcie_inclusive"] = {
+            "reads_per_s": round(nreads / dt, 1), "ms": round(dt * 1e3, 1), "hits": int(len(h)),
+            "stage_ms": round(st["stage_ms"], 1), "search_ms": round(st["total_ms"], 1),
+            "output_ms": round(st["output_ms"], 1),
+            "path": "sahara_gpu_search from host ranks: H2D + pack, search, locate, sort, hits D2H into host memory"}
+        del h
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -87,6 +87,8 @@ typedef struct sahara_stats {
     uint32_t pipelined;          /* 1 if FM and text phases of consecutive batches overlapped */
     double   seed_ms;            /* starting cursors (k-mer table lookups) */
     uint64_t text_steps;         /* text-kernel micro-steps, lane count (count=1) */
+    double   stage_ms;           /* wall time of staging the patterns: H2D, 4-bit packing, rank check */
+    double   output_ms;          /* sahara_gpu_search: wall time of handing the hits to the host */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

@@ -59,7 +59,8 @@ class Stats(C.Structure):
                 ("text_refills", C.c_uint64), ("text_cycles_refill", C.c_uint64),
                 ("text_cycles_step", C.c_uint64), ("text_cycles_emit", C.c_uint64),
                 ("text_compare_steps", C.c_uint64), ("text_grid", C.c_uint32), ("pipelined", C.c_uint32),
-                ("seed_ms", C.c_double), ("text_steps", C.c_uint64)]
+                ("seed_ms", C.c_double), ("text_steps", C.c_uint64), ("stage_ms", C.c_double),
+                ("output_ms", C.c_double)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -274,6 +275,31 @@ class BiFMIndex:
             pass
 
 
+class _HitBuffer:
+    """Owner of a library-allocated hit array: the numpy view keeps it alive,
+    and the buffer goes back to sahara_gpu_free with the last reference."""
+
+    def __init__(self, ptr, n):
+        self.ptr = ptr
+        self.__array_interface__ = {"shape": (n,), "typestr": "|V%d" % HIT_DTYPE.itemsize,
+                                    "descr": HIT_DTYPE.descr, "data": (ptr, False), "version": 3}
+
+    def __del__(self):
+        if self.ptr:
+            lib().sahara_gpu_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def _hits_array(out, n):
+    if not out.value:
+        return np.zeros(0, HIT_DTYPE)
+    if n == 0:
+        lib().sahara_gpu_free(out)
+        return np.zeros(0, HIT_DTYPE)
+    a = np.asarray(_HitBuffer(out.value, n))  # zero-copy; the base frees the buffer
+    return a.view(HIT_DTYPE)
+
+
 def search(index, queries, scheme, edit=True, max_hits=0):
     """fmc::search_ng24::search<Edit> + fmc::LocateLinear (search.cpp:218-250).
 
@@ -289,13 +315,7 @@ def search(index, queries, scheme, edit=True, max_hits=0):
     _check(lib().sahara_gpu_search(index._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
                                    _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit), max_hits,
                                    C.byref(out), C.byref(n)))
-    try:
-        if n.value == 0:
-            return np.zeros(0, HIT_DTYPE)
-        raw = (C.c_uint8 * (n.value * HIT_DTYPE.itemsize)).from_address(out.value)
-        return np.frombuffer(raw, dtype=HIT_DTYPE).copy()
-    finally:
-        lib().sahara_gpu_free(out)
+    return _hits_array(out, n.value)
 
 
 def search_best(index, queries, schemes, max_hits=0):
@@ -317,13 +337,7 @@ def search_best(index, queries, schemes, max_hits=0):
     _check(lib().sahara_gpu_search_best(index._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
                                         _p(l, u32p), _p(u, u32p), _p(ns, u32p), len(schemes), max_hits,
                                         C.byref(out), C.byref(n)))
-    try:
-        if n.value == 0:
-            return np.zeros(0, HIT_DTYPE)
-        raw = (C.c_uint8 * (n.value * HIT_DTYPE.itemsize)).from_address(out.value)
-        return np.frombuffer(raw, dtype=HIT_DTYPE).copy()
-    finally:
-        lib().sahara_gpu_free(out)
+    return _hits_array(out, n.value)
 
 
 def scheme_generators():

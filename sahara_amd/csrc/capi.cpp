@@ -75,6 +75,7 @@ struct Ctx {
     DevBuf<char> tmp;
     DevBuf<sahara_hit> out;
     uint64_t nout = 0;
+    double stageMs = 0;                   // wall time of the last stage(): H2D, pack, validation
     uint32_t hitCap = 0, taskCap = 0;
     sahara_stats stats{};
     hipEvent_t ev[8] = {};
@@ -248,8 +249,7 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);
     if ((size_t)ns * m * 4 > 60 * 1024) throw Error("scheme too large for LDS (searches * len > 15360)");
     if (ns > 255) throw Error("at most 255 searches per scheme");
-    for (uint64_t i = 0; i < npat * m; ++i)
-        if (ranks[i] == 0 || ranks[i] >= c->I.sigma) throw Error("pattern rank out of range for this index");
+    const auto t0 = std::chrono::steady_clock::now();
     textTable(pi, l, u, ns, m, packed, cover);
     c->patWords = (m + 7) / 8;
     {
@@ -257,8 +257,15 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
         raw.reserve(npat * m);
         SH_HIP(hipMemcpyAsync(raw.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
         c->pats.reserve(npat * c->patWords + 4);  // + tail words read by paired loads
-        launchPackPatterns(raw.ptr, npat, m, c->patWords, c->pats.ptr, c->st);
+        SH_HIP(hipMemsetAsync(c->small.ptr, 0, sizeof(uint32_t), c->st));
+        launchPackPatterns(raw.ptr, npat, m, c->patWords, c->I.sigma, c->pats.ptr, c->small.ptr, c->st);
+        uint32_t bad = 0;
+        SH_HIP(hipMemcpyAsync(&bad, c->small.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
         SH_HIP(hipStreamSynchronize(c->st));
+        if (bad) {
+            c->staged = false;
+            throw Error("pattern rank out of range for this index");
+        }
     }
     c->scheme.reserve(packed.size());
     SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
@@ -284,6 +291,7 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     c->nsearch = ns;
     c->edit = edit != 0;
     c->staged = true;
+    c->stageMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 
@@ -312,6 +320,7 @@ void run(Ctx* c, bool count) {
         runPass(c, count, true, S, overflow);
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    S.stage_ms = c->stageMs;
     c->stats = S;
 }
 
@@ -830,10 +839,26 @@ int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint
         Ctx* c = ctxOf(ctx);
         stage(c, ranks, n_patterns, len, pi, l, u, n_searches, edit);
         run(c, false);
-        std::vector<sahara_hit> v(c->nout);
-        if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
-        if (max_hits) limitHits(v, max_hits);
-        handOver(v, hits, n_hits);
+        const auto t0 = std::chrono::steady_clock::now();
+        if (max_hits) {
+            std::vector<sahara_hit> v(c->nout);
+            if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
+            limitHits(v, max_hits);
+            handOver(v, hits, n_hits);
+        } else {  // straight into the caller-owned buffer
+            auto* buf = static_cast<sahara_hit*>(std::malloc(std::max<uint64_t>(c->nout, 1) * sizeof(sahara_hit)));
+            if (!buf) throw Error("out of host memory for hits");
+            if (c->nout) {
+                const hipError_t e = hipMemcpy(buf, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost);
+                if (e != hipSuccess) {
+                    std::free(buf);
+                    SH_HIP(e);
+                }
+            }
+            *hits = buf;
+            *n_hits = c->nout;
+        }
+        c->stats.output_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
 }
 

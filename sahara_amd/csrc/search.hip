@@ -1183,9 +1183,12 @@ __global__ void kDigest(const sahara_hit* __restrict__ h, uint64_t n, unsigned l
 }
 
 // pattern bytes (one symbol per byte) -> 4-bit words, patWords per pattern
+// Also validates the ranks (ivs::verify_rank, search.cpp:118-120): *bad != 0
+// if any is 0 or >= sigma.
 __global__ void kPackPatterns(const uint8_t* __restrict__ src, uint64_t npat, uint32_t m, uint32_t patWords,
-                              uint32_t* __restrict__ dst) {
+                              uint32_t sigma, uint32_t* __restrict__ dst, uint32_t* __restrict__ bad) {
     const uint64_t total = npat * patWords;
+    bool invalid = false;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p = i / patWords;
@@ -1193,10 +1196,15 @@ __global__ void kPackPatterns(const uint8_t* __restrict__ src, uint64_t npat, ui
         uint32_t v = 0;
         for (uint32_t j = 0; j < 8; ++j) {
             const uint32_t q = w * 8 + j;
-            if (q < m) v |= (uint32_t)(src[p * m + q] & 0xFu) << (4 * j);
+            if (q < m) {
+                const uint32_t r = src[p * m + q];
+                invalid |= r == 0 || r >= sigma;
+                v |= (r & 0xFu) << (4 * j);
+            }
         }
         dst[i] = v;
     }
+    if (__any(invalid) && (threadIdx.x & 63u) == 0) atomicOr(bad, 1u);
 }
 
 struct SegOff {  // begin (d = 0) / end (d = 1) of a listed query's segment
@@ -1273,11 +1281,11 @@ void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const
     SH_HIP(hipGetLastError());
 }
 
-void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t* dst,
-                        hipStream_t st) {
+void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
+                        uint32_t* dst, uint32_t* bad, hipStream_t st) {
     const uint64_t blocks = std::min<uint64_t>((npat * patWords + 255) / 256, 65536);
     hipLaunchKernelGGL(kPackPatterns, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(256), 0, st, src, npat, m,
-                       patWords, dst);
+                       patWords, sigma, dst, bad);
     SH_HIP(hipGetLastError());
 }
 

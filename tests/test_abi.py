@@ -88,3 +88,27 @@ def test_interleave_rc():
 def test_generators_listed():
     g = sa.scheme_generators()
     assert "h2-k2" in g and "backtracking" in g and "pigeon" in g
+
+
+def test_hit_arrays_are_zero_copy_views_freed_by_the_library():
+    import ctypes as C
+    import gc
+    libc = C.CDLL(None)
+    libc.malloc.restype = C.c_void_p
+    libc.malloc.argtypes = [C.c_size_t]
+    n = 5
+    ptr = libc.malloc(n * sa.HIT_DTYPE.itemsize)
+    src = np.zeros(n, sa.HIT_DTYPE)
+    src["qid"] = np.arange(n) * 3
+    src["pos"] = 7
+    C.memmove(ptr, src.ctypes.data, src.nbytes)
+    a = sa._hits_array(C.c_void_p(ptr), n)
+    assert a.dtype == sa.HIT_DTYPE and a.ctypes.data == ptr
+    assert a["qid"].tolist() == [0, 3, 6, 9, 12] and (a["pos"] == 7).all()
+    b = a[1:3]  # views keep the buffer alive
+    del a
+    gc.collect()
+    assert b["qid"].tolist() == [3, 6]
+    del b
+    gc.collect()
+    assert len(sa._hits_array(C.c_void_p(None), 0)) == 0
