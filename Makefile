@@ -13,7 +13,7 @@ HDRS     := $(wildcard $(CSRC)/*.h) include/sahara_hip.h
 
 OBJS := $(OBJDIR)/index_build.o $(OBJDIR)/search.o $(OBJDIR)/capi.o $(OBJDIR)/host_util.o $(OBJDIR)/scheme.o
 
-all: $(LIB) oracle $(if $(wildcard sahara_amd/cli/*.cpp),$(CLI),)
+all: $(LIB) oracle $(if $(wildcard sahara_amd/cli/*.cpp),$(CLI),) tools/gather_bench
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -39,6 +39,9 @@ CLI_SRC := $(wildcard sahara_amd/cli/*.cpp)
 $(CLI): $(CLI_SRC) $(wildcard sahara_amd/cli/*.h) include/sahara_hip.h $(LIB)
 	@mkdir -p bin
 	g++ $(CXXFLAGS) -Iinclude $(CLI_SRC) -o $@ -L$(LIBDIR) -lsahara_hip -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+tools/gather_bench: tools/gather_bench.hip
+	$(HIPCC) $(HIPFLAGS) $< -o $@
 
 oracle:
 	$(MAKE) -C oracle
