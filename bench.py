@@ -11,8 +11,10 @@ generator h2-k2.
 
 Multi-GPU (torchrun, one process per GPU): every rank builds the full index
 on its own GPU (replicated, as SURVEY §8(e) prescribes), searches its own
-shard of 10M reads (weak scaling), and the per-rank hit counts and digests
-are all-gathered over RCCL. No collective sits on the data path.
+shard of 10M reads (weak scaling); the max step time and hit counts are
+reduced over RCCL. No collective sits on the data path. After the timed
+steps, the hit records are gathered to rank 0 over RCCL (xGMI) in a step of
+their own, reported as config.hit_gather (not part of `value`).
 
 Rank 0 at N=1 also times the CPU restatement (oracle/, the reference's
 algorithm restated in C++) on a bounded sample of the same reads on the host
@@ -90,6 +92,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host buffers) pass")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed RCCL gather of hit records")
     ap.add_argument("--traffic-json", default=None,
                     help="measured HBM bytes per launch per kernel (tools/traffic.sh + tools/traffic_summary.py); "
                          "default profiles/traffic_<config>.json when it exists")
@@ -163,10 +166,13 @@ def main():
     elapsed = time.perf_counter() - t0
     digest = idx.digest()
 
+    gather = None
     if world > 1:
         from sahara_amd.dist import max_over_ranks, sum_over_ranks
         elapsed = max_over_ranks(elapsed, device="cuda")  # RCCL over xGMI
         total_hits = sum_over_ranks(nh, device="cuda")
+        if not args.no_gather:
+            gather = gather_step(idx, nh, nreads, world, rank, barrier, dist, torch)
     else:
         total_hits = nh
 
@@ -273,12 +279,46 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if gather:
+        gather["reads_per_s_incl_gather"] = round(nreads * world / (ms_per_step / 1e3 + gather["ms"] / 1e3), 1)
+        out["config"]["hit_gather"] = gather
     if cpu and cpu.get("value"):
         out["config"]["gpu_over_cpu"] = round(reads_per_s / cpu["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def gather_step(idx, nh, nreads, world, rank, barrier, dist, torch, device="cuda"):
+    """the last step's hit records (24-B sahara_hit, global
+    qids) gathered to rank 0 over RCCL (xGMI), timed on its own (barrier +
+    synchronize on both sides, max over ranks) and checked record for record
+    by per-rank word sums. Not part of `value` (hits stay in HBM at N=1 too)."""
+    from sahara_amd.dist import gather_hit_records, max_over_ranks
+
+    local = {}
+
+    def fill(buf):
+        idx.copy_hits(buf.data_ptr(), buf.shape[0], qid_offset=2 * nreads * rank)
+        local["sum"] = buf[:nh].sum()
+
+    barrier()
+    t = time.perf_counter()
+    parts, counts = gather_hit_records(nh, fill, device=device)
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t, device=device)
+    sums = [torch.zeros_like(local["sum"]) for _ in range(world)]
+    dist.all_gather(sums, local["sum"])
+    ok = None
+    if rank == 0:
+        ok = bool(all(int(p.sum().item()) == int(s.item()) for p, s in zip(parts, sums)))
+        qmin = [int(p[:, 0].min().item()) if len(p) else None for p in parts]
+        ok = ok and all(q is None or q >= 2 * nreads * r for r, q in enumerate(qmin))
+    nrec = sum(counts)
+    return {"ms": round(el * 1e3, 2), "records": nrec, "bytes": nrec * 24,
+            "GBs_into_rank0": round(nrec * 24 / el / 1e9, 1), "verified": ok,
+            "collective": "all_gather of counts + gather of padded 24-B records to rank 0 (RCCL over xGMI)"}
 
 
 def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):

@@ -152,6 +152,11 @@ int  sahara_gpu_stage(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint
                       int edit);
 int  sahara_gpu_run(void* ctx, int count, uint64_t* n_hits);
 int  sahara_gpu_fetch(void* ctx, sahara_hit* out, uint64_t capacity, uint64_t* n_hits);
+/* The last run's hits, copied on the device into dst_device (device memory of
+ * the context's GPU, >= capacity records) with qid_offset added to every qid:
+ * rank-local -> global qids, ready for a gather of hit records across GPUs
+ * (the reference is single-process, search.cpp:218-261). */
+int  sahara_gpu_copy_hits(void* ctx, void* dst_device, uint64_t capacity, uint64_t qid_offset, uint64_t* n_hits);
 /* Order-independent digest of the last run's hits (sum of a 64-bit mix of
  * each record) computed on the device. */
 int  sahara_gpu_digest(void* ctx, uint64_t* digest);

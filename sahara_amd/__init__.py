@@ -91,6 +91,7 @@ EXPORTED = {
     "sahara_gpu_run": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "sahara_gpu_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "sahara_gpu_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "sahara_gpu_copy_hits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "sahara_gpu_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "sahara_gpu_free": (None, [C.c_void_p]),
     "sahara_gpu_close": (None, [C.c_void_p]),
@@ -114,7 +115,8 @@ EXPORTED = {
 
 
 def library_path():
-    return os.path.join(_HERE, "lib", "libsahara_hip.so")
+    # SAHARA_HIP_LIB: another build of the same library (A/B benchmarks)
+    return os.environ.get("SAHARA_HIP_LIB") or os.path.join(_HERE, "lib", "libsahara_hip.so")
 
 
 def lib():
@@ -127,6 +129,8 @@ def lib():
                               f"__graft_entry__.build())")
         L = C.CDLL(path)
         for name, (res, args) in EXPORTED.items():
+            if os.environ.get("SAHARA_HIP_LIB") and not hasattr(L, name):
+                continue  # an older build under A/B comparison
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -252,6 +256,14 @@ class BiFMIndex:
         out = np.zeros(max(st["hits"], 1), HIT_DTYPE)
         _check(lib().sahara_gpu_fetch(self._h, out.ctypes.data_as(C.c_void_p), len(out), C.byref(n)))
         return out[: n.value]
+
+    def copy_hits(self, dst_ptr, capacity, qid_offset=0):
+        """Copy the last run's hits (HIT_DTYPE records) into device memory at
+        dst_ptr (e.g. a torch tensor's data_ptr() on this GPU), qids shifted by
+        qid_offset. Returns the number of records."""
+        n = C.c_uint64()
+        _check(lib().sahara_gpu_copy_hits(self._h, C.c_void_p(dst_ptr), capacity, qid_offset, C.byref(n)))
+        return n.value
 
     def digest(self):
         d = C.c_uint64()

@@ -36,9 +36,10 @@ struct Ctx {
     DeviceIndex I;
 
     // staged inputs
-    DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern
+    DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern (FM phase)
+    DevBuf<uint4> pats3;                  // 3-bit-plane blocks, patBlocks per pattern (text phase)
     uint64_t npat = 0;
-    uint32_t m = 0, patWords = 0;
+    uint32_t m = 0, patWords = 0, patBlocks = 0;
     DevBuf<uint32_t> scheme, cover, kmerStart;        // FM scheme table; text table (textTable)
     uint32_t nsearch = 0;
     uint32_t maxErr = 0;
@@ -259,6 +260,9 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
         c->pats.reserve(npat * c->patWords + 4);  // + tail words read by paired loads
         SH_HIP(hipMemsetAsync(c->small.ptr, 0, sizeof(uint32_t), c->st));
         launchPackPatterns(raw.ptr, npat, m, c->patWords, c->I.sigma, c->pats.ptr, c->small.ptr, c->st);
+        c->patBlocks = (m + 31) / 32;
+        c->pats3.reserve(npat * c->patBlocks);
+        launchPackPatterns3(raw.ptr, npat, m, c->patBlocks, c->pats3.ptr, c->st);
         uint32_t bad = 0;
         SH_HIP(hipMemcpyAsync(&bad, c->small.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, c->st));
         SH_HIP(hipStreamSynchronize(c->st));
@@ -338,14 +342,15 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
     int bpc = fullBpc;
     // Overlapped with the text phase of the previous batch, the FM phase
-    // (memory-latency bound) runs with one workgroup per CU and leaves the
-    // CUs' issue slots to the text phase (ALU bound); alone it takes them all.
+    // (memory-latency bound) runs with two workgroups per CU and leaves the
+    // CUs' other issue slots to the text phase (ALU bound); alone it takes
+    // them all. (Measured at C3: 1 WG/CU 24.0 ms/step, 2: 19.5, 3: 20.4, 4: 20.9.)
     // patterns per batch: 4M, fewer for schemes with many searches (work
     // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (const char* e = std::getenv("SAHARA_BATCH")) maxBatch = std::max<uint64_t>(1, std::min<uint64_t>(maxBatch, std::atoll(e)));
     const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
-    if (!serial && batchesHere > 1 && c->verify) bpc = 1;
+    if (!serial && batchesHere > 1 && c->verify) bpc = std::min(2, fullBpc);
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     // the first batch's FM phase has nothing to overlap with: full occupancy
@@ -357,16 +362,20 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
 
     // text phase geometry (LDS per lane: window | pattern | stack)
     // window: |t| + what both sides can still consume <= m + 2k symbols, plus
-    // the word alignment of its start (7 symbols); an even number of words
-    const uint32_t winWords = ((c->m + 2 * c->maxErr + 7 + 7) / 8 + 1) & ~1u;
+    // the block alignment of its start (31 symbols); 3 words per block
+    const uint32_t winBlocks = (c->m + 2 * c->maxErr + 31 + 31) / 32;
     const uint32_t textStack = 2 * c->maxErr + 2;
     const size_t textLds = (size_t)2 * c->nsearch * c->m * 4 +
-                           (size_t)256 * (winWords + c->patWords + 2 * textStack) * 4;
+                           (size_t)256 * (3 * (winBlocks + c->patBlocks) + 2 * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
     int tbpc = 0;
-    if (c->verify && c->m <= 2047 && textLds <= 160 * 1024) tbpc = textBlocksPerCU(sigma, c->edit, textLds);
+    // the text phase addresses text and a batch's patterns with 32-bit buffer offsets
+    const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
+                          maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
+    if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
+        tbpc = textBlocksPerCU(sigma, c->edit, textLds);
     if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(tbpc, std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
@@ -496,9 +505,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         if (split) {
             TextArgs t{};
             t.sa = c->I.saFull.ptr;
-            t.text4w = reinterpret_cast<const uint32_t*>(c->I.text4.ptr);
-            t.pats = c->pats.ptr + q0 * c->patWords;
-            t.patWords = c->patWords;
+            t.text3 = c->I.text3.ptr;
+            t.pats3 = c->pats3.ptr + q0 * c->patBlocks;
+            t.patBlocks = c->patBlocks;
+            t.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
+            t.pats3Bytes = (uint32_t)std::min<uint64_t>((c->npat - q0) * c->patBlocks * 16, 0xFFFFFF00ull);
             t.m = c->m;
             t.nsearch = c->nsearch;
             t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
@@ -512,7 +523,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.filled = sl.small.ptr + 3;
             t.flags = sl.small.ptr + 2;
             t.counters = c->counters.ptr;
-            t.winWords = winWords;
+            t.winBlocks = winBlocks;
             t.stackCap = textStack;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
@@ -757,9 +768,13 @@ int sahara_gpu_export_sa(void* ctx, uint32_t* sa) {
 int sahara_gpu_export_text(void* ctx, uint8_t* text) {
     return guarded([&] {
         Ctx* c = ctxOf(ctx);
-        std::vector<uint8_t> t4((c->I.n + 1) / 2);
-        SH_HIP(hipMemcpy(t4.data(), c->I.text4.ptr, t4.size(), hipMemcpyDeviceToHost));
-        for (uint64_t i = 0; i < c->I.n; ++i) text[i] = (t4[i >> 1] >> ((i & 1) * 4)) & 15;
+        std::vector<uint32_t> t3(((c->I.n + 31) / 32) * 4);
+        SH_HIP(hipMemcpy(t3.data(), c->I.text3.ptr, t3.size() * 4, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < c->I.n; ++i) {
+            const uint32_t* b = &t3[(i / 32) * 4];
+            const uint32_t j = (uint32_t)(i & 31);
+            text[i] = (uint8_t)(((b[0] >> j) & 1u) | (((b[1] >> j) & 1u) << 1) | (((b[2] >> j) & 1u) << 2));
+        }
     });
 }
 
@@ -813,6 +828,17 @@ int sahara_gpu_fetch(void* ctx, sahara_hit* out, uint64_t capacity, uint64_t* n_
         if (n_hits) *n_hits = c->nout;
         if (capacity < c->nout) throw Error("sahara_gpu_fetch: capacity too small");
         if (c->nout) SH_HIP(hipMemcpy(out, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
+    });
+}
+
+int sahara_gpu_copy_hits(void* ctx, void* dst_device, uint64_t capacity, uint64_t qid_offset, uint64_t* n_hits) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (n_hits) *n_hits = c->nout;
+        if (capacity < c->nout) throw Error("sahara_gpu_copy_hits: capacity too small");
+        if (c->nout && !dst_device) throw Error("sahara_gpu_copy_hits: null destination");
+        launchCopyHits(c->out.ptr, c->nout, qid_offset, static_cast<sahara_hit*>(dst_device), c->st);
+        SH_HIP(hipStreamSynchronize(c->st));
     });
 }
 

@@ -44,7 +44,12 @@ struct DevBuf {  // minimal owning device buffer that only ever grows
     DevBuf& operator=(const DevBuf&) = delete;
 };
 
-constexpr uint64_t kTextPad = 1u << 16;  // zero padding after the packed text (text-phase windows)
+// Text (and patterns) for the text phase as 3-bit-plane blocks: block i holds
+// symbols [32i, 32i+32) as {plane0, plane1, plane2, 0}, bit j of plane b =
+// bit b of symbol 32i+j. One 16-B load per 32 symbols, and per-symbol masks of
+// 32 symbols come out of 3 word operations (search.hip, kSearchText).
+constexpr uint64_t kTextPadBlocks = 4096;  // zero blocks after the text (text-phase windows)
+inline uint64_t text3Blocks(uint64_t n) { return (n + 31) / 32 + kTextPadBlocks; }
 
 struct DeviceIndex {
     int device = 0;
@@ -60,7 +65,7 @@ struct DeviceIndex {
     DevBuf<uint64_t> dRecStarts;
     // Resident for the search (HBM is 288 GB; at 3 Gbp these are 12 + 1.5 GB):
     DevBuf<uint32_t> saFull;        // SA[row] for every row: locate = one read
-    DevBuf<uint8_t> text4;          // text, 4 bits per symbol (two per byte), '$' = 0, kTextPad zero bytes after
+    DevBuf<uint4> text3;            // text as 3-bit-plane blocks of 32 symbols, '$' = 0, kTextPadBlocks zero blocks after
     // k-mer table: the bidirectional cursor {lb, lbRev, len, 0} of every
     // ACGT string of length kmerK (2 bits per symbol, first symbol most
     // significant). A search whose first kmerK steps admit no error starts
@@ -69,7 +74,7 @@ struct DeviceIndex {
     uint32_t kmerK = 0;
     uint64_t deviceBytes() const {
         return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8 + saFull.cap * 4 +
-               text4.cap + kmer.cap * sizeof(uint4);
+               text3.cap * sizeof(uint4) + kmer.cap * sizeof(uint4);
     }
 };
 

@@ -228,13 +228,21 @@ __global__ void kSampledWords(const OccLine* __restrict__ lines, uint64_t nb, ui
 
 
 // text bytes (one symbol per byte) -> 4-bit packed, two symbols per byte
-__global__ void kPackText(const uint8_t* __restrict__ T, uint64_t N, uint8_t* __restrict__ t4) {
-    const uint64_t nb = (N + 1) / 2;
+// text (one symbol per byte) -> 3-bit-plane blocks of 32 symbols (device_index.h)
+__global__ void kPackText(const uint8_t* __restrict__ T, uint64_t N, uint4* __restrict__ t3) {
+    const uint64_t nb = (N + 31) / 32;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nb;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint8_t a = T[2 * i];
-        const uint8_t b = (2 * i + 1 < N) ? T[2 * i + 1] : 0;
-        t4[i] = (uint8_t)(a | (b << 4));
+        uint32_t p0 = 0, p1 = 0, p2 = 0;
+        const uint64_t base = 32 * i;
+        const uint32_t cnt = (uint32_t)(N - base < 32 ? N - base : 32);
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t c = T[base + j];
+            p0 |= (c & 1u) << j;
+            p1 |= ((c >> 1) & 1u) << j;
+            p2 |= ((c >> 2) & 1u) << j;
+        }
+        t3[i] = make_uint4(p0, p1, p2, 0u);
     }
 }
 
@@ -471,9 +479,9 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
     // resident full SA + packed text for the search (locate = one read)
     I.saFull.reserve(N);
     SH_HIP(hipMemcpyAsync(I.saFull.ptr, sa.ptr, N * 4, hipMemcpyDeviceToDevice, st));
-    I.text4.reserve((N + 1) / 2 + kTextPad);
-    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (N + 1) / 2 + kTextPad, st));
-    hipLaunchKernelGGL(kPackText, dim3(gridFor((N + 1) / 2)), dim3(kTB), 0, st, T.ptr, N, I.text4.ptr);
+    I.text3.reserve(text3Blocks(N));
+    SH_HIP(hipMemsetAsync(I.text3.ptr, 0, text3Blocks(N) * sizeof(uint4), st));
+    hipLaunchKernelGGL(kPackText, dim3(gridFor((N + 31) / 32)), dim3(kTB), 0, st, T.ptr, N, I.text3.ptr);
     SH_HIP(hipGetLastError());
 
     // reverse direction: SA, BWT, lines (no sampling)
@@ -524,9 +532,9 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     hipLaunchKernelGGL(kDensify, dim3(gridFor(n)), dim3(kTB), 0, st, I.occF.ptr, n, I.samples.ptr, dC.ptr, rate,
                        I.saFull.ptr, bwt.ptr, err.ptr);
     SH_HIP(hipGetLastError());
-    I.text4.reserve((n + 1) / 2 + kTextPad);
-    SH_HIP(hipMemsetAsync(I.text4.ptr, 0, (n + 1) / 2 + kTextPad, st));
-    hipLaunchKernelGGL(kPackText, dim3(gridFor((n + 1) / 2)), dim3(kTB), 0, st, bwt.ptr, n, I.text4.ptr);
+    I.text3.reserve(text3Blocks(n));
+    SH_HIP(hipMemsetAsync(I.text3.ptr, 0, text3Blocks(n) * sizeof(uint4), st));
+    hipLaunchKernelGGL(kPackText, dim3(gridFor((n + 31) / 32)), dim3(kTB), 0, st, bwt.ptr, n, I.text3.ptr);
     SH_HIP(hipGetLastError());
     unsigned int herr = 0;
     SH_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, st));

@@ -54,9 +54,11 @@ struct SeedArgs {
 
 struct TextArgs {
     const uint32_t* sa;      // full SA (tasks arrive resolved by launchResolveTasks)
-    const uint32_t* text4w;  // 4-bit packed text as u32 words (8 symbols each)
-    const uint32_t* pats;
-    uint32_t patWords;
+    const uint4* text3;      // text as 3-bit-plane blocks of 32 symbols (device_index.h)
+    const uint4* pats3;      // patterns as 3-bit-plane blocks, patBlocks per pattern
+    uint32_t patBlocks;
+    uint32_t text3Bytes;     // bytes of text3 / of this batch's pats3 (buffer-load bounds; < 4 GiB)
+    uint32_t pats3Bytes;
     uint32_t m;
     uint32_t nsearch;
     const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
@@ -70,7 +72,7 @@ struct TextArgs {
     uint32_t* filled;
     uint32_t* flags;
     unsigned long long* counters;
-    uint32_t winWords;       // window words per lane (8 symbols each)
+    uint32_t winBlocks;      // window blocks per lane (32 symbols each)
     uint32_t stackCap;       // text DFS stack entries per lane
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
@@ -116,6 +118,9 @@ size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
 void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff, uint32_t nq, const uint32_t* big,
                 uint32_t nbig, uint64_t qidBase, const uint64_t* starts, uint32_t nrec, sahara_hit* out, void* tmp,
                 size_t tmpBytes, hipStream_t st);
+void launchPackPatterns3(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patBlocks, uint4* dst,
+                         hipStream_t st);
 void launchDigest(const sahara_hit* h, uint64_t n, unsigned long long* out, hipStream_t st);
+void launchCopyHits(const sahara_hit* h, uint64_t n, uint64_t qidOffset, sahara_hit* dst, hipStream_t st);
 
 }  // namespace sahara

@@ -533,8 +533,8 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 // LDS: table[S*m] (uint2: packed scheme | run << 25, covered [a, b)) | per
 // lane, interleaved so that the lanes of a wave hit consecutive banks at
 // equal offsets:
-//   window  (winWords u32 words of 8 nibbles)   W[j*256 + t]
-//   pattern (patWords u32 words of 8 nibbles)   P[j*256 + t]
+//   window  (winBlocks blocks of 32 symbols)     W[(3j+b)*256 + t], plane b
+//   pattern (patBlocks blocks of 32 symbols)     P[(3j+b)*256 + t]
 //   stack   (stackCap uint2 entries)            S[d*256 + t]
 //
 // A lane's state is one DFS node `cur` (x = window offsets xo | yo << 16 of
@@ -549,57 +549,77 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 
 
 
-// ---- 16-symbol runs as u64 (symbol j in nibble j) and per-symbol bit masks
-// (bit 4j for symbol j)
-constexpr uint64_t kOnes16 = 0x1111111111111111ull;
-__device__ __forceinline__ uint64_t ones16(uint32_t n) {  // symbols [0, n), n <= 16
-    return n >= 16u ? kOnes16 : kOnes16 & ((1ull << (4u * n)) - 1ull);
+// ---- runs of symbols as bit masks: bit j = chain symbol j. Symbols come as
+// 3 bit planes (device_index.h), so the per-symbol equality of 32 symbols is
+// three word xors; the chain logic uses the low 16 bits.
+constexpr uint32_t kRun = 16;              // symbols per micro-step run
+constexpr uint32_t kRunMask = 0xFFFFu;
+__device__ __forceinline__ uint32_t onesR(uint32_t n) {  // symbols [0, n), capped at kRun
+    return n >= kRun ? kRunMask : (1u << n) - 1u;
 }
-__device__ __forceinline__ uint64_t beyond16(uint32_t n) { return kOnes16 & ~ones16(n); }  // symbols >= n
-__device__ __forceinline__ uint64_t nz16(uint64_t x) { return (x | (x >> 1) | (x >> 2) | (x >> 3)) & kOnes16; }
-__device__ __forceinline__ uint64_t eq16(uint64_t a, uint64_t b) { return ~nz16(a ^ b) & kOnes16; }
-// bit 4j set iff bits 4j .. 4(j+6) are all set (7 consecutive matches from j)
-__device__ __forceinline__ uint64_t run7(uint64_t m) {
-    const uint64_t m2 = m & (m >> 4), m4 = m2 & (m2 >> 8);
-    return m4 & (m2 >> 16) & (m >> 24);
+__device__ __forceinline__ uint32_t beyondR(uint32_t n) { return kRunMask & ~onesR(n); }  // symbols >= n
+// bit j set iff bits j .. j+6 are all set (7 consecutive matches from j)
+__device__ __forceinline__ uint32_t run7(uint32_t m) {
+    const uint32_t m2 = m & (m >> 1), m4 = m2 & (m2 >> 2);
+    return m4 & (m2 >> 4) & (m >> 6);
 }
-// nibbles [o, o+16) of an interleaved word array (reads may run past the
-// array into the lane's next region; callers mask)
-__device__ __forceinline__ uint64_t read16(const uint32_t* A, uint32_t o) {
-    const uint32_t i = o >> 3, sh = (o & 7u) * 4u;
-    const uint32_t w0 = A[i * 256u], w1 = A[(i + 1u) * 256u], w2 = A[(i + 2u) * 256u];
-    return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
+struct Planes { uint32_t b0, b1, b2; };
+__device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
+    return ~((p.b0 ^ t.b0) | (p.b1 ^ t.b1) | (p.b2 ^ t.b2));
 }
-__device__ __forceinline__ uint32_t revNib32(uint32_t x) {
-    x = __builtin_bswap32(x);
-    return ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+__device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
+// 32 symbols from offset o of a lane's interleaved plane array (block i, plane
+// b at word (3i + b) * 256). Reads may run past the array into the lane's
+// next region; callers mask.
+__device__ __forceinline__ uint32_t read32(const uint32_t* A, uint32_t o, uint32_t b) {
+    const uint32_t i = o >> 5;
+    return __builtin_amdgcn_alignbit(A[(3u * i + 3u + b) * 256u], A[(3u * i + b) * 256u], o & 31u);
 }
-__device__ __forceinline__ uint64_t rev16(uint64_t v) {
-    return (uint64_t)revNib32((uint32_t)(v >> 32)) | ((uint64_t)revNib32((uint32_t)v) << 32);
+// 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
+// reversed (back: bit j = symbol o - 1 - j, 0 before the array start)
+__device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
+    const uint32_t off = fwd ? o : (o >= 32u ? o - 32u : 0u);
+    const uint32_t sh = fwd || o >= 32u ? 0u : 32u - o;
+    Planes r;
+    uint32_t v[3];
+#pragma unroll
+    for (uint32_t b = 0; b < 3; ++b) {
+        const uint32_t w = read32(A, off, b);
+        const uint32_t ws = sh >= 32u ? 0u : w << sh;
+        v[b] = fwd ? w : __builtin_bitreverse32(ws);
+    }
+    r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
+    return r;
 }
 
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef u32x2 u32x2a4 __attribute__((aligned(4)));
+// Raw buffer resource over [base, base + bytes) (gfx9 dword3): loads at an
+// offset past the end return 0 without a memory request, so guarded loads
+// need no branch (and no wait at a branch join).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bufferOf(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+constexpr uint32_t kBufOOB = 0xFFFFFFFFu;  // offset of a load that returns 0
 
-// Copy two word arrays (window, pattern) from global memory into this lane's
-// interleaved LDS slots: all loads of a 16-word block are issued before the
-// first store, so a task start costs one memory round trip for m <~ 110.
-__device__ __forceinline__ void copyPair(uint32_t* DA, const u32x2a4* A, uint32_t na, uint32_t* DB,
-                                         const u32x2a4* B, uint32_t nb) {
+// Copy two block arrays (window, pattern) from global memory into this lane's
+// interleaved LDS slots (3 words per block): all loads of up to 8 blocks of
+// each array are issued before the first store, so a task start costs one
+// memory round trip for m <~ 190.
+__device__ __forceinline__ void copyBlocks(uint32_t* DA, __amdgpu_buffer_rsrc_t RA, uint32_t offA, uint32_t na,
+                                           uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB, uint32_t nb) {
     const uint32_t n = max(na, nb);
-    for (uint32_t b = 0; b < n; b += 16) {
-        u32x2 va[8], vb[8];
+    for (uint32_t c = 0; c < n; c += 8) {
+        decltype(__builtin_amdgcn_raw_buffer_load_b128(RA, 0u, 0, 0)) va[8], vb[8];
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
-            const uint32_t j = b + 2u * i;
-            if (j < na) va[i] = A[j >> 1];
-            if (j < nb) vb[i] = B[j >> 1];
+            const uint32_t j = c + i;
+            va[i] = __builtin_amdgcn_raw_buffer_load_b128(RA, j < na ? offA + 16u * j : kBufOOB, 0, 0);
+            vb[i] = __builtin_amdgcn_raw_buffer_load_b128(RB, j < nb ? offB + 16u * j : kBufOOB, 0, 0);
         }
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
-            const uint32_t j = b + 2u * i;
-            if (j < na) { DA[j * 256u] = va[i].x; if (j + 1u < na) DA[(j + 1u) * 256u] = va[i].y; }
-            if (j < nb) { DB[j * 256u] = vb[i].x; if (j + 1u < nb) DB[(j + 1u) * 256u] = vb[i].y; }
+            const uint32_t j = c + i;
+            if (j < na) { uint32_t* D = DA + 3u * j * 256u; D[0] = va[i][0]; D[256] = va[i][1]; D[512] = va[i][2]; }
+            if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[i][0]; D[256] = vb[i][1]; D[512] = vb[i][2]; }
         }
     }
 }
@@ -623,11 +643,13 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t ltMask = (1ull << lane) - 1ull;
-    const uint32_t winWords = a.winWords, patWords = a.patWords;
+    const uint32_t winBlocks = a.winBlocks, patBlocks = a.patBlocks;
     uint32_t* W = slot + threadIdx.x;
-    uint32_t* P = slot + winWords * 256u + threadIdx.x;
-    uint2* S = reinterpret_cast<uint2*>(slot + (winWords + patWords) * 256u) + threadIdx.x;
-    const uint32_t winLen = winWords * 8u;
+    uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
+    uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
+    const uint32_t winLen = winBlocks * 32u;
+    const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
+    const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
     const uint32_t m = a.m;
     const uint32_t ntasks = min(*a.taskCount, a.taskCap);
 
@@ -709,9 +731,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
                 const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
-                wb = (x > left ? x - left : 0u) & ~7u;              // word-aligned window start
-                copyPair(W, reinterpret_cast<const u32x2a4*>(a.text4w + (wb >> 3)), winWords, P,
-                         reinterpret_cast<const u32x2a4*>(a.pats + (size_t)pid * patWords), patWords);
+                wb = (x > left ? x - left : 0u) & ~31u;             // block-aligned window start
+                copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
                 have = true;
             }
@@ -749,26 +770,20 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const bool r0 = (t0 >> 24) & 1u;
             const uint32_t run0 = t0 >> 25, same0 = (tab.y >> 24) & 0x7Fu;
 
-            // ---- 16 pattern symbols from pi[pos] in this step's direction and
-            // the 16 text symbols beyond the span on that side, both in chain
-            // order (symbol j of the chain in nibble j); text past the window
-            // edge or before the text start reads as 0 and never matches
-            // one read each at a side-dependent offset (a left run ends at the
-            // position and is reversed), so the lanes of both sides share it
-            const uint32_t pOff = r0 ? q0 : (q0 >= 15u ? q0 - 15u : 0u);
-            const uint32_t tOff = r0 ? yo : (xo >= 16u ? xo - 16u : 0u);
-            const uint64_t pr = read16(P, pOff), tr = read16(W, tOff);
-            const uint32_t pSh = !r0 && q0 < 15u ? 4u * (15u - q0) : 0u;
-            const uint32_t tSh = !r0 && xo < 16u ? 4u * (16u - xo) : 0u;
-            const uint64_t pa = pr << pSh, ta = tSh >= 64u ? 0ull : tr << tSh;
-            const uint64_t P16 = r0 ? pa : rev16(pa);
-            const uint64_t T16 = r0 ? ta : rev16(ta);
+            // ---- pattern symbols from pi[pos] in this step's direction and
+            // the text symbols beyond the span on that side, both in chain
+            // order (symbol j of the chain in bit j); text past the window
+            // edge or before the text start reads as 0 and never matches.
+            // One read each at a side-dependent offset (a left run ends at the
+            // position and is bit-reversed), so the lanes of both sides share it
+            const Planes P16 = chain32(P, r0 ? q0 : q0 + 1u, r0);
+            const Planes T16 = chain32(W, r0 ? yo : xo, r0);
             const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
-            const uint64_t VT = ones16(min(avail, 16u));
-            const uint64_t E0 = eq16(P16, T16) & VT;                // p_j == t_j     (M chain, S runs)
-            const uint64_t ED = eq16(P16, T16 >> 4) & (VT >> 4);    // p_j == t_{j+1} (D runs)
-            const uint64_t EI = eq16(P16 >> 4, T16) & VT;           // p_{j+1} == t_j (I runs)
-            const uint64_t TZ = nz16(T16) & VT;                     // t_j is a symbol (not '$' / edge)
+            const uint32_t VT = onesR(avail);
+            const uint32_t E0 = eqm(P16, T16) & VT;                 // p_j == t_j     (M chain, S runs)
+            const uint32_t ED = eqm(P16, shr1(T16)) & (VT >> 1);    // p_j == t_{j+1} (D runs)
+            const uint32_t EI = eqm(shr1(P16), T16) & VT;           // p_{j+1} == t_j (I runs)
+            const uint32_t TZ = (T16.b0 | T16.b1 | T16.b2) & VT;    // t_j is a symbol (not '$' / edge)
 
             const bool atLeaf = live && pos == m;
             const bool node = live && pos < m;
@@ -783,29 +798,29 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             // forced run on the way; any other node is expanded alone
             const uint32_t B = forced ? min(run0, 16u)
                                       : (kidsF ? max(1u, min(min(same0, run0 - 1u), 8u)) : 1u);
-            const uint64_t miss = ~E0 & kOnes16;
-            const uint32_t L = mOK ? min(B, miss ? (uint32_t)__builtin_ctzll(miss) >> 2 : 16u) : 0u;
+            const uint32_t miss = ~E0 & kRunMask;
+            const uint32_t L = mOK ? min(B, miss ? (uint32_t)__builtin_ctz(miss) : kRun) : 0u;
 
             // ---- error children of the chain nodes i < NN (node L = the mismatch)
             const uint32_t NN = L < B ? L + 1u : B;
-            const uint64_t nodesM = node && !forced ? ones16(NN) : 0ull;  // leaves / idle lanes: none
-            const uint64_t first = 1ull;  // chain node 0 (= this node)
-            uint64_t Dm = EDIT ? (nodesM & TZ) : 0ull;
+            const uint32_t nodesM = node && !forced ? onesR(NN) : 0u;  // leaves / idle lanes: none
+            const uint32_t first = 1u;  // chain node 0 (= this node)
+            uint32_t Dm = EDIT ? (nodesM & TZ) : 0u;
             if (pos == 0u || side == OP_I) Dm &= ~first;
-            uint64_t Im = EDIT && misOK ? nodesM : 0ull;
+            uint32_t Im = EDIT && misOK ? nodesM : 0u;
             if (side == OP_D) Im &= ~first;
             // S at the first mismatch (not where M is merely disallowed: l > e)
-            bool Sx = node && !forced && L < B && misOK && ((TZ & ~E0) >> (4u * L)) & 1ull;
+            bool Sx = node && !forced && L < B && misOK && ((TZ & ~E0) >> L) & 1u;
             if (kidsF) {
                 // forced runs: D at i needs p[i..] == t[i+1..], I at i needs
                 // p[i+1..] == t[i..], S at L needs p[L+1..] == t[L+1..], each for
                 // min(7, rest of the run) symbols (positions past the run count as matches)
-                Dm &= run7(ED | beyond16(run0));
-                Im &= run7(EI | beyond16(run0 - 1u));
-                Sx = Sx && ((run7(E0 | beyond16(run0)) >> (4u * (L + 1u))) & 1ull);
+                Dm &= run7(ED | beyondR(run0));
+                Im &= run7(EI | beyondR(run0 - 1u));
+                Sx = Sx && ((run7(E0 | beyondR(run0)) >> (L + 1u)) & 1u);
             }
             const bool contM = node && L >= B;  // the match chain continues at pos + B
-            uint32_t nSurv = (uint32_t)__popcll(Dm) + (uint32_t)__popcll(Im) + (Sx ? 1u : 0u);
+            uint32_t nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
             // the lane continues with one child and stacks the others: a
             // surviving error child first, the match chain below it
             uint32_t Bc = B;
@@ -819,7 +834,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 Dm &= first;
                 Im &= first;
                 Sx = Sx && L == 0u;
-                nSurv = (uint32_t)__popcll(Dm) + (uint32_t)__popcll(Im) + (Sx ? 1u : 0u);
+                nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
             }
             const bool contM1 = node && L >= Bc;
             if (node && nSurv && sp + nSurv + (contM1 ? 1u : 0u) - 1u > a.stackCap) {
@@ -860,12 +875,12 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     pend = v;
                     hasPend = true;
                 };
-                for (uint64_t d = Dm; d; d &= d - 1ull) {
-                    const uint32_t i = (uint32_t)__builtin_ctzll(d) >> 2, k = runLen(i);
+                for (uint32_t d = Dm; d; d &= d - 1u) {
+                    const uint32_t i = (uint32_t)__builtin_ctz(d), k = runLen(i);
                     emit(make_uint2(extend(cur.x, i + 1u + k), (pos + i + k) | e1 | metaAt(i, OP_D, k)));
                 }
-                for (uint64_t d = Im; d; d &= d - 1ull) {
-                    const uint32_t i = (uint32_t)__builtin_ctzll(d) >> 2, k = i + 1u < run0 ? runLen(i + 1u) : 0u;
+                for (uint32_t d = Im; d; d &= d - 1u) {
+                    const uint32_t i = (uint32_t)__builtin_ctz(d), k = i + 1u < run0 ? runLen(i + 1u) : 0u;
                     emit(make_uint2(extend(cur.x, i + k), (pos + i + 1u + k) | e1 | metaAt(i, OP_I, k)));
                 }
                 if (Sx) {
@@ -1182,6 +1197,18 @@ __global__ void kDigest(const sahara_hit* __restrict__ h, uint64_t n, unsigned l
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, (unsigned long long)acc);
 }
 
+// Hit records into a caller's device buffer with qids shifted by qidOffset
+// (rank-local -> global qids before a gather across ranks).
+__global__ void kCopyHits(const sahara_hit* __restrict__ h, uint64_t n, uint64_t qidOffset,
+                          sahara_hit* __restrict__ dst) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        sahara_hit r = h[i];
+        r.qid += qidOffset;
+        dst[i] = r;
+    }
+}
+
 // pattern bytes (one symbol per byte) -> 4-bit words, patWords per pattern
 // Also validates the ranks (ivs::verify_rank, search.cpp:118-120): *bad != 0
 // if any is 0 or >= sigma.
@@ -1205,6 +1232,29 @@ __global__ void kPackPatterns(const uint8_t* __restrict__ src, uint64_t npat, ui
         dst[i] = v;
     }
     if (__any(invalid) && (threadIdx.x & 63u) == 0) atomicOr(bad, 1u);
+}
+
+// pattern bytes -> 3-bit-plane blocks of 32 symbols (device_index.h),
+// patBlocks per pattern, zero past m (the text phase's layout)
+__global__ void kPackPatterns3(const uint8_t* __restrict__ src, uint64_t npat, uint32_t m, uint32_t patBlocks,
+                               uint4* __restrict__ dst) {
+    const uint64_t total = npat * patBlocks;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = i / patBlocks;
+        const uint32_t b = (uint32_t)(i - p * patBlocks);
+        uint32_t p0 = 0, p1 = 0, p2 = 0;
+        for (uint32_t j = 0; j < 32; ++j) {
+            const uint32_t q = b * 32 + j;
+            if (q < m) {
+                const uint32_t r = src[p * m + q];
+                p0 |= (r & 1u) << j;
+                p1 |= ((r >> 1) & 1u) << j;
+                p2 |= ((r >> 2) & 1u) << j;
+            }
+        }
+        dst[i] = make_uint4(p0, p1, p2, 0u);
+    }
 }
 
 struct SegOff {  // begin (d = 0) / end (d = 1) of a listed query's segment
@@ -1341,10 +1391,24 @@ void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff,
     SH_HIP(hipGetLastError());
 }
 
+void launchPackPatterns3(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patBlocks, uint4* dst,
+                         hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>((npat * patBlocks + 255) / 256, 65536);
+    hipLaunchKernelGGL(kPackPatterns3, dim3((unsigned)blocks), dim3(256), 0, st, src, npat, m, patBlocks, dst);
+    SH_HIP(hipGetLastError());
+}
+
 void launchDigest(const sahara_hit* h, uint64_t n, unsigned long long* out, hipStream_t st) {
     if (n == 0) return;
     const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
     hipLaunchKernelGGL(kDigest, dim3((unsigned)blocks), dim3(256), 0, st, h, n, out);
+    SH_HIP(hipGetLastError());
+}
+
+void launchCopyHits(const sahara_hit* h, uint64_t n, uint64_t qidOffset, sahara_hit* dst, hipStream_t st) {
+    if (n == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(kCopyHits, dim3((unsigned)blocks), dim3(256), 0, st, h, n, qidOffset, dst);
     SH_HIP(hipGetLastError());
 }
 

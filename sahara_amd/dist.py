@@ -52,6 +52,58 @@ def gather_hits(rows: np.ndarray, qid_offset: int, device="cpu") -> np.ndarray |
     return np.concatenate(out) if out else np.zeros((0, 4), np.uint64)
 
 
+HIT_WORDS = 3  # a sahara_hit record (24 B) as three int64 words
+
+
+def gather_hit_records(n_local: int, fill, device="cpu"):
+    """Gather every rank's hit records to rank 0 in rank order: the hit
+    record gather of SURVEY §8(e), over RCCL (xGMI) on GPUs, gloo on CPU.
+
+    `fill(buf)` writes this rank's n_local records (global qids) into the
+    first rows of `buf`, an int64 tensor (cap, 3) on `device` — on a GPU,
+    BiFMIndex.copy_hits(buf.data_ptr(), cap, qid_offset) does it on the
+    device. One all_gather of the counts (8 B per rank), then one gather of
+    the records padded to the largest count. Returns (parts, counts) on rank
+    0, parts[r] = rank r's records (counts[r], 3); (None, counts) elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    cnt = torch.tensor([int(n_local)], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    cap = max(max(counts), 1)
+    buf = torch.zeros((cap, HIT_WORDS), dtype=torch.int64, device=device)
+    fill(buf)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gather_list=parts, dst=0)
+    if rank != 0:
+        return None, counts
+    return [p[:c] for p, c in zip(parts, counts)], counts
+
+
+def hit_rows_from_records(rec) -> np.ndarray:
+    """(n, 3) int64 sahara_hit records -> (n, 4) u64 rows (qid, seq_id, pos, e)."""
+    a = np.ascontiguousarray(np.asarray(rec, dtype=np.int64)).view(np.uint64).reshape(-1, HIT_WORDS)
+    out = np.empty((len(a), 4), np.uint64)
+    out[:, 0] = a[:, 0]
+    out[:, 1] = a[:, 1] & np.uint64(0xFFFFFFFF)
+    out[:, 2] = a[:, 2]
+    out[:, 3] = a[:, 1] >> np.uint64(32)
+    return out
+
+
+def hit_records_from_rows(rows) -> np.ndarray:
+    """(n, 4) u64 rows (qid, seq_id, pos, e) -> (n, 3) int64 sahara_hit records."""
+    r = np.asarray(rows, dtype=np.uint64).reshape(-1, 4)
+    a = np.empty((len(r), HIT_WORDS), np.uint64)
+    a[:, 0] = r[:, 0]
+    a[:, 1] = (r[:, 1] & np.uint64(0xFFFFFFFF)) | (r[:, 3] << np.uint64(32))
+    a[:, 2] = r[:, 2]
+    return a.view(np.int64)
+
+
 def max_over_ranks(x: float, device="cpu") -> float:
     """The slowest rank's time: the whole job's time (bench contract)."""
     import torch

@@ -163,6 +163,18 @@ def test_no_hits_and_device_resident_path(gpu_device):
     st2 = gpu.stats()
     assert st2["rank_nodes"] < st["rank_nodes"] and st2["conversions"] > 0
     assert np.array_equal(gpu.fetch(), direct)
+    # device-side copy for the cross-GPU hit gather: global qids, same records
+    import torch
+    from sahara_amd.dist import hit_rows_from_records
+    buf = torch.full((len(direct) + 5, 3), -1, dtype=torch.int64, device=f"cuda:{gpu_device}")
+    assert gpu.copy_hits(buf.data_ptr(), buf.shape[0], qid_offset=1000) == len(direct)
+    rows = hit_rows_from_records(buf[: len(direct)].cpu().numpy())
+    want = hits_as_rows(direct).copy()
+    want[:, 0] += np.uint64(1000)
+    assert np.array_equal(rows, want)
+    assert (buf[len(direct):] == -1).all()
+    with pytest.raises(sa.SaharaError):
+        gpu.copy_hits(buf.data_ptr(), len(direct) - 1)
 
 
 def test_errors_are_loud(gpu_device):

@@ -36,10 +36,12 @@ def _with_rc(reads):
 
 def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
     import torch.distributed as dist
 
     import oracle
-    from sahara_amd.dist import gather_hits, max_over_ranks, shard_bounds, sum_over_ranks
+    from sahara_amd.dist import (gather_hit_records, gather_hits, hit_records_from_rows, hit_rows_from_records,
+                                 max_over_ranks, shard_bounds, sum_over_ranks)
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -50,7 +52,19 @@ def _worker(rank, world, port, outdir):
         allh = gather_hits(h, qid_offset=2 * lo)
         total = sum_over_ranks(len(h))
         t = max_over_ranks(float(rank + 1))
+        # the bench's record gather: fill() writes global-qid records into the buffer
+        rows = np.asarray(h, np.uint64).reshape(-1, 4).copy()
+        rows[:, 0] += np.uint64(2 * lo)
+        rec = hit_records_from_rows(rows)
+
+        def fill(buf):
+            buf[: len(rec)] = torch.from_numpy(rec)
+
+        parts, counts = gather_hit_records(len(rec), fill)
+        assert counts[rank] == len(rec)
         if rank == 0:
+            got2 = np.concatenate([hit_rows_from_records(p.numpy()) for p in parts])
+            np.save(os.path.join(outdir, "gathered2.npy"), got2)
             np.save(os.path.join(outdir, "gathered.npy"), allh)
             np.save(os.path.join(outdir, "meta.npy"), np.array([total, t]))
     finally:
@@ -61,6 +75,19 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def test_hit_record_layout_round_trip():
+    import sahara_amd as sa
+    from sahara_amd.dist import hit_records_from_rows, hit_rows_from_records
+    rng = np.random.default_rng(3)
+    rows = np.stack([rng.integers(0, 2**40, 50), rng.integers(0, 2**31, 50), rng.integers(0, 2**33, 50),
+                     rng.integers(0, 4, 50)], 1).astype(np.uint64)
+    rec = hit_records_from_rows(rows)
+    assert np.array_equal(hit_rows_from_records(rec), rows)
+    h = rec.view(sa.HIT_DTYPE).reshape(-1)  # same bytes as the C ABI's sahara_hit
+    assert np.array_equal(h["qid"], rows[:, 0]) and np.array_equal(h["seq_id"], rows[:, 1])
+    assert np.array_equal(h["pos"], rows[:, 2]) and np.array_equal(h["err"], rows[:, 3])
 
 
 def test_shard_bounds_partition():
@@ -79,11 +106,59 @@ def test_two_rank_gather_equals_single_process(world):
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=True, start_method="spawn")
         got = np.load(os.path.join(d, "gathered.npy"))
+        got2 = np.load(os.path.join(d, "gathered2.npy"))
         total, t = np.load(os.path.join(d, "meta.npy"))
     recs, reads = _inputs()
     I = oracle.Index.build(recs, sigma=6)
     want, _ = I.search(_with_rc(reads), oracle.scheme("h2-k2", 0, K, M), edit=True)
     assert len(want) > 0
     assert np.array_equal(hits_as_rows(got), hits_as_rows(want))
+    assert np.array_equal(hits_as_rows(got2), hits_as_rows(want))
     assert int(total) == len(want)
     assert t == float(world)  # max over ranks
+
+
+class _FakeIndex:
+    """Stands in for BiFMIndex.copy_hits on CPU: writes this rank's records
+    (sahara_hit layout, qids shifted) to the destination pointer."""
+
+    def __init__(self, rows):
+        from sahara_amd.dist import hit_records_from_rows
+        self.rec = hit_records_from_rows(rows)
+
+    def copy_hits(self, ptr, cap, qid_offset=0):
+        import ctypes
+        assert cap >= len(self.rec)
+        r = self.rec.copy()
+        r[:, 0] += qid_offset
+        ctypes.memmove(ptr, r.ctypes.data, r.nbytes)
+        return len(r)
+
+
+def _bench_gather_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(100 + rank)
+        n = 37 + 20 * rank  # ragged per-rank counts
+        rows = np.stack([rng.integers(0, 2 * 50, n), rng.integers(0, 24, n), rng.integers(0, 2**33, n),
+                         rng.integers(0, 3, n)], 1).astype(np.uint64)
+        g = bench.gather_step(_FakeIndex(rows), n, 50, world, rank, dist.barrier, dist, torch, device="cpu")
+        if rank == 0:
+            np.save(os.path.join(outdir, "g.npy"), np.array([g["records"], int(g["verified"])]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_gather_step_two_ranks():
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_bench_gather_worker, args=(2, _free_port(), d), nprocs=2, join=True,
+                           start_method="spawn")
+        recs, ok = np.load(os.path.join(d, "g.npy"))
+    assert recs == 37 + 57 and ok == 1
