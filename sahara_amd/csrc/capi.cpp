@@ -365,8 +365,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // the block alignment of its start (31 symbols); 3 words per block
     const uint32_t winBlocks = (c->m + 2 * c->maxErr + 31 + 31) / 32;
     const uint32_t textStack = 2 * c->maxErr + 2;
+    // one-word stack entries where a node fits 30 bits (search.hip packNode)
+    const bool packedStack = c->m <= 127 && winBlocks <= 7 && c->maxErr <= 7 && !std::getenv("SAHARA_WIDE_STACK");
     const size_t textLds = (size_t)2 * c->nsearch * c->m * 4 +
-                           (size_t)256 * (3 * (winBlocks + c->patBlocks) + 2 * textStack) * 4;
+                           (size_t)256 * (3 * (winBlocks + c->patBlocks) + (packedStack ? 1 : 2) * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
@@ -375,7 +377,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
-        tbpc = textBlocksPerCU(sigma, c->edit, textLds);
+        tbpc = textBlocksPerCU(sigma, c->edit, packedStack, textLds);
     if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(tbpc, std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
@@ -525,6 +527,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.counters = c->counters.ptr;
             t.winBlocks = winBlocks;
             t.stackCap = textStack;
+            t.packedStack = packedStack ? 1u : 0u;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
             t.dbg = c->dbg.ptr;

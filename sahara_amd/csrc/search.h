@@ -74,6 +74,7 @@ struct TextArgs {
     unsigned long long* counters;
     uint32_t winBlocks;      // window blocks per lane (32 symbols each)
     uint32_t stackCap;       // text DFS stack entries per lane
+    uint32_t packedStack;    // 1: one-word stack entries (m <= 127, winBlocks <= 7, maxErr <= 7)
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t* dbg;           // 16 words: state of the first lane that violated a bound (or nullptr)
@@ -96,7 +97,7 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
+int textBlocksPerCU(uint32_t sigma, bool edit, bool packedStack, size_t lds);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);

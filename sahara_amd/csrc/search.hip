@@ -535,7 +535,8 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 // equal offsets:
 //   window  (winBlocks blocks of 32 symbols)     W[(3j+b)*256 + t], plane b
 //   pattern (patBlocks blocks of 32 symbols)     P[(3j+b)*256 + t]
-//   stack   (stackCap uint2 entries)            S[d*256 + t]
+//   stack   (stackCap entries)                   S[d*256 + t]: uint2, or one
+//           packed word (PK: m <= 127, window <= 256 symbols, e <= 7)
 //
 // A lane's state is one DFS node `cur` (x = window offsets xo | yo << 16 of
 // the text t matched so far, y = pos | e << 16 | lastL << 20 | lastR << 22).
@@ -633,7 +634,18 @@ __global__ void kResolveTasks(uint4* __restrict__ tasks, const uint32_t* __restr
         tasks[i].x = sa[tasks[i].x];
 }
 
-template <int SIGMA, bool EDIT, bool COUNT>
+// One-word form of a text DFS node (PK): xo, yo (8 bits each) | pos (7) | e (3)
+// | lastL, lastR (2 each). Frees LDS for a fourth workgroup per CU at m = 100.
+__device__ __forceinline__ uint32_t packNode(uint2 v) {
+    return (v.x & 0xFFu) | ((v.x >> 8) & 0xFF00u) | ((v.y & 0x7Fu) << 16) | (((v.y >> 16) & 7u) << 23) |
+           (((v.y >> 20) & 0xFu) << 26);
+}
+__device__ __forceinline__ uint2 unpackNode(uint32_t w) {
+    return make_uint2((w & 0xFFu) | ((w & 0xFF00u) << 8),
+                      ((w >> 16) & 0x7Fu) | (((w >> 23) & 7u) << 16) | (((w >> 26) & 0xFu) << 20));
+}
+
+template <int SIGMA, bool EDIT, bool COUNT, bool PK>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     uint2* SC = reinterpret_cast<uint2*>(lds);
@@ -647,6 +659,12 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint32_t* W = slot + threadIdx.x;
     uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
     uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
+    uint32_t* S1 = slot + 3u * (winBlocks + patBlocks) * 256u + threadIdx.x;
+    auto stackGet = [&](uint32_t d) -> uint2 { return PK ? unpackNode(S1[d * 256u]) : S[d * 256u]; };
+    auto stackPut = [&](uint32_t d, const uint2& v) {
+        if (PK) S1[d * 256u] = packNode(v);
+        else S[d * 256u] = v;
+    };
     const uint32_t winLen = winBlocks * 32u;
     const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
     const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
@@ -755,7 +773,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         uint32_t leafStart = 0, leafE = 0;
         for (uint32_t step = 0; step < a.steps; ++step) {
             const bool pop = !have && !leaf && sp > 0;
-            const uint2 top = S[(pop ? sp - 1u : 0u) * 256u];
+            const uint2 top = stackGet(pop ? sp - 1u : 0u);
             if (pop) { cur = top; --sp; have = true; }
             const bool live = have && !leaf;
             if (!__any(live)) break;  // wave-uniform
@@ -871,7 +889,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 uint2 pend = cM;
                 bool hasPend = contM1;
                 auto emit = [&](const uint2& v) {
-                    if (hasPend) S[min(spw++, a.stackCap - 1u) * 256u] = pend;
+                    if (hasPend) stackPut(min(spw++, a.stackCap - 1u), pend);
                     pend = v;
                     hasPend = true;
                 };
@@ -1276,12 +1294,22 @@ void launchFMT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds
 
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
-    if (edit) {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false>), grid, dim3(256), lds, st, a);
+    if (a.packedStack) {
+        if (edit) {
+            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, true>), grid, dim3(256), lds, st, a);
+            else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, true>), grid, dim3(256), lds, st, a);
+        } else {
+            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, true>), grid, dim3(256), lds, st, a);
+            else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, true>), grid, dim3(256), lds, st, a);
+        }
     } else {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false>), grid, dim3(256), lds, st, a);
+        if (edit) {
+            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, false>), grid, dim3(256), lds, st, a);
+            else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, false>), grid, dim3(256), lds, st, a);
+        } else {
+            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, false>), grid, dim3(256), lds, st, a);
+            else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, false>), grid, dim3(256), lds, st, a);
+        }
     }
 }
 
@@ -1296,11 +1324,16 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     return b < 1 ? 1 : b;
 }
 
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
+int textBlocksPerCU(uint32_t sigma, bool edit, bool packedStack, size_t lds) {
     int b = 0;
     const void* f;
-    if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false> : (const void*)kSearchText<5, false, false>;
-    else            f = edit ? (const void*)kSearchText<6, true, false> : (const void*)kSearchText<6, false, false>;
+    if (packedStack) {
+        if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false, true> : (const void*)kSearchText<5, false, false, true>;
+        else            f = edit ? (const void*)kSearchText<6, true, false, true> : (const void*)kSearchText<6, false, false, true>;
+    } else {
+        if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false, false> : (const void*)kSearchText<5, false, false, false>;
+        else            f = edit ? (const void*)kSearchText<6, true, false, false> : (const void*)kSearchText<6, false, false, false>;
+    }
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b;
 }

@@ -209,9 +209,13 @@ def test_medium_scale_parity(gpu_device, k, m, nreads, ref_len):
     assert found.all()
 
 
-def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch):
+@pytest.mark.parametrize("wide", [False, True])
+def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch, wide):
     """Occurrences that touch position 0, the last symbol of the text and
-    record delimiters: the text-phase windows are clamped there."""
+    record delimiters: the text-phase windows are clamped there. Both text
+    stack forms (one-word packed nodes, and the two-word form of m > 127)."""
+    if wide:
+        monkeypatch.setenv("SAHARA_WIDE_STACK", "1")
     rng = np.random.default_rng(21)
     recs = random_records(rng, [60, 45, 200, 33, 90], 6)
     m = 24

@@ -43,8 +43,9 @@ def states(P, T, sch, edit, limit=300):
     return out
 
 
+@pytest.mark.parametrize("run,chain_len", [(16, 8), (32, 16)])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_chain_step_equals_plain_dfs(seed):
+def test_chain_step_equals_plain_dfs(seed, run, chain_len):
     rng = random.Random(seed)
     checked = 0
     for _ in range(60):
@@ -72,6 +73,6 @@ def test_chain_step_equals_plain_dfs(seed):
         cap = 2 * max(max(u), 1) + 2
         nodes = states(P, T, (pi, l, u, dirs), edit)
         for task in rng.sample(nodes, min(5, len(nodes))):
-            assert chain(P, T, task, (pi, l, u, dirs), edit, cap=cap) == plain(P, T, task, (pi, l, u, dirs), edit)
+            assert chain(P, T, task, (pi, l, u, dirs), edit, cap=cap, RUN=run, CHAIN=chain_len) == plain(P, T, task, (pi, l, u, dirs), edit)
             checked += 1
     assert checked > 100

@@ -2,8 +2,8 @@
 
 Test infrastructure: `chain()` restates, one node at a time and with Python
 sets instead of nibble masks, what a lane of the text kernel does per
-micro-step — forced-run nodes matching up to 16 symbols, chain nodes walking
-up to 8 positions of a match chain and checking every error child's forced
+micro-step — forced-run nodes matching up to RUN symbols, chain nodes walking
+up to CHAIN positions of a match chain and checking every error child's forced
 run, the stack reserve rule — and `plain()` is the textbook DFS of policy P0
 (docs/semantics.md) against the text. tests/test_text_model.py holds the two
 to the same leaf multiset from arbitrary DFS states.
@@ -11,6 +11,8 @@ to the same leaf multiset from arbitrary DFS states.
 import collections
 
 MS, I_, D_ = 1, 2, 3
+RUN = 16    # symbols per micro-step run (kRun in search.hip)
+CHAIN = 8   # chain positions per micro-step of a node whose error children are forced
 
 def sides(pos, right, lastL, lastR, op):
     if pos == 0: return op, op
@@ -53,7 +55,7 @@ def tables(sch):
         run[p], same[p] = k, s
     return run, same
 
-def chain(P, T, task, sch, edit, cap=100):
+def chain(P, T, task, sch, edit, cap=100, RUN=RUN, CHAIN=CHAIN):
     pi, l, u, dirs = sch
     m = len(pi)
     run, same = tables(sch)
@@ -68,17 +70,19 @@ def chain(P, T, task, sch, edit, cap=100):
         # chain-order sequences
         def pj(j):
             qq = q0 + j if r0 else q0 - j
-            return P[qq] if 0 <= qq < len(P) else 99  # garbage beyond pattern
+            # beyond the pattern the kernel reads whatever precedes / follows it in
+            # LDS: arbitrary symbols, which the chain logic must never use
+            return P[qq] if 0 <= qq < len(P) else (qq * 7 + 3) % 6
         def tj(j):
             tt = ye + j if r0 else xs - 1 - j
             return T[tt] if 0 <= tt < len(T) else 0
-        E0 = {j for j in range(16) if pj(j) == tj(j)}
-        ED = {j for j in range(16) if pj(j) == tj(j+1)}
-        EI = {j for j in range(16) if pj(j+1) == tj(j)}
-        TZ = {j for j in range(16) if tj(j) != 0}
+        E0 = {j for j in range(RUN) if pj(j) == tj(j)}
+        ED = {j for j in range(RUN) if pj(j) == tj(j+1)}
+        EI = {j for j in range(RUN) if pj(j+1) == tj(j)}
+        TZ = {j for j in range(RUN) if tj(j) != 0}
         forced = e == ub0; kidsF = e + 1 == ub0
         mOK = lb0 <= e <= ub0; misOK = lb0 <= e+1 <= ub0
-        B = min(run0, 16) if forced else (max(1, min(same0, run0-1, 8)) if kidsF else 1)
+        B = min(run0, RUN) if forced else (max(1, min(same0, run0-1, CHAIN)) if kidsF else 1)
         L = 0
         if mOK:
             while L < B and L in E0: L += 1
@@ -90,7 +94,7 @@ def chain(P, T, task, sch, edit, cap=100):
         if side == D_: Im.discard(0)
         Sx = (not forced) and L < B and misOK and (L in TZ) and (L not in E0)
         def run7(S, beyond):
-            return {j for j in range(16) if all((jj in S) or jj >= beyond for jj in range(j, j+7))}
+            return {j for j in range(RUN) if all((jj in S) or jj >= beyond for jj in range(j, j+7))}
         if kidsF:
             Dm &= run7(ED, run0)
             Im &= run7(EI, run0 - 1)
