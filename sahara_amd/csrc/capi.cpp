@@ -342,15 +342,15 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
     int bpc = fullBpc;
     // Overlapped with the text phase of the previous batch, the FM phase
-    // (memory-latency bound) runs with two workgroups per CU and leaves the
-    // CUs' other issue slots to the text phase (ALU bound); alone it takes
-    // them all. (Measured at C3: 1 WG/CU 24.0 ms/step, 2: 19.5, 3: 20.4, 4: 20.9.)
+    // (memory-latency bound, and short with a depth-16 k-mer table) runs one
+    // workgroup per CU, which fits in the LDS beside three text workgroups;
+    // alone it takes them all. (Measured at C3: 1 WG/CU 15.2 ms/step, 2: 15.8.)
     // patterns per batch: 4M, fewer for schemes with many searches (work
     // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (const char* e = std::getenv("SAHARA_BATCH")) maxBatch = std::max<uint64_t>(1, std::min<uint64_t>(maxBatch, std::atoll(e)));
     const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
-    if (!serial && batchesHere > 1 && c->verify) bpc = std::min(2, fullBpc);
+    if (!serial && batchesHere > 1 && c->verify) bpc = 1;
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     // the first batch's FM phase has nothing to overlap with: full occupancy
@@ -366,8 +366,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const uint32_t winBlocks = (c->m + 2 * c->maxErr + 31 + 31) / 32;
     const uint32_t textStack = 2 * c->maxErr + 2;
     // one-word stack entries where a node fits 30 bits (search.hip packNode)
-    const bool packedStack = c->m <= 127 && winBlocks <= 7 && c->maxErr <= 7 && !std::getenv("SAHARA_WIDE_STACK");
-    const size_t textLds = (size_t)2 * c->nsearch * c->m * 4 +
+    // (SAHARA_PACKED_STACK; off by default: at m = 100 it buys a fourth text
+    // workgroup per CU, but costs a pack / unpack per micro-step, and three
+    // workgroups leave LDS for an FM workgroup beside them)
+    const bool packedStack = c->m <= 127 && winBlocks <= 7 && c->maxErr <= 7 && std::getenv("SAHARA_PACKED_STACK") &&
+                             std::atoi(std::getenv("SAHARA_PACKED_STACK")) != 0;
+    const uint32_t tableWords = std::max<uint32_t>(2 * c->nsearch * c->m, kTextTableMin);
+    const size_t textLds = (size_t)tableWords * 4 +
                            (size_t)256 * (3 * (winBlocks + c->patBlocks) + (packedStack ? 1 : 2) * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
@@ -380,6 +385,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         tbpc = textBlocksPerCU(sigma, c->edit, packedStack, textLds);
     if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(tbpc, std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
+    // where a task's SA row becomes its text position: 2 = inside the text
+    // kernel, a chunk of task records ahead (default: no pass between the FM
+    // and text phases); 1 = kResolveTasks after the FM phase on its stream;
+    // 0 = kResolveTasks before the text phase (SAHARA_RESOLVE)
+    uint32_t fmPrio = 0;
+    if (const char* e = std::getenv("SAHARA_FM_PRIO")) fmPrio = (uint32_t)std::max(0, std::min(3, std::atoi(e)));
+    int resolveMode = 2;
+    if (const char* e = std::getenv("SAHARA_RESOLVE")) resolveMode = std::max(0, std::min(2, std::atoi(e)));
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -473,6 +486,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.tasks = sl.tasks.ptr;
         a.taskCap = c->taskCap;
         a.split = split;
+        a.prio = serial ? 0u : fmPrio;
         // starting cursors; reference execution (verify off) ranks every node
         // from the root, so it does not use the k-mer table
         SeedArgs sd{};
@@ -496,6 +510,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sA);
         SH_HIP(hipEventRecord(sl.seedDone, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 ? firstBlocks : blocks, lds, sA);
+        if (split && resolveMode == 1)
+            launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sA);
         SH_HIP(hipEventRecord(sl.fmDone, sA));
         ++S.search_launches;
     };
@@ -528,10 +544,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.winBlocks = winBlocks;
             t.stackCap = textStack;
             t.packedStack = packedStack ? 1u : 0u;
+            t.tableWords = tableWords;
+            t.resolveRows = resolveMode == 2 ? 1u : 0u;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
             t.dbg = c->dbg.ptr;
-            launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
+            if (resolveMode == 0)
+                launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));

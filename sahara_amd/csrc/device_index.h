@@ -84,9 +84,10 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec,
                     uint32_t rate, const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits,
                     const uint32_t* samples, uint64_t nsamples, hipStream_t st);
-// depth of the k-mer table for a text of n symbols: floor(log4 n) - 2 (the
-// mean interval then still holds ~16-64 rows), at most 14 (4.3 GB);
-// SAHARA_KMER overrides (0 = no table)
+// depth of the k-mer table for a text of n symbols: floor(log4 n) + 1, at
+// most 16 (a 68.7 GB table at 3 Gbp, where the mean 16-mer occurs 0.7 times:
+// most exact first parts of a search then start as a text task), and at most
+// what fits in half of the free HBM; SAHARA_KMER overrides (0 = no table)
 uint32_t kmerDepth(uint64_t n);
 void buildKmerTable(DeviceIndex& I, uint32_t K, hipStream_t st);
 void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits,

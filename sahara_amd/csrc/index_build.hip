@@ -546,9 +546,15 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
 uint32_t kmerDepth(uint64_t n) {
     uint32_t lg = 0;
     while (lg < 31 && (1ull << (2 * (lg + 1))) <= n) ++lg;  // floor(log4 n)
-    int k = (int)lg - 2;
+    int k = (int)lg + 1;
     if (const char* e = std::getenv("SAHARA_KMER")) k = std::atoi(e);
-    return (uint32_t)std::max(0, std::min(k, 14));
+    k = std::max(0, std::min(k, 16));
+    // the table (16 B x 4^K) and its build levels (2 x 16 B x 4^(K-1)) take at
+    // most half of the free HBM
+    size_t freeB = 0, totalB = 0;
+    if (hipMemGetInfo(&freeB, &totalB) == hipSuccess)
+        while (k > 0 && (16ull << (2 * k)) + (32ull << (2 * (k - 1))) > freeB / 2) --k;
+    return (uint32_t)k;
 }
 
 void buildKmerTable(DeviceIndex& I, uint32_t K, hipStream_t st) {

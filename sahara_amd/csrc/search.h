@@ -36,6 +36,7 @@ struct SearchArgs {
     uint32_t taskCap;
     uint32_t* taskCount;
     uint32_t split;          // intervals of <= split rows go to the text phase (0: never)
+    uint32_t prio;           // wave priority (s_setprio 0..3) when overlapped with the text phase
 };
 
 struct SeedArgs {
@@ -52,8 +53,13 @@ struct SeedArgs {
     uint32_t* seedCount;
 };
 
+// Text phase LDS: the scheme table comes first and takes at least one block of
+// lane words (3 planes x 256 lanes), so that a read of a lane's window block -1
+// (left reads near the window start) stays inside the workgroup's LDS.
+constexpr uint32_t kTextTableMin = 3u * 256u;
+
 struct TextArgs {
-    const uint32_t* sa;      // full SA (tasks arrive resolved by launchResolveTasks)
+    const uint32_t* sa;      // full SA (resolveRows; else tasks arrive resolved by launchResolveTasks)
     const uint4* text3;      // text as 3-bit-plane blocks of 32 symbols (device_index.h)
     const uint4* pats3;      // patterns as 3-bit-plane blocks, patBlocks per pattern
     uint32_t patBlocks;
@@ -75,6 +81,8 @@ struct TextArgs {
     uint32_t winBlocks;      // window blocks per lane (32 symbols each)
     uint32_t stackCap;       // text DFS stack entries per lane
     uint32_t packedStack;    // 1: one-word stack entries (m <= 127, winBlocks <= 7, maxErr <= 7)
+    uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)
+    uint32_t resolveRows;    // 1: task records carry SA rows; the kernel reads their text positions
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t* dbg;           // 16 words: state of the first lane that violated a bound (or nullptr)

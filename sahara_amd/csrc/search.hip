@@ -252,7 +252,7 @@ __device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& kee
                 code = code * 4u + ((SIGMA == 6 && c == 5u) ? 3u : c - 1u);
             }
             if (acgt) {
-                const uint4 t = a.kmer[code & ((1u << (2u * a.kmerK)) - 1u)];
+                const uint4 t = a.kmer[(uint32_t)(code & ((1ull << (2u * a.kmerK)) - 1ull))];
                 cur = make_uint4(t.x, t.y, t.z, packMeta(a.kmerK, 0u, OP_MS, OP_MS));
                 keep = t.z != 0u;
             }
@@ -308,6 +308,14 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
 template <int SIGMA, bool EDIT, bool COUNT>
 __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     extern __shared__ uint32_t sch[];
+    // Overlapped with the text phase, this latency-bound kernel's few
+    // instructions go first: the text phase (issue-bound) fills the rest.
+    switch (a.prio) {  // s_setprio takes an immediate
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        default: break;
+    }
     for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) sch[i] = a.scheme[i];
     __syncthreads();
 
@@ -570,24 +578,27 @@ __device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
 }
 __device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
 // 32 symbols from offset o of a lane's interleaved plane array (block i, plane
-// b at word (3i + b) * 256). Reads may run past the array into the lane's
-// next region; callers mask.
-__device__ __forceinline__ uint32_t read32(const uint32_t* A, uint32_t o, uint32_t b) {
-    const uint32_t i = o >> 5;
-    return __builtin_amdgcn_alignbit(A[(3u * i + 3u + b) * 256u], A[(3u * i + b) * 256u], o & 31u);
+// b at word (3i + b) * 256). o may be negative (down to -32): reads may run
+// past either end of the array into the lane's neighbouring LDS regions; callers
+// mask.
+__device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b) {
+    const int i = o >> 5;
+    return __builtin_amdgcn_alignbit(A[(3 * i + 3 + (int)b) * 256], A[(3 * i + (int)b) * 256], (uint32_t)o & 31u);
 }
 // 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
-// reversed (back: bit j = symbol o - 1 - j, 0 before the array start)
+// reversed (back: bit j = symbol o - 1 - j). Symbols outside the array are
+// whatever the LDS holds there (the window's block -1 is the table region,
+// kTextTableMin words, the pattern's is the window): the window's are masked
+// by its `avail`, the pattern's lie beyond the pattern, which the chain logic
+// never uses (tests/text_model.py reads arbitrary symbols there).
 __device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
-    const uint32_t off = fwd ? o : (o >= 32u ? o - 32u : 0u);
-    const uint32_t sh = fwd || o >= 32u ? 0u : 32u - o;
+    const int off = (int)o - (fwd ? 0 : 32);
     Planes r;
     uint32_t v[3];
 #pragma unroll
     for (uint32_t b = 0; b < 3; ++b) {
         const uint32_t w = read32(A, off, b);
-        const uint32_t ws = sh >= 32u ? 0u : w << sh;
-        v[b] = fwd ? w : __builtin_bitreverse32(ws);
+        v[b] = fwd ? w : __builtin_bitreverse32(w);
     }
     r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
     return r;
@@ -649,7 +660,7 @@ template <int SIGMA, bool EDIT, bool COUNT, bool PK>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     uint2* SC = reinterpret_cast<uint2*>(lds);
-    uint32_t* slot = lds + 2u * a.nsearch * a.m;
+    uint32_t* slot = lds + a.tableWords;  // >= kTextTableMin: the window's block -1 stays in LDS
     for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = a.table[i];
     __syncthreads();
 
@@ -680,6 +691,17 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
     uint32_t nBase = 0, nEnd = 0, qBase = 0;
     bool haveNext = false;
+    // resolveRows: the prefetched chunk's records still hold SA rows. Their
+    // text positions are read at the next refill, beside its window loads (one
+    // round trip for both), or at the latest when the chunk becomes current.
+    bool nextRaw = false;
+    const bool resolve = a.resolveRows != 0u;
+    auto resolveNext = [&]() {
+        if (nextRaw) {  // wave-uniform
+            if (nBase + lane < nEnd) nextRec.x = a.sa[nextRec.x];
+            nextRaw = false;
+        }
+    };
     StripedQueue queue(a.work, ntasks);
     {
         uint32_t b = 0, e = 0;
@@ -688,6 +710,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             nEnd = e;
             if (b + lane < e) nextRec = a.tasks[b + lane];
             haveNext = true;
+            nextRaw = resolve;
         } else {
             qDone = true;
         }
@@ -708,10 +731,12 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
         const bool need = refill && idle;
         uint64_t pending = refill ? idleMask : 0ull;
+        if (pending) resolveNext();
         while (pending) {  // wave-uniform
             if (qNext >= qEnd) {
                 // switch to the prefetched chunk, prefetch the one after it
                 if (!haveNext) break;
+                resolveNext();
                 qBase = nBase;
                 qNext = nBase;
                 qEnd = nEnd;
@@ -726,6 +751,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                         nEnd = e;
                         if (b + lane < e) nextRec = a.tasks[b + lane];
                         haveNext = true;
+                        nextRaw = resolve;
                     }
                 }
                 if (qNext >= qEnd) continue;
@@ -738,9 +764,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
                                        __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
             if (mine) {
-                // ---- start a task (x = its text position, resolved by
-                // kResolveTasks): copy the pattern and the text window its
-                // subtree can reach
+                // ---- start a task (x = its text position): copy the pattern
+                // and the text window its subtree can reach
                 const uint32_t x = t.x;
                 pid = t.z;
                 sBase = (t.w >> 24) * m;
@@ -866,44 +891,39 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
 
             // ---- children as stack entries (x = span, y = meta)
             auto extend = [&](uint32_t span, uint32_t k) -> uint32_t { return r0 ? span + (k << 16) : span - k; };
-            // side memory after i chain matches, then op at chain node i, then
-            // k forced matches; pos 0 operations set both sides
+            // side memory of a child: its extension side holds the operation,
+            // or MS once k forced matches follow it; the other side keeps its
+            // memory, except at pos 0, where the first operation sets both (for
+            // chain node i > 0 that was a match)
+            const uint32_t lastOther = r0 ? lastL : lastR;
             auto metaAt = [&](uint32_t i, uint32_t op, uint32_t k) -> uint32_t {
-                uint32_t ml = lastL, mr = lastR;
-                if (i > 0u) {
-                    if (pos == 0u) ml = mr = OP_MS;
-                    else if (r0) mr = OP_MS;
-                    else ml = OP_MS;
-                }
-                if (pos + i == 0u) ml = mr = op;
-                else if (r0) mr = op;
-                else ml = op;
-                if (k) { if (r0) mr = OP_MS; else ml = OP_MS; }
-                return (ml << 20) | (mr << 22);
+                const uint32_t mine = k ? (uint32_t)OP_MS : op;
+                const uint32_t other = pos ? lastOther : (i ? (uint32_t)OP_MS : op);
+                return r0 ? (other << 20) | (mine << 22) : (mine << 20) | (other << 22);
             };
             const uint32_t e1 = (e + 1u) << 16;
             auto runLen = [&](uint32_t i) -> uint32_t { return kidsF ? min(run0 - i, 7u) : 0u; };
             const uint2 cM = make_uint2(extend(cur.x, Bc), (pos + Bc) | (e << 16) | metaAt(Bc, OP_MS, 0u));
-            if (nSurv) {  // rare: the surviving error children; the last one stays in registers
+            if (nSurv) {  // the surviving error children; the last one stays in registers
                 uint32_t spw = sp;
                 uint2 pend = cM;
                 bool hasPend = contM1;
-                auto emit = [&](const uint2& v) {
+                // one loop over all of them — D at chain node i (bit i), I at i
+                // (bit 16 + i), S at L (bit 32 + L), in that order — so the wave
+                // runs max(nSurv) iterations rather than one loop per kind
+                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << 16) | (Sx ? 1ull << (32u + L) : 0ull);
+                while (sv) {
+                    const uint32_t j = (uint32_t)__builtin_ctzll(sv);
+                    sv &= sv - 1ull;
+                    const uint32_t kind = j >> 4, i = j & 15u;  // 0 D, 1 I, 2 S
+                    const uint32_t ii = i + (kind ? 1u : 0u);   // chain node where its forced run starts
+                    const uint32_t k = ii < run0 ? runLen(ii) : 0u;
+                    const uint32_t op = kind == 0u ? (uint32_t)OP_D : (kind == 1u ? (uint32_t)OP_I : (uint32_t)OP_MS);
+                    const uint2 v = make_uint2(extend(cur.x, i + k + (kind == 1u ? 0u : 1u)),
+                                               (pos + ii + k) | e1 | metaAt(i, op, k));
                     if (hasPend) stackPut(min(spw++, a.stackCap - 1u), pend);
                     pend = v;
                     hasPend = true;
-                };
-                for (uint32_t d = Dm; d; d &= d - 1u) {
-                    const uint32_t i = (uint32_t)__builtin_ctz(d), k = runLen(i);
-                    emit(make_uint2(extend(cur.x, i + 1u + k), (pos + i + k) | e1 | metaAt(i, OP_D, k)));
-                }
-                for (uint32_t d = Im; d; d &= d - 1u) {
-                    const uint32_t i = (uint32_t)__builtin_ctz(d), k = i + 1u < run0 ? runLen(i + 1u) : 0u;
-                    emit(make_uint2(extend(cur.x, i + k), (pos + i + 1u + k) | e1 | metaAt(i, OP_I, k)));
-                }
-                if (Sx) {
-                    const uint32_t k = L + 1u < run0 ? runLen(L + 1u) : 0u;
-                    emit(make_uint2(extend(cur.x, L + 1u + k), (pos + L + 1u + k) | e1 | metaAt(L, OP_MS, k)));
                 }
                 sp = min(spw, a.stackCap);
                 cur = pend;

@@ -214,8 +214,7 @@ def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch, wide)
     """Occurrences that touch position 0, the last symbol of the text and
     record delimiters: the text-phase windows are clamped there. Both text
     stack forms (one-word packed nodes, and the two-word form of m > 127)."""
-    if wide:
-        monkeypatch.setenv("SAHARA_WIDE_STACK", "1")
+    monkeypatch.setenv("SAHARA_PACKED_STACK", "0" if wide else "1")
     rng = np.random.default_rng(21)
     recs = random_records(rng, [60, 45, 200, 33, 90], 6)
     m = 24
@@ -239,13 +238,16 @@ def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch, wide)
             assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (k, verify, locate_sa)
 
 
-@pytest.mark.parametrize("batch", ["97", "1000000"])
-def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch):
+@pytest.mark.parametrize("batch,resolve", [("97", "2"), ("97", "1"), ("97", "0"), ("1000000", "2")])
+def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch, resolve):
     """Per-query segments of every length: reads from a 40-fold repeated unit
     have > 8 located rows (segmented radix sort), unique reads 1-2 (register
     sort), random reads none. SAHARA_BATCH=97 runs many batches through the
-    three-stream pipeline, with the per-query counters reused between them."""
+    three-stream pipeline, with the per-query counters reused between them.
+    SAHARA_RESOLVE: text tasks' SA rows resolved inside the text kernel (2) or
+    by kResolveTasks on the FM stream (1) / the text stream (0)."""
     monkeypatch.setenv("SAHARA_BATCH", batch)
+    monkeypatch.setenv("SAHARA_RESOLVE", resolve)
     rng = np.random.default_rng(5)
     unit = random_records(rng, [400], 6)[0]
     parts = []
