@@ -180,10 +180,18 @@ def main():
     reads_per_s = nreads * world * args.steps / elapsed
 
     # instrumented run (untimed): deterministic work counters -> algorithmic bytes
-    cnt = None
+    cnt = ref_cnt = None
     if not args.no_count:
         idx.run(count=True)
         cnt = idx.stats()
+        # SURVEY §8(d) B_read: the reference algorithm's bytes per read, counted
+        # in the reference-execution mode (every node ranked from the root, LF
+        # locate to the rate-16 samples), whose counters equal the CPU
+        # restatement's (tests/test_gpu_parity.py::test_no_hits_and_device_resident_path)
+        idx.set_mode(verify=False, locate_sa=False)
+        idx.run(count=True)
+        ref_cnt = idx.stats()
+        idx.set_mode(verify=True, locate_sa=True)
     search_ms_step = search_ms / args.steps
     roofline = None
     extra = {}
@@ -202,11 +210,26 @@ def main():
                 "kSearchText": {"ms": round(text_ms_step, 2), "bytes": text_bytes,
                                 "GBs": round(text_bytes / max(text_ms_step, 1e-6) * 1e3 / 1e9, 1)}}
         dom = max(kern, key=lambda n: kern[n]["ms"])
-        achieved = kern[dom]["GBs"]
         per_launch = max(1, launches // args.steps)  # one FM and one text launch per batch
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "algorithmic_bytes_per_launch": round(kern[dom]["bytes"] / per_launch)}
+        reads_per_launch = nreads / per_launch
+        launch_ms = kern[dom]["ms"] / per_launch
+        # B_read (§8(d)): 64 B per Occ line the reference's DFS ranks and per
+        # located row (LF steps + the SA-sample line), plus the 2L query bytes
+        b_read = (64.0 * (ref_cnt["ext_lines"] + ref_cnt["lf_steps"] + ref_cnt["hits"]) + pats.size) / nreads
+        achieved = b_read * reads_per_launch / (launch_ms / 1e3) / 1e9
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "bytes_per_unit": round(b_read, 1), "unit_of_work": "read",
+                    "units_per_launch": round(reads_per_launch), "launch_ms": round(launch_ms, 3),
+                    "algorithmic_bytes_per_launch": round(b_read * reads_per_launch),
+                    "basis": "SURVEY 8(d) B_read (the reference algorithm's Occ / LF / SA-sample lines + query "
+                             "bytes per read, counted in the reference-execution mode) x reads per launch / the "
+                             "dominant kernel's launch time",
+                    "whole_job_GBs": round(b_read * reads_per_s / 1e9, 1),
+                    "own_path": {"bytes_per_launch": round(kern[dom]["bytes"] / per_launch),
+                                 "achieved": kern[dom]["GBs"], "frac": round(kern[dom]["GBs"] / HBM_PEAK_GBS, 4),
+                                 "note": "bytes this build's kernel itself reads (window, pattern, task, SA entry "
+                                         "per text task; Occ lines + query bytes for FM)"}}
         tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tj):
             tr = json.load(open(tj)).get(dom)
@@ -237,6 +260,10 @@ def main():
                  "sort_ms": round(sort_ms / args.steps, 2), "seed_ms": round(seed_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
                  "search_grid": cnt["search_grid"], "text_grid": cnt["text_grid"],
                  "pipelined": bool(cnt["pipelined"]),
+                 "reference_algorithm": {"ext_lines_per_read": round(ref_cnt["ext_lines"] / nreads, 1),
+                                         "lf_steps_per_read": round(ref_cnt["lf_steps"] / nreads, 2),
+                                         "rows_per_read": round(ref_cnt["hits"] / nreads, 3),
+                                         "same_hits": ref_cnt["hits"] == cnt["hits"]},
                  }
 
     # PCIe-inclusive rate (SURVEY §8(d)'s definition; not `value`): host ranks

@@ -503,6 +503,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sd.seeds = c->seeds.ptr;
         sd.seedItem = c->seedItem.ptr;
         sd.seedCount = sl.small.ptr + 6;
+        sd.m = c->m;
+        const char* seedTasks = std::getenv("SAHARA_SEED_TASKS");  // 0: every seed goes through the FM kernel
+        sd.toText = split >= 1 && (!seedTasks || std::atoi(seedTasks) != 0) ? 1u : 0u;
+        sd.tasks = sl.tasks.ptr;
+        sd.taskCap = c->taskCap;
+        sd.taskCount = sl.small.ptr + 4;
+        sd.flags = sl.small.ptr + 2;
+        sd.counters = count ? c->counters.ptr : nullptr;
         a.seeds = c->seeds.ptr;
         a.seedItem = c->seedItem.ptr;
         a.seedCount = sl.small.ptr + 6;

@@ -51,6 +51,15 @@ struct SeedArgs {
     uint4* seeds;
     uint32_t* seedItem;
     uint32_t* seedCount;
+    // a seed whose k-mer occurs once is already a text task: written straight
+    // to the task list (the FM kernel's record format) instead of the seeds
+    uint32_t m;
+    uint32_t toText;            // 1: convert single-row seeds (the text phase runs, split >= 1)
+    uint4* tasks;
+    uint32_t taskCap;
+    uint32_t* taskCount;
+    uint32_t* flags;            // 8: task buffer too small
+    unsigned long long* counters;  // count mode: text tasks (+6), else nullptr
 };
 
 // Text phase LDS: the scheme table comes first and takes at least one block of

@@ -263,44 +263,66 @@ __device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& kee
 
 // Each block takes 1024 consecutive items per round (4 per thread, so four
 // table lookups are in flight per lane) and appends the survivors with one
-// atomic per round.
+// atomic per round and output list: seeds for the FM kernel, and text tasks
+// for seeds whose k-mer occurs exactly once (toText) — the node the FM kernel
+// would hand to the text phase at once.
 template <int SIGMA>
 __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
-    __shared__ uint32_t wcount[4], blockBase;
+    __shared__ uint32_t wcount[2][4], blockBase[2];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t ltMask = (1ull << lane) - 1ull;
+    uint64_t cTasks = 0;
     for (uint32_t base = blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
         uint4 cur[4];
-        bool keep[4];
+        bool keep[4], task[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k]);
-        uint64_t m[4];
-        uint32_t wsum = 0;
+        for (int k = 0; k < 4; ++k) {
+            cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k]);
+            task[k] = keep[k] && a.toText && cur[k].z == 1u && (cur[k].w & 0xFFFFu) < a.m;
+            keep[k] = keep[k] && !task[k];
+        }
+        uint64_t m[4], mt[4];
+        uint32_t wsum = 0, wtask = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             m[k] = __ballot(keep[k]);
+            mt[k] = __ballot(task[k]);
             wsum += (uint32_t)__popcll(m[k]);
+            wtask += (uint32_t)__popcll(mt[k]);
         }
-        if (lane == 0) wcount[w] = wsum;
+        if (lane == 0) { wcount[0][w] = wsum; wcount[1][w] = wtask; }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
-            blockBase = tot ? atomicAdd(a.seedCount, tot) : 0u;
+        if (threadIdx.x < 2) {
+            const uint32_t* wc = wcount[threadIdx.x];
+            const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
+            blockBase[threadIdx.x] = tot ? atomicAdd(threadIdx.x ? a.taskCount : a.seedCount, tot) : 0u;
         }
         __syncthreads();
-        uint32_t slot = blockBase;
-        for (uint32_t j = 0; j < w; ++j) slot += wcount[j];
+        uint32_t slot = blockBase[0], tslot = blockBase[1];
+        for (uint32_t j = 0; j < w; ++j) { slot += wcount[0][j]; tslot += wcount[1][j]; }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t at = slot + (uint32_t)__popcll(m[k] & ltMask);
+            const uint32_t item = base + k * 256u + threadIdx.x;
             if (keep[k]) {
+                const uint32_t at = slot + (uint32_t)__popcll(m[k] & ltMask);
                 a.seeds[at] = cur[k];
-                a.seedItem[at] = base + k * 256u + threadIdx.x;
+                a.seedItem[at] = item;
+            }
+            if (task[k]) {  // (row, |t| = kmerK, pattern, node meta | search << 24)
+                const uint32_t at = tslot + (uint32_t)__popcll(mt[k] & ltMask);
+                const uint32_t pid = item / a.nsearch, sIdx = item - pid * a.nsearch;
+                if (at < a.taskCap)
+                    a.tasks[at] = make_uint4(cur[k].x, cur[k].w & 0xFFFFu, pid, (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
+                else
+                    atomicOr(a.flags, 8u);
+                ++cTasks;
             }
             slot += (uint32_t)__popcll(m[k]);
+            tslot += (uint32_t)__popcll(mt[k]);
         }
         __syncthreads();  // wcount / blockBase reused next round
     }
+    if (a.counters && cTasks) atomicAdd(a.counters + 6, (unsigned long long)cTasks);
 }
 
 // =========================================================== phase 1: FM ====
@@ -763,7 +785,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t srcLane = (qNext - qBase + rank) & 63u;
             const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
                                        __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
-            if (mine) {
+            if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
                 // ---- start a task (x = its text position): copy the pattern
                 // and the text window its subtree can reach
                 const uint32_t x = t.x;
