@@ -583,8 +583,12 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 // ---- runs of symbols as bit masks: bit j = chain symbol j. Symbols come as
 // 3 bit planes (device_index.h), so the per-symbol equality of 32 symbols is
 // three word xors; the chain logic uses the low 16 bits.
-constexpr uint32_t kRun = 16;              // symbols per micro-step run
-constexpr uint32_t kRunMask = 0xFFFFu;
+constexpr uint32_t kRun = 32;              // symbols per micro-step run (a forced node's match budget)
+constexpr uint32_t kRunMask = 0xFFFFFFFFu;
+// chain positions per micro-step of a node whose error children are forced:
+// the forced-run check of an error child at chain node i reads symbols
+// i .. i + 7 of the 32 (kChain + 7 <= kRun)
+constexpr uint32_t kChain = 25;
 __device__ __forceinline__ uint32_t onesR(uint32_t n) {  // symbols [0, n), capped at kRun
     return n >= kRun ? kRunMask : (1u << n) - 1u;
 }
@@ -857,12 +861,12 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const bool mOK = lb0 <= e && e <= ub0;
             const bool misOK = lb0 <= e + 1u && e + 1u <= ub0;
             const uint32_t side = r0 ? lastR : lastL;
-            // chain budget: a forced node matches up to 16 symbols; a node whose
-            // error children are forced walks up to 8 positions of its match
-            // chain (same direction, l and u), checking every error child's
-            // forced run on the way; any other node is expanded alone
-            const uint32_t B = forced ? min(run0, 16u)
-                                      : (kidsF ? max(1u, min(min(same0, run0 - 1u), 8u)) : 1u);
+            // chain budget: a forced node matches up to kRun symbols; a node
+            // whose error children are forced walks up to kChain positions of
+            // its match chain (same direction, l and u), checking every error
+            // child's forced run on the way; any other node is expanded alone
+            const uint32_t B = forced ? min(run0, kRun)
+                                      : (kidsF ? max(1u, min(min(same0, run0 - 1u), kChain)) : 1u);
             const uint32_t miss = ~E0 & kRunMask;
             const uint32_t L = mOK ? min(B, miss ? (uint32_t)__builtin_ctz(miss) : kRun) : 0u;
 
@@ -931,13 +935,14 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 uint2 pend = cM;
                 bool hasPend = contM1;
                 // one loop over all of them — D at chain node i (bit i), I at i
-                // (bit 16 + i), S at L (bit 32 + L), in that order — so the wave
-                // runs max(nSurv) iterations rather than one loop per kind
-                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << 16) | (Sx ? 1ull << (32u + L) : 0ull);
+                // (bit kChain + i), S at L (bit 2 kChain), in that order — so
+                // the wave runs max(nSurv) iterations rather than one loop per kind
+                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << kChain) | (Sx ? 1ull << (2u * kChain) : 0ull);
                 while (sv) {
                     const uint32_t j = (uint32_t)__builtin_ctzll(sv);
                     sv &= sv - 1ull;
-                    const uint32_t kind = j >> 4, i = j & 15u;  // 0 D, 1 I, 2 S
+                    const uint32_t kind = j < kChain ? 0u : (j < 2u * kChain ? 1u : 2u);  // 0 D, 1 I, 2 S
+                    const uint32_t i = kind == 0u ? j : (kind == 1u ? j - kChain : L);
                     const uint32_t ii = i + (kind ? 1u : 0u);   // chain node where its forced run starts
                     const uint32_t k = ii < run0 ? runLen(ii) : 0u;
                     const uint32_t op = kind == 0u ? (uint32_t)OP_D : (kind == 1u ? (uint32_t)OP_I : (uint32_t)OP_MS);

@@ -43,7 +43,7 @@ def states(P, T, sch, edit, limit=300):
     return out
 
 
-@pytest.mark.parametrize("run,chain_len", [(16, 8), (32, 16)])
+@pytest.mark.parametrize("run,chain_len", [(16, 8), (32, 16), (32, 25)])
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_chain_step_equals_plain_dfs(seed, run, chain_len):
     rng = random.Random(seed)

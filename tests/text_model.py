@@ -11,8 +11,8 @@ to the same leaf multiset from arbitrary DFS states.
 import collections
 
 MS, I_, D_ = 1, 2, 3
-RUN = 16    # symbols per micro-step run (kRun in search.hip)
-CHAIN = 8   # chain positions per micro-step of a node whose error children are forced
+RUN = 32    # symbols per micro-step run (kRun in search.hip)
+CHAIN = 25  # chain positions per micro-step of a node whose error children are forced (kChain)
 
 def sides(pos, right, lastL, lastR, op):
     if pos == 0: return op, op
