@@ -348,7 +348,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // patterns per batch: 4M, fewer for schemes with many searches (work
     // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
-    if (const char* e = std::getenv("SAHARA_BATCH")) maxBatch = std::max<uint64_t>(1, std::min<uint64_t>(maxBatch, std::atoll(e)));
+    if (const char* e = std::getenv("SAHARA_BATCH"))
+        maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
     const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
     if (!serial && batchesHere > 1 && c->verify) bpc = 1;
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
