@@ -67,7 +67,7 @@ struct Ctx {
     size_t pinnedCap = 0;
     bool pipeline = true;
     DevBuf<uint4> stack, seeds;           // FM spill stack; starting cursors (stream st only)
-    DevBuf<uint32_t> seedItem, dbg;
+    DevBuf<uint32_t> seedItem;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
@@ -446,8 +446,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     SH_HIP(hipStreamSynchronize(c->stC));
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
-    c->dbg.reserve(16);
-    SH_HIP(hipMemsetAsync(c->dbg.ptr, 0, 16 * sizeof(uint32_t), sA));
     // a slot's counters and queues are zero when its `free` event fires:
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
@@ -557,7 +555,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.resolveRows = resolveMode == 2 ? 1u : 0u;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
-            t.dbg = c->dbg.ptr;
             if (resolveMode == 0)
                 launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
@@ -586,14 +583,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
         S.text_ms += ms;
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
-        if (hs[2] & 16u) {
-            uint32_t d[16] = {};
-            SH_HIP(hipMemcpy(d, c->dbg.ptr, sizeof(d), hipMemcpyDeviceToHost));
-            std::string st;
-            for (int j = 1; j < 16; ++j) st += " " + std::to_string(d[j]);
-            throw Error("text phase: internal window/stack bound violated (pos e lb ub sp nSurv contM B L run same side"
-                        " Dm Im Sx:" + st + ")");
-        }
+        if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
         if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
             if (hs[2] & 8u) growCap(c->taskCap, hs[4]);
             if (hs[2] & 2u) growCap(c->hitCap, hs[1]);

@@ -94,7 +94,6 @@ struct TextArgs {
     uint32_t resolveRows;    // 1: task records carry SA rows; the kernel reads their text positions
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
-    uint32_t* dbg;           // 16 words: state of the first lane that violated a bound (or nullptr)
 };
 
 struct LocateArgs {

@@ -906,48 +906,45 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
             }
             const bool contM1 = node && L >= Bc;
-            if (node && nSurv && sp + nSurv + (contM1 ? 1u : 0u) - 1u > a.stackCap) {
-                bad = true;
-                if (a.dbg && atomicCAS(a.dbg, 0u, 1u) == 0u) {  // first violation: keep the lane's state
-                    const uint32_t v[15] = {pos, e, lb0, ub0, sp, nSurv, contM1, B, L, run0, same0, side,
-                                            (uint32_t)Dm, (uint32_t)Im, Sx};
-                    for (int j = 0; j < 15; ++j) a.dbg[1 + j] = v[j];
-                }
-            }
+            // cannot happen (the reserve rule above; tests/text_model.py): flagged, not handled
+            bad = bad || (node && nSurv && sp + nSurv + (contM1 ? 1u : 0u) - 1u > a.stackCap);
 
-            // ---- children as stack entries (x = span, y = meta)
-            auto extend = [&](uint32_t span, uint32_t k) -> uint32_t { return r0 ? span + (k << 16) : span - k; };
-            // side memory of a child: its extension side holds the operation,
-            // or MS once k forced matches follow it; the other side keeps its
-            // memory, except at pos 0, where the first operation sets both (for
-            // chain node i > 0 that was a match)
-            const uint32_t lastOther = r0 ? lastL : lastR;
+            // ---- children as stack entries (x = span, y = meta). Per step:
+            // extending by n symbols adds n << 16 (right) or -n (left) to the
+            // span, one mad; a child's side memory is its operation on the
+            // extension side (MS once k forced matches follow it), the other
+            // side keeps its memory — except at pos 0, where the first
+            // operation sets both (for chain node i > 0 that was a match)
+            const int extMul = r0 ? 65536 : -1;
+            auto extend = [&](uint32_t span, uint32_t n) -> uint32_t { return span + (uint32_t)((int)n * extMul); };
+            const uint32_t shMine = r0 ? 22u : 20u, shOther = r0 ? 20u : 22u;
+            const uint32_t otherKept = pos ? (r0 ? lastL : lastR) : (uint32_t)OP_MS;
             auto metaAt = [&](uint32_t i, uint32_t op, uint32_t k) -> uint32_t {
                 const uint32_t mine = k ? (uint32_t)OP_MS : op;
-                const uint32_t other = pos ? lastOther : (i ? (uint32_t)OP_MS : op);
-                return r0 ? (other << 20) | (mine << 22) : (mine << 20) | (other << 22);
+                const uint32_t other = (pos == 0u && i == 0u) ? op : otherKept;
+                return (mine << shMine) | (other << shOther);
             };
             const uint32_t e1 = (e + 1u) << 16;
-            auto runLen = [&](uint32_t i) -> uint32_t { return kidsF ? min(run0 - i, 7u) : 0u; };
+            // forced matches after an error child whose run starts at chain node ii
+            const uint32_t kEnd = kidsF ? run0 : 0u;
             const uint2 cM = make_uint2(extend(cur.x, Bc), (pos + Bc) | (e << 16) | metaAt(Bc, OP_MS, 0u));
             if (nSurv) {  // the surviving error children; the last one stays in registers
                 uint32_t spw = sp;
                 uint2 pend = cM;
                 bool hasPend = contM1;
                 // one loop over all of them — D at chain node i (bit i), I at i
-                // (bit kChain + i), S at L (bit 2 kChain), in that order — so
-                // the wave runs max(nSurv) iterations rather than one loop per kind
-                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << kChain) | (Sx ? 1ull << (2u * kChain) : 0ull);
+                // (bit 32 + i), S at L (bit 63), in that order — so the wave
+                // runs max(nSurv) iterations rather than one loop per kind
+                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << 32) | (Sx ? 1ull << 63 : 0ull);
                 while (sv) {
                     const uint32_t j = (uint32_t)__builtin_ctzll(sv);
                     sv &= sv - 1ull;
-                    const uint32_t kind = j < kChain ? 0u : (j < 2u * kChain ? 1u : 2u);  // 0 D, 1 I, 2 S
-                    const uint32_t i = kind == 0u ? j : (kind == 1u ? j - kChain : L);
-                    const uint32_t ii = i + (kind ? 1u : 0u);   // chain node where its forced run starts
-                    const uint32_t k = ii < run0 ? runLen(ii) : 0u;
-                    const uint32_t op = kind == 0u ? (uint32_t)OP_D : (kind == 1u ? (uint32_t)OP_I : (uint32_t)OP_MS);
-                    const uint2 v = make_uint2(extend(cur.x, i + k + (kind == 1u ? 0u : 1u)),
-                                               (pos + ii + k) | e1 | metaAt(i, op, k));
+                    const bool isS = j == 63u, isD = j < 32u, isI = !isD && !isS;
+                    const uint32_t i = isS ? L : (j & 31u);
+                    const uint32_t ii = i + (isD ? 0u : 1u);  // chain node where its forced run starts
+                    const uint32_t k = ii < kEnd ? min(kEnd - ii, 7u) : 0u;
+                    const uint32_t op = isD ? (uint32_t)OP_D : (isI ? (uint32_t)OP_I : (uint32_t)OP_MS);
+                    const uint2 v = make_uint2(extend(cur.x, i + k + (isI ? 0u : 1u)), (pos + ii + k) | e1 | metaAt(i, op, k));
                     if (hasPend) stackPut(min(spw++, a.stackCap - 1u), pend);
                     pend = v;
                     hasPend = true;
@@ -959,7 +956,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             }
 
             if (atLeaf) { leaf = true; leafStart = xo; leafE = e; }
-            if (live) have = node && (nSurv || contM1);
+            have = live ? node && (nSurv || contM1) : have;
             if (COUNT) {
                 cNodes += forced ? 0u : (node ? NN : 0u);
                 cCmp += (node && forced) ? 1u : 0u;
