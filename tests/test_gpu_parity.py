@@ -269,3 +269,24 @@ def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch, r
         gpu.set_mode(verify, locate_sa)
         for _ in range(2):
             assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
+
+
+@pytest.mark.parametrize("kmer", ["0", "8", "16"])
+def test_kmer_depths_and_seed_tasks(gpu_device, monkeypatch, kmer):
+    """The k-mer table only changes where searches start: no table, a shallow
+    one, and one as deep as a 3 Gbp index gets (16: on this 1 Mbp text nearly
+    every 16-mer is unique, so most searches become text tasks straight from
+    kSeedItems). Every depth, with and without that seed-to-task shortcut,
+    gives the oracle's multiset."""
+    monkeypatch.setenv("SAHARA_KMER", kmer)
+    flat, lens = sa.synth_reference([600_000, 400_000], sigma=6, seed=3)
+    reads = sa.synth_reads(flat, lens, 4000, 100, 2, sigma=6, seed=11)
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme("h2-k2", 0, 2, 100)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    ex = gpu.export()
+    ref = O.Index.from_parts(6, ex["n"], lens, 16, ex["bwt_f"], ex["bwt_r"], ex["sampled"], ex["samples"])
+    want = hits_as_rows(ref.search(pats, sch, edit=True, nthreads=8)[0])
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want)
+    monkeypatch.setenv("SAHARA_SEED_TASKS", "0")
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want)
