@@ -338,7 +338,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     overflow = false;
     S.patterns = c->npat;
     const uint32_t sigma = c->I.sigma;
-    const size_t lds = (size_t)c->nsearch * c->m * 4;
+    // FM LDS: the scheme table, then the bottom fmLdsDepth DFS levels (16 B
+    // per lane each; SAHARA_FM_LDS_DEPTH). None by default: with a depth-16
+    // k-mer table the FM phase is light, its stack lives in L2, and its 1.2 KB
+    // fit beside four text workgroups per CU (measured: depth 0 846M, 1 845M,
+    // 4 817M reads/s at C3)
+    uint32_t fmLdsDepth = 0;
+    if (const char* e = std::getenv("SAHARA_FM_LDS_DEPTH")) fmLdsDepth = (uint32_t)std::max(0, std::min(8, std::atoi(e)));
+    const size_t lds = (size_t)((c->nsearch * c->m + 3u) & ~3u) * 4 + (size_t)fmLdsDepth * 256 * 16;
     const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
     int bpc = fullBpc;
     // Overlapped with the text phase of the previous batch, the FM phase
@@ -364,7 +371,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // text phase geometry (LDS per lane: window | pattern | stack)
     // window: |t| + what both sides can still consume <= m + 2k symbols, plus
     // the block alignment of its start (31 symbols); 3 words per block
-    const uint32_t winBlocks = (c->m + 2 * c->maxErr + 31 + 31) / 32;
+    // (exact start: m + 2k symbols in whole blocks, copied funnel-shifted from
+    // one block more; SAHARA_EXACT_WINDOW=0: the block-aligned start below it)
+    const char* exactEnv = std::getenv("SAHARA_EXACT_WINDOW");
+    const uint32_t exactBlocks = (c->m + 2 * c->maxErr + 31) / 32;
+    const bool exactWindow = (!exactEnv || std::atoi(exactEnv) != 0) && exactBlocks + 1 <= 8 && c->patBlocks <= 8;
+    const uint32_t winBlocks = exactWindow ? exactBlocks : (c->m + 2 * c->maxErr + 31 + 31) / 32;
     const uint32_t textStack = 2 * c->maxErr + 2;
     // one-word stack entries where a node fits 30 bits (search.hip packNode)
     // (SAHARA_PACKED_STACK; off by default: at m = 100 it buys a fourth text
@@ -485,6 +497,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.tasks = sl.tasks.ptr;
         a.taskCap = c->taskCap;
         a.split = split;
+        a.ldsDepth = fmLdsDepth;
         a.prio = serial ? 0u : fmPrio;
         // starting cursors; reference execution (verify off) ranks every node
         // from the root, so it does not use the k-mer table
@@ -549,6 +562,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.flags = sl.small.ptr + 2;
             t.counters = c->counters.ptr;
             t.winBlocks = winBlocks;
+            t.exactWindow = exactWindow ? 1u : 0u;
             t.stackCap = textStack;
             t.packedStack = packedStack ? 1u : 0u;
             t.tableWords = tableWords;

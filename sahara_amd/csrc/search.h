@@ -36,6 +36,7 @@ struct SearchArgs {
     uint32_t taskCap;
     uint32_t* taskCount;
     uint32_t split;          // intervals of <= split rows go to the text phase (0: never)
+    uint32_t ldsDepth;       // DFS levels kept in LDS (after the scheme table; the rest spill to HBM)
     uint32_t prio;           // wave priority (s_setprio 0..3) when overlapped with the text phase
 };
 
@@ -88,6 +89,7 @@ struct TextArgs {
     uint32_t* flags;
     unsigned long long* counters;
     uint32_t winBlocks;      // window blocks per lane (32 symbols each)
+    uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
     uint32_t stackCap;       // text DFS stack entries per lane
     uint32_t packedStack;    // 1: one-word stack entries (m <= 127, winBlocks <= 7, maxErr <= 7)
     uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)

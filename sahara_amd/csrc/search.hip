@@ -115,7 +115,6 @@ __device__ __forceinline__ uint32_t nib(uint32_t word, uint32_t i) { return (wor
 constexpr uint32_t kSeedChunk = 64;   // seeds a wave takes per atomic
 constexpr uint32_t kTaskChunk = 64;   // text tasks a wave takes per atomic
 constexpr uint32_t kHitChunk = 64;    // hit / task slots a wave reserves per atomic
-constexpr uint32_t kLdsDepth = 4;     // FM DFS stack levels kept in LDS (16 KB per block)
 
 // Per-wave slot reservation for append-only outputs (hits, tasks): ballot +
 // prefix count inside the wave's current range; a fresh range of kHitChunk
@@ -346,10 +345,11 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t ltMask = (1ull << lane) - 1ull;
     const bool odd = lane & 1u;
-    // DFS stack: the bottom kLdsDepth levels live in LDS ([level][thread],
-    // conflict-free 16-B rows when lanes sit at equal depth), deeper levels
-    // spill to HBM ([level][grid thread]).
-    __shared__ uint4 lstk[kLdsDepth][256];
+    // DFS stack: the bottom a.ldsDepth levels live in LDS after the scheme
+    // table ([level][thread], conflict-free 16-B rows when lanes sit at equal
+    // depth), deeper levels spill to HBM ([level][grid thread]).
+    uint4* lstk = reinterpret_cast<uint4*>(sch + ((a.nsearch * a.m + 3u) & ~3u));
+    const uint32_t ldsDepth = a.ldsDepth;
     uint4* stk = a.stack + gtid;
 
     uint32_t sp = 0, pid = 0, sIdx = 0;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
         if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
         if (!have && sp > 0) {
             --sp;
-            cur = sp < kLdsDepth ? lstk[sp][threadIdx.x] : stk[(size_t)(sp - kLdsDepth) * T];
+            cur = sp < ldsDepth ? lstk[sp * 256u + threadIdx.x] : stk[(size_t)(sp - ldsDepth) * T];
             have = true;
         }
         if (!__any(have)) break;
@@ -533,8 +533,8 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
             };
             auto push = [&](const uint4& v) {
                 if (sp < a.stackCap) {
-                    if (sp < kLdsDepth) lstk[sp][threadIdx.x] = v;
-                    else stk[(size_t)(sp - kLdsDepth) * T] = v;
+                    if (sp < ldsDepth) lstk[sp * 256u + threadIdx.x] = v;
+                    else stk[(size_t)(sp - ldsDepth) * T] = v;
                     ++sp;
                 } else {
                     atomicOr(a.flags, 1u);
@@ -660,6 +660,30 @@ __device__ __forceinline__ void copyBlocks(uint32_t* DA, __amdgpu_buffer_rsrc_t 
             if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[i][0]; D[256] = vb[i][1]; D[512] = vb[i][2]; }
         }
     }
+}
+
+// Same, but the window starts at any symbol: na blocks come from na + 1
+// source blocks funnel-shifted by sh symbols (na + 1 <= 8, nb <= 8).
+__device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_rsrc_t RA, uint32_t offA, uint32_t sh,
+                                                  uint32_t na, uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB,
+                                                  uint32_t nb) {
+    decltype(__builtin_amdgcn_raw_buffer_load_b128(RA, 0u, 0, 0)) va[8], vb[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        va[j] = __builtin_amdgcn_raw_buffer_load_b128(RA, j <= na ? offA + 16u * j : kBufOOB, 0, 0);
+        vb[j] = __builtin_amdgcn_raw_buffer_load_b128(RB, j < nb ? offB + 16u * j : kBufOOB, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 7; ++j)
+        if (j < na) {
+            uint32_t* D = DA + 3u * j * 256u;
+            D[0] = __builtin_amdgcn_alignbit(va[j + 1][0], va[j][0], sh);
+            D[256] = __builtin_amdgcn_alignbit(va[j + 1][1], va[j][1], sh);
+            D[512] = __builtin_amdgcn_alignbit(va[j + 1][2], va[j][2], sh);
+        }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+        if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[j][0]; D[256] = vb[j][1]; D[512] = vb[j][2]; }
 }
 
 // Text tasks carry an SA row; replace it by its text position (one SA read
@@ -800,8 +824,14 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
                 const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
-                wb = (x > left ? x - left : 0u) & ~31u;             // block-aligned window start
-                copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
+                wb = x > left ? x - left : 0u;  // window start
+                if (a.exactWindow) {            // at wb: m + 2k symbols fit in winBlocks blocks
+                    copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
+                                      pid * patBlocks * 16u, patBlocks);
+                } else {                        // at the block start below wb (31 more symbols)
+                    wb &= ~31u;
+                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
+                }
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
                 have = true;
             }
