@@ -57,8 +57,8 @@ struct Ctx {
     static constexpr int kSlots = 3;
     struct Slot {
         DevBuf<uint4> hits, tasks;
-        DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, -, seedCount
-        DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512)
+        DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
+        DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512), [512, 768)
         hipEvent_t fmStart = nullptr, seedDone = nullptr, fmDone = nullptr, textStart = nullptr, textDone = nullptr,
                    free = nullptr;
     } slot[kSlots];
@@ -167,7 +167,7 @@ Ctx* newCtx(int device) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);
-        sl.queues.reserve(512);
+        sl.queues.reserve(768);
     }
     c->small.reserve(8);
     c->counters.reserve(16);
@@ -406,6 +406,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     if (const char* e = std::getenv("SAHARA_FM_PRIO")) fmPrio = (uint32_t)std::max(0, std::min(3, std::atoi(e)));
     int resolveMode = 2;
     if (const char* e = std::getenv("SAHARA_RESOLVE")) resolveMode = std::max(0, std::min(2, std::atoi(e)));
+    // (pipelined, in-kernel task resolve) the first batch's text phase starts
+    // on its seed tasks while its FM phase runs (SAHARA_EARLY_TEXT=0: after it)
+    const char* earlyEnv = std::getenv("SAHARA_EARLY_TEXT");
+    const bool early = !serial && split && resolveMode == 2 && (!earlyEnv || std::atoi(earlyEnv) != 0);
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -462,7 +466,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
         SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), s));
-        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 512 * sizeof(uint32_t), s));
+        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 768 * sizeof(uint32_t), s));
         SH_HIP(hipEventRecord(sl.free, s));
     };
     for (auto& sl : c->slot) resetSlot(sl, sA);
@@ -528,8 +532,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.seedCount = sl.small.ptr + 6;
         SH_HIP(hipEventRecord(sl.fmStart, sA));
         launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sA);
+        if (early && b == 0)  // the seed tasks end here: the text phase may start on them
+            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sA));
         SH_HIP(hipEventRecord(sl.seedDone, sA));
-        launchSearch(a, sigma, c->edit, count, b == 0 ? firstBlocks : blocks, lds, sA);
+        launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
         if (split && resolveMode == 1)
             launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sA);
         SH_HIP(hipEventRecord(sl.fmDone, sA));
@@ -538,7 +544,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     auto issueText = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b];
-        SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+        const bool split0 = early && b == 0;
+        SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone : sl.fmDone, 0));
         SH_HIP(hipEventRecord(sl.textStart, sB));
         if (split) {
             TextArgs t{};
@@ -571,6 +578,16 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.refillAt = c->refillAt;
             if (resolveMode == 0)
                 launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
+            if (split0) {
+                // the first batch's seed tasks while its FM phase runs, then the
+                // tasks the FM phase appended after them
+                t.taskCount = sl.small.ptr + 5;
+                launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+                SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+                t.taskBegin = sl.small.ptr + 5;
+                t.taskCount = sl.small.ptr + 4;
+                t.work = sl.queues.ptr + 512;
+            }
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));

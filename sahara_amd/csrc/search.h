@@ -80,6 +80,7 @@ struct TextArgs {
     const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
     const uint4* tasks;
     const uint32_t* taskCount;  // tasks written by the FM kernel (device-side: no host round trip)
+    const uint32_t* taskBegin;  // first task of this launch (device-side; nullptr: 0)
     uint32_t taskCap;
     uint32_t* work;
     uint4* hits;

@@ -730,7 +730,11 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
     const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
     const uint32_t m = a.m;
-    const uint32_t ntasks = min(*a.taskCount, a.taskCap);
+    // this launch's tasks: [tBase, taskCount) of the batch's list
+    const uint32_t tEnd = min(*a.taskCount, a.taskCap);
+    const uint32_t tBase = a.taskBegin ? min(*a.taskBegin, tEnd) : 0u;
+    const uint32_t ntasks = tEnd - tBase;
+    const uint4* tasks = a.tasks + tBase;
 
     uint32_t sp = 0, pid = 0, wb = 0, sBase = 0;
     bool have = false, exhausted = false, bad = false;
@@ -758,7 +762,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         if (queue.next(lane, kTaskChunk, b, e)) {
             nBase = b;
             nEnd = e;
-            if (b + lane < e) nextRec = a.tasks[b + lane];
+            if (b + lane < e) nextRec = tasks[b + lane];
             haveNext = true;
             nextRaw = resolve;
         } else {
@@ -799,7 +803,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     } else {
                         nBase = b;
                         nEnd = e;
-                        if (b + lane < e) nextRec = a.tasks[b + lane];
+                        if (b + lane < e) nextRec = tasks[b + lane];
                         haveNext = true;
                         nextRaw = resolve;
                     }
