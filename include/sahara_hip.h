@@ -89,6 +89,7 @@ typedef struct sahara_stats {
     uint64_t text_steps;         /* text-kernel micro-steps, lane count (count=1) */
     double   stage_ms;           /* wall time of staging the patterns: H2D, 4-bit packing, rank check */
     double   output_ms;          /* sahara_gpu_search: wall time of handing the hits to the host */
+    uint64_t text_launches;      /* text-phase kernel launches in the pass */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

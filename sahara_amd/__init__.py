@@ -60,7 +60,7 @@ class Stats(C.Structure):
                 ("text_cycles_step", C.c_uint64), ("text_cycles_emit", C.c_uint64),
                 ("text_compare_steps", C.c_uint64), ("text_grid", C.c_uint32), ("pipelined", C.c_uint32),
                 ("seed_ms", C.c_double), ("text_steps", C.c_uint64), ("stage_ms", C.c_double),
-                ("output_ms", C.c_double)]
+                ("output_ms", C.c_double), ("text_launches", C.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

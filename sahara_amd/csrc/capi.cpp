@@ -587,8 +587,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                 t.taskBegin = sl.small.ptr + 5;
                 t.taskCount = sl.small.ptr + 4;
                 t.work = sl.queues.ptr + 512;
+                ++S.text_launches;
             }
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+            ++S.text_launches;
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));
     };
