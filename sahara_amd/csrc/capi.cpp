@@ -72,6 +72,7 @@ struct Ctx {
     size_t pinnedCap = 0;
     bool pipeline = true;
     DevBuf<uint4> stack, seeds;           // FM spill stack; starting cursors (stream st only)
+    DevBuf<uint8_t> rawPats;              // staged pattern bytes before packing
     DevBuf<uint32_t> seedItem;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
@@ -262,7 +263,7 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     textTable(pi, l, u, ns, m, packed, cover);
     c->patWords = (m + 7) / 8;
     {
-        DevBuf<uint8_t> raw;
+        DevBuf<uint8_t>& raw = c->rawPats;  // kept: no 2 GB allocate / free per call at C3
         raw.reserve(npat * m);
         SH_HIP(hipMemcpyAsync(raw.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
         c->pats.reserve(npat * c->patWords + 4);  // + tail words read by paired loads
