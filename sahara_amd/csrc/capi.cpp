@@ -55,15 +55,16 @@ struct Ctx {
     // work buffers. Batches rotate over three slots so that the FM phase runs
     // up to two batches ahead (stream `st`) of the text phase (stream `stB`),
     // while batch i-1 runs its locate and sort (stream `stC`).
-    static constexpr int kSlots = 3;
+    static constexpr int kSlots = 5;
     struct Slot {
-        DevBuf<uint4> hits, tasks;
+        DevBuf<uint4> hits, tasks, seeds;  // seeds: starting cursors (kSeedItems -> kSearchFM)
+        DevBuf<uint32_t> seedItem;
         DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
         DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512), [512, 768)
         hipEvent_t fmStart = nullptr, seedDone = nullptr, fmDone = nullptr, textStart = nullptr, textDone = nullptr,
                    free = nullptr;
     } slot[kSlots];
-    hipStream_t stB = nullptr, stC = nullptr;
+    hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
     uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
     // two pinned staging chunks for handing hits to pageable host memory: the
     // DMA of one chunk overlaps the host copy out of the other (copyOut)
@@ -71,9 +72,8 @@ struct Ctx {
     void* outStage[2] = {nullptr, nullptr};
     size_t pinnedCap = 0;
     bool pipeline = true;
-    DevBuf<uint4> stack, seeds;           // FM spill stack; starting cursors (stream st only)
+    DevBuf<uint4> stack;                  // FM spill stack (stream st only)
     DevBuf<uint8_t> rawPats;              // staged pattern bytes before packing
-    DevBuf<uint32_t> seedItem;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
@@ -98,6 +98,7 @@ struct Ctx {
             if (p) (void)hipHostFree(p);
         if (stB) (void)hipStreamDestroy(stB);
         if (stC) (void)hipStreamDestroy(stC);
+        if (stD) (void)hipStreamDestroy(stD);
         if (st) (void)hipStreamDestroy(st);
     }
 };
@@ -170,6 +171,7 @@ Ctx* newCtx(int device) {
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stD, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
@@ -358,16 +360,16 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
     int bpc = fullBpc;
     // Overlapped with the text phase of the previous batch, the FM phase
-    // (memory-latency bound, and short with a depth-16 k-mer table) runs one
-    // workgroup per CU, which fits in the LDS beside three text workgroups;
-    // alone it takes them all. (Measured at C3: 1 WG/CU 15.2 ms/step, 2: 15.8.)
+    // (memory-latency bound) runs two workgroups per CU beside three text
+    // workgroups; alone it takes all that fit. (Measured at C3 with pruned
+    // text steps: text 3 + FM 2 846-873M reads/s, text 4 + FM 1 845-847M.)
     // patterns per batch: 4M, fewer for schemes with many searches (work
     // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (const char* e = std::getenv("SAHARA_BATCH"))
         maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
     const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
-    if (!serial && batchesHere > 1 && c->verify) bpc = 1;
+    if (!serial && batchesHere > 1 && c->verify) bpc = 2;
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     // the first batch's FM phase has nothing to overlap with: full occupancy
@@ -405,7 +407,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
         tbpc = textBlocksPerCU(sigma, c->edit, packedStack, textLds);
-    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(tbpc, std::atoi(e)));
+    // overlapped with the FM phase, three text workgroups per CU leave room
+    // for two FM workgroups beside them (the FM chain of seeds and FM launches
+    // is the other critical path once the text phase prunes dead children)
+    if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, packedStack, textLds), std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     // where a task's SA row becomes its text position: 2 = inside the text
     // kernel, a chunk of task records ahead (default: no pass between the FM
@@ -465,10 +471,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->big.reserve(maxBatch);
     }
     SH_HIP(hipMemsetAsync(c->qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
-    hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC;
+    hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
     SH_HIP(hipStreamSynchronize(c->st));
     SH_HIP(hipStreamSynchronize(c->stB));
     SH_HIP(hipStreamSynchronize(c->stC));
+    SH_HIP(hipStreamSynchronize(c->stD));
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
     // a slot's counters and queues are zero when its `free` event fires:
@@ -523,10 +530,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sd.kmer = c->verify && c->I.kmerK ? c->I.kmer.ptr : nullptr;
         sd.kmerK = c->I.kmerK;
         sd.kmerStart = c->kmerStart.ptr;
-        c->seeds.reserve(a.nitems);
-        c->seedItem.reserve(a.nitems);
-        sd.seeds = c->seeds.ptr;
-        sd.seedItem = c->seedItem.ptr;
+        sl.seeds.reserve(a.nitems);
+        sl.seedItem.reserve(a.nitems);
+        sd.seeds = sl.seeds.ptr;
+        sd.seedItem = sl.seedItem.ptr;
         sd.seedCount = sl.small.ptr + 6;
         sd.m = c->m;
         const char* seedTasks = std::getenv("SAHARA_SEED_TASKS");  // 0: every seed goes through the FM kernel
@@ -536,14 +543,18 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sd.taskCount = sl.small.ptr + 4;
         sd.flags = sl.small.ptr + 2;
         sd.counters = count ? c->counters.ptr : nullptr;
-        a.seeds = c->seeds.ptr;
-        a.seedItem = c->seedItem.ptr;
+        a.seeds = sl.seeds.ptr;
+        a.seedItem = sl.seedItem.ptr;
         a.seedCount = sl.small.ptr + 6;
-        SH_HIP(hipEventRecord(sl.fmStart, sA));
-        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sA);
+        // seeds on their own stream (sD), so that they run ahead of the FM
+        // phase of the batch before (both are HBM-latency bound and light)
+        SH_HIP(hipStreamWaitEvent(sD, sl.free, 0));
+        SH_HIP(hipEventRecord(sl.fmStart, sD));
+        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sD);
         if (early && b == 0)  // the seed tasks end here: the text phase may start on them
-            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sA));
-        SH_HIP(hipEventRecord(sl.seedDone, sA));
+            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+        SH_HIP(hipEventRecord(sl.seedDone, sD));
+        SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
         if (split && resolveMode == 1)
             launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sA);
@@ -719,6 +730,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamSynchronize(sA));
         SH_HIP(hipStreamSynchronize(sB));
         SH_HIP(hipStreamSynchronize(sC));
+        SH_HIP(hipStreamSynchronize(sD));
         if (overflow) return;  // the caller redoes the pass serially with the grown buffers
     } else {
         for (uint64_t b = 0; b < nbatch; ++b) {

@@ -603,6 +603,7 @@ __device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
     return ~((p.b0 ^ t.b0) | (p.b1 ^ t.b1) | (p.b2 ^ t.b2));
 }
 __device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
+__device__ __forceinline__ Planes shr2(const Planes& p) { return {p.b0 >> 2, p.b1 >> 2, p.b2 >> 2}; }
 // 32 symbols from offset o of a lane's interleaved plane array (block i, plane
 // b at word (3i + b) * 256). o may be negative (down to -32): reads may run
 // past either end of the array into the lane's neighbouring LDS regions; callers
@@ -914,13 +915,50 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             if (side == OP_D) Im &= ~first;
             // S at the first mismatch (not where M is merely disallowed: l > e)
             bool Sx = node && !forced && L < B && misOK && ((TZ & ~E0) >> L) & 1u;
+            // forced runs: a child at e + 1 = u is forced for the rest of the run,
+            // and survives only if min(7, rest of the run) symbols match on its
+            // diagonal (positions past the run count as matches): R7x bit j =
+            // that check for a run starting at chain position j on diagonal x
+            const uint32_t bR = beyondR(run0), bR1 = beyondR(run0 - 1u);
+            const uint32_t R7E0 = run7(E0 | bR), R7ED = run7(ED | bR), R7EI = run7(EI | bR1);
             if (kidsF) {
-                // forced runs: D at i needs p[i..] == t[i+1..], I at i needs
-                // p[i+1..] == t[i..], S at L needs p[L+1..] == t[L+1..], each for
-                // min(7, rest of the run) symbols (positions past the run count as matches)
-                Dm &= run7(ED | beyondR(run0));
-                Im &= run7(EI | beyondR(run0 - 1u));
-                Sx = Sx && ((run7(E0 | beyondR(run0)) >> (L + 1u)) & 1u);
+                // D at i: p[i..] vs t[i+1..]; I at i: p[i+1..] vs t[i..]; S at L: p[L+1..] vs t[L+1..]
+                Dm &= R7ED;
+                Im &= R7EI;
+                Sx = Sx && ((R7E0 >> (L + 1u)) & 1u);
+            }
+            if (EDIT && node && e + 2u == ub0) {
+                // A node expanded alone whose error children are chain nodes:
+                // keep only the children whose subtree outlives their own first
+                // step. A child does if its match chain leaves the run or the
+                // 32 symbols read (chain length > kRun - 9), or one of its own
+                // error children (forced) passes the check above on its
+                // diagonal; no I right after D, no D right after I (policy P0).
+                // tests/text_model.py holds this to the plain DFS.
+                const uint32_t ED2 = eqm(P16, shr2(T16)) & (VT >> 2);   // p_j == t_{j+2}
+                const uint32_t EI2 = eqm(shr2(P16), T16) & VT;          // p_{j+2} == t_j
+                const uint32_t bR2 = run0 >= 2u ? beyondR(run0 - 2u) : kRunMask;
+                const uint32_t R7ED2 = run7(ED2 | bR), R7EI2 = run7(EI2 | bR2);
+                const uint32_t I2after = (R7E0 >> 1) & ~1u;  // bit j: I2 (back to diagonal 0) at chain node j > 0
+                constexpr uint32_t kLim = kRun - 9u;
+                if (Dm & first) {  // D child: p_j vs t_{j+1}
+                    const uint32_t LD = (uint32_t)__builtin_ctz(~ED);
+                    const bool keep = LD >= run0 || LD > kLim || ((R7ED >> (LD + 1u)) & 1u) ||
+                                      ((R7ED2 | I2after) & onesR(LD + 1u)) != 0u;
+                    if (!keep) Dm &= ~first;
+                }
+                if (Im & first) {  // I child: p_{x+1} vs t_x
+                    const uint32_t LI = ~EI ? (uint32_t)__builtin_ctz(~EI) : kRun;
+                    const bool keep = LI + 1u >= run0 || LI > kLim || ((R7EI >> (LI + 1u)) & 1u) ||
+                                      ((I2after | R7EI2) & onesR(LI + 1u)) != 0u;
+                    if (!keep) Im &= ~first;
+                }
+                if (Sx) {  // S child at the mismatch L = 0: p_x vs t_x, x >= 1
+                    const uint32_t rest = ~E0 & ~1u;
+                    const uint32_t LS = rest ? (uint32_t)__builtin_ctz(rest) : kRun;
+                    Sx = LS >= run0 || LS > kLim || ((R7E0 >> (LS + 1u)) & 1u) ||
+                         ((R7ED | R7EI) & ~1u & onesR(LS + 1u)) != 0u;
+                }
             }
             const bool contM = node && L >= B;  // the match chain continues at pos + B
             uint32_t nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);

@@ -44,7 +44,7 @@ def states(P, T, sch, edit, limit=300):
 
 
 @pytest.mark.parametrize("run,chain_len", [(16, 8), (32, 16), (32, 25)])
-@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
 def test_chain_step_equals_plain_dfs(seed, run, chain_len):
     rng = random.Random(seed)
     checked = 0
@@ -76,3 +76,36 @@ def test_chain_step_equals_plain_dfs(seed, run, chain_len):
             assert chain(P, T, task, (pi, l, u, dirs), edit, cap=cap, RUN=run, CHAIN=chain_len) == plain(P, T, task, (pi, l, u, dirs), edit)
             checked += 1
     assert checked > 100
+
+
+def test_pruning_on_true_reads():
+    """h2-k2, m = 100, k = 2: reads with two random edits against their text.
+    From every task the FM phase could hand over at depth 16, the pruned step
+    (nodes two errors below their bound keep only viable error children) gives
+    the plain DFS's leaves, in fewer micro-steps."""
+    rng = random.Random(5)
+    m, k = 100, 2
+    pi, l, u = oracle.scheme("h2-k2", 0, k, m)
+    steps = {True: {}, False: {}}
+    for _ in range(12):
+        T = [rng.randint(1, 4) for _ in range(400)]
+        P = T[150:250]
+        for _ in range(k):
+            j, r = rng.randrange(5, 95), rng.random()
+            if r < 0.33:
+                P[j] = rng.choice([c for c in (1, 2, 3, 4) if c != P[j]])
+            elif r < 0.66:
+                del P[j]
+                P.append(T[250])
+            else:
+                P.insert(j, rng.randint(1, 4))
+                P.pop()
+        for s in range(len(pi)):
+            sp, sl, su = [int(v) for v in pi[s]], [int(v) for v in l[s]], [int(v) for v in u[s]]
+            dirs = [sp[p] > sp[p - 1] if p else sp[1] > sp[0] for p in range(m)]
+            sch = (sp, sl, su, dirs)
+            for task in [n for n in states(P, T, sch, True, limit=100000) if n[2] == 16]:
+                want = plain(P, T, task, sch, True)
+                for prune in (True, False):
+                    assert chain(P, T, task, sch, True, cap=6, PRUNE=prune, stats=steps[prune]) == want
+    assert steps[True]["steps"] < 0.85 * steps[False]["steps"]

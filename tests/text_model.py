@@ -4,7 +4,9 @@ Test infrastructure: `chain()` restates, one node at a time and with Python
 sets instead of nibble masks, what a lane of the text kernel does per
 micro-step — forced-run nodes matching up to RUN symbols, chain nodes walking
 up to CHAIN positions of a match chain and checking every error child's forced
-run, the stack reserve rule — and `plain()` is the textbook DFS of policy P0
+run, nodes two errors below their bound keeping only the error children that
+outlive their own first step, the stack reserve rule — and `plain()` is the
+textbook DFS of policy P0
 (docs/semantics.md) against the text. tests/test_text_model.py holds the two
 to the same leaf multiset from arbitrary DFS states.
 """
@@ -55,7 +57,7 @@ def tables(sch):
         run[p], same[p] = k, s
     return run, same
 
-def chain(P, T, task, sch, edit, cap=100, RUN=RUN, CHAIN=CHAIN):
+def chain(P, T, task, sch, edit, cap=100, RUN=RUN, CHAIN=CHAIN, PRUNE=True, stats=None):
     pi, l, u, dirs = sch
     m = len(pi)
     run, same = tables(sch)
@@ -63,6 +65,8 @@ def chain(P, T, task, sch, edit, cap=100, RUN=RUN, CHAIN=CHAIN):
     st = [task]
     while st:
         xs, ye, pos, e, lL, lR = st.pop()
+        if stats is not None:
+            stats['steps'] = stats.get('steps', 0) + 1
         if pos == m:
             out.append((xs, e)); continue
         q0 = pi[pos]; r0 = dirs[pos]; lb0 = l[pos]; ub0 = u[pos]; run0 = run[pos]; same0 = same[pos]
@@ -99,6 +103,37 @@ def chain(P, T, task, sch, edit, cap=100, RUN=RUN, CHAIN=CHAIN):
             Dm &= run7(ED, run0)
             Im &= run7(EI, run0 - 1)
             Sx = Sx and ((L+1) in run7(E0, run0))
+        elif PRUNE and edit and e + 2 == ub0:
+            # a node expanded alone whose error children are chain nodes
+            # (kidsF): keep only the children whose subtree survives their own
+            # first step (side rules: no I right after D, no D right after I)
+            ED2 = {j for j in range(RUN) if pj(j) == tj(j+2)}
+            EI2 = {j for j in range(RUN) if pj(j+2) == tj(j)}
+            LIM = RUN - 9
+            R = run0
+            R7 = {}
+            def r7(S, beyond, j):
+                key = (id(S), beyond)
+                if key not in R7: R7[key] = run7(S, beyond)
+                return j in R7[key]
+            def first_not(S, j):
+                while j < RUN and j in S: j += 1
+                return j
+            if 0 in Dm:   # D child: pattern j vs text j + 1
+                LD = first_not(ED, 0)
+                if not (LD >= R or LD > LIM or r7(ED, R, LD + 1) or
+                        any(r7(ED2, R, j) or (j > 0 and r7(E0, R, j + 1)) for j in range(LD + 1))):
+                    Dm.discard(0)
+            if 0 in Im:   # I child: pattern x + 1 vs text x
+                LI = first_not(EI, 0)
+                if not (LI >= R - 1 or LI > LIM or r7(EI, R - 1, LI + 1) or
+                        any((x > 0 and r7(E0, R, x + 1)) or r7(EI2, R - 2, x) for x in range(LI + 1))):
+                    Im.discard(0)
+            if Sx:        # S child at the mismatch L = 0: pattern x vs text x, x >= 1
+                LS = first_not(E0, 1)
+                if not (LS >= R or LS > LIM or r7(E0, R, LS + 1) or
+                        any(r7(ED, R, x) or r7(EI, R - 1, x) for x in range(1, LS + 1))):
+                    Sx = False
         contM = L >= B
         n = len(Dm) + len(Im) + (1 if Sx else 0)
         Bc = B
