@@ -424,7 +424,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // (pipelined, in-kernel task resolve) the first batch's text phase starts
     // on its seed tasks while its FM phase runs (SAHARA_EARLY_TEXT=0: after it)
     const char* earlyEnv = std::getenv("SAHARA_EARLY_TEXT");
-    const bool early = !serial && split && resolveMode == 2 && (!earlyEnv || std::atoi(earlyEnv) != 0);
+    // (only with several batches: a lone batch's FM phase runs at full
+    // occupancy, and its text phase split in two measured 45M against 68M
+    // reads/s at C5)
+    const bool early = !serial && split && resolveMode == 2 && batchesHere > 1 &&
+                       (!earlyEnv || std::atoi(earlyEnv) != 0);
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -590,6 +594,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.counters = c->counters.ptr;
             t.winBlocks = winBlocks;
             t.exactWindow = exactWindow ? 1u : 0u;
+            // (SAHARA_PRUNE=0 turns it off; C3: 43 -> 28 micro-steps per read,
+            // C5: 439 -> 303 and 68M -> 82M reads/s)
+            const char* pruneEnv = std::getenv("SAHARA_PRUNE");
+            t.prune = !pruneEnv || std::atoi(pruneEnv) != 0 ? 1u : 0u;
             t.stackCap = textStack;
             t.packedStack = packedStack ? 1u : 0u;
             t.tableWords = tableWords;

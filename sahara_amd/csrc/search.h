@@ -91,6 +91,7 @@ struct TextArgs {
     unsigned long long* counters;
     uint32_t winBlocks;      // window blocks per lane (32 symbols each)
     uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
+    uint32_t prune;          // 1: drop error children of e + 2 = u nodes that die in their first step
     uint32_t stackCap;       // text DFS stack entries per lane
     uint32_t packedStack;    // 1: one-word stack entries (m <= 127, winBlocks <= 7, maxErr <= 7)
     uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)

@@ -927,7 +927,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 Im &= R7EI;
                 Sx = Sx && ((R7E0 >> (L + 1u)) & 1u);
             }
-            if (EDIT && node && e + 2u == ub0) {
+            if (a.prune && EDIT && node && e + 2u == ub0) {
                 // A node expanded alone whose error children are chain nodes:
                 // keep only the children whose subtree outlives their own first
                 // step. A child does if its match chain leaves the run or the
