@@ -230,34 +230,57 @@ __device__ __forceinline__ uint32_t childMeta(uint32_t pos, uint32_t e, uint32_t
 // items whose k-mer does not occur end here. Every other item starts at the
 // root. Surviving items are appended (wave ballot + one atomic per wave) to
 // the seed list that kSearchFM consumes.
+// The k-mer table index of item i's error-free first part, or ~0u when the
+// item starts at the root (no table, no error-free first part, or an N in it).
+template <int SIGMA>
+__device__ __forceinline__ uint32_t seedCode(const SeedArgs& a, uint32_t i) {
+    if (i >= a.nitems || !a.kmer) return ~0u;
+    const uint32_t pid = i / a.nsearch, s = i - pid * a.nsearch;
+    const uint32_t ks = a.kmerStart[s];
+    if (ks == 0xFFFFFFFFu) return ~0u;
+    const uint32_t* pw = a.pats + (size_t)pid * a.patWords + (ks >> 3);
+    const uint32_t w0 = pw[0], w1 = pw[1], w2 = pw[2];
+    const uint32_t sh = (ks & 7u) * 4u;
+    const uint64_t run = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) |
+                         ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
+    uint32_t code = 0;
+    bool acgt = true;
+    for (uint32_t j = 0; j < a.kmerK; ++j) {
+        const uint32_t c = (uint32_t)(run >> (4u * j)) & 0xFu;  // A1 C2 G3 (N4) T5|T4
+        acgt = acgt && !(SIGMA == 6 && c == 4u);
+        code = code * 4u + ((SIGMA == 6 && c == 5u) ? 3u : c - 1u);
+    }
+    return acgt ? (uint32_t)(code & ((1ull << (2u * a.kmerK)) - 1ull)) : ~0u;
+}
+
+// Item i's starting cursor: the k-mer table entry of its error-free first
+// part (depth kmerK), else the root. The two lanes of a pair fetch each
+// other's 16-B entries cooperatively — each lane 8 B of the even lane's entry,
+// then 8 B of the odd lane's, swapped back with DPP — so that a load
+// instruction touches at most 32 distinct lines of the 68.7 GB table (address
+// translation, not bandwidth, bounds these random lookups: tools/gather_bench).
+// Must be called by all lanes of the wave.
 template <int SIGMA>
 __device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& keep) {
-    uint4 cur = make_uint4(0u, 0u, a.n, kDeltaZero);
     keep = i < a.nitems;
-    if (keep && a.kmer) {
-        const uint32_t pid = i / a.nsearch, s = i - pid * a.nsearch;
-        const uint32_t ks = a.kmerStart[s];
-        if (ks != 0xFFFFFFFFu) {
-            const uint32_t* pw = a.pats + (size_t)pid * a.patWords + (ks >> 3);
-            const uint32_t w0 = pw[0], w1 = pw[1], w2 = pw[2];
-            const uint32_t sh = (ks & 7u) * 4u;
-            const uint64_t run = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) |
-                                 ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32);
-            uint32_t code = 0;
-            bool acgt = true;
-            for (uint32_t j = 0; j < a.kmerK; ++j) {
-                const uint32_t c = (uint32_t)(run >> (4u * j)) & 0xFu;  // A1 C2 G3 (N4) T5|T4
-                acgt = acgt && !(SIGMA == 6 && c == 4u);
-                code = code * 4u + ((SIGMA == 6 && c == 5u) ? 3u : c - 1u);
-            }
-            if (acgt) {
-                const uint4 t = a.kmer[(uint32_t)(code & ((1ull << (2u * a.kmerK)) - 1ull))];
-                cur = make_uint4(t.x, t.y, t.z, packMeta(a.kmerK, 0u, OP_MS, OP_MS));
-                keep = t.z != 0u;
-            }
-        }
-    }
-    return cur;
+    const uint32_t code = seedCode<SIGMA>(a, i);
+    const bool need = keep && code != ~0u;
+    const bool odd = (threadIdx.x & 1u) != 0u;
+    const uint64_t own = (uint64_t)(a.kmer + (need ? code : 0u));
+    const uint64_t other = pairSwap64(own);
+    const bool otherNeed = pairSwap(need ? 1u : 0u) != 0u;
+    const uint64_t addrE = odd ? other : own, addrO = odd ? own : other;
+    const bool needE = odd ? otherNeed : need, needO = odd ? need : otherNeed;
+    const uint32_t half = odd ? 8u : 0u;
+    uint2 rE = make_uint2(0u, 0u), rO = rE;
+    if (needE) rE = *reinterpret_cast<const uint2*>(addrE + half);  // even's entry: bytes 0-7 | 8-15
+    if (needO) rO = *reinterpret_cast<const uint2*>(addrO + half);  // odd's entry: bytes 0-7 | 8-15
+    const uint2 gE = make_uint2(pairSwap(rE.x), pairSwap(rE.y));     // even <- bytes 8-15 of its entry
+    const uint2 gO = make_uint2(pairSwap(rO.x), pairSwap(rO.y));     // odd <- bytes 0-7 of its entry
+    const uint4 t = odd ? make_uint4(gO.x, gO.y, rO.x, rO.y) : make_uint4(rE.x, rE.y, gE.x, gE.y);
+    if (!need) return make_uint4(0u, 0u, a.n, kDeltaZero);
+    keep = t.z != 0u;
+    return make_uint4(t.x, t.y, t.z, packMeta(a.kmerK, 0u, OP_MS, OP_MS));
 }
 
 // Each block takes 1024 consecutive items per round (4 per thread, so four
