@@ -16,6 +16,7 @@
 #include <memory>
 #include <random>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -74,6 +75,10 @@ struct Ctx {
     bool pipeline = true;
     DevBuf<uint4> stack;                  // FM spill stack (stream st only)
     DevBuf<uint8_t> rawPats;              // staged pattern bytes before packing
+    DevBuf<uint8_t> nibPats;              // the same, two symbols per byte as uploaded (stageIn)
+    bool nibbleUpload = true;             // SAHARA_NIBBLE_UPLOAD=0: pattern bytes go up as given
+    uint8_t* nibHost = nullptr;           // pinned: the packed patterns on their way up
+    size_t nibHostCap = 0;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
@@ -94,6 +99,7 @@ struct Ctx {
             for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmDone, sl.textStart, sl.textDone, sl.free})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
+        if (nibHost) (void)hipHostFree(nibHost);
         for (void* p : outStage)
             if (p) (void)hipHostFree(p);
         if (stB) (void)hipStreamDestroy(stB);
@@ -254,6 +260,73 @@ void textTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_
     }
 }
 
+// Host pattern bytes -> device, one symbol per byte. Patterns cross PCIe as
+// two symbols per byte: host threads each pack a slice, 4 MB at a time, into
+// one pinned buffer and queue each piece's DMA as soon as it is packed, and
+// kUnpackNibbles expands them on the device. At C3 this halves the 2 GB
+// upload, which runs at the link's rate. Returns false when a byte is >= 16
+// (no rank of any alphabet; smaller out-of-range ranks are found by the
+// device check against this index's sigma).
+static bool stageIn(Ctx* c, uint8_t* dst, const uint8_t* src, size_t n) {
+    if (const char* e = std::getenv("SAHARA_NIBBLE_UPLOAD")) c->nibbleUpload = std::atoi(e) != 0;
+    if (!c->nibbleUpload || n < (64u << 20)) {
+        SH_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->st));
+        return true;
+    }
+    const size_t nb = (n + 1) / 2;  // packed bytes
+    if (c->nibHostCap < nb) {
+        if (c->nibHost) SH_HIP(hipHostFree(c->nibHost));
+        c->nibHost = nullptr;
+        c->nibHostCap = 0;
+        SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->nibHost), nb));
+        c->nibHostCap = nb;
+    }
+    c->nibPats.reserve(nb + 8);
+    SH_HIP(hipStreamSynchronize(c->st));  // the pinned buffer may still feed the last call's DMA
+    uint8_t* out = c->nibHost;
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    constexpr size_t kPiece = 4u << 20;
+    const size_t pieces = (nb + kPiece - 1) / kPiece;
+    std::atomic<uint64_t> orAll{0};
+    std::atomic<int> failed{0};
+    auto pack = [&](size_t lo, size_t hi) {  // packed bytes [lo, hi)
+        uint64_t acc = 0;
+        const uint8_t* in = src + 2 * lo;
+        const size_t full = std::min(hi, n / 2);  // bytes with both symbols
+        size_t i = lo;
+        for (; i + 4 <= full; i += 4, in += 8) {  // 8 symbols -> 4 bytes
+            uint64_t v;
+            std::memcpy(&v, in, 8);
+            acc |= v;
+            v = (v | (v >> 4)) & 0x00FF00FF00FF00FFull;
+            v = (v | (v >> 8)) & 0x0000FFFF0000FFFFull;
+            const uint32_t w = (uint32_t)(v | (v >> 16));
+            std::memcpy(out + i, &w, 4);
+        }
+        for (; i < full; ++i, in += 2) {
+            out[i] = (uint8_t)(in[0] | (in[1] << 4));
+            acc |= (uint64_t)(in[0] | in[1]);
+        }
+        for (; i < hi; ++i, in += 2) {  // the odd last symbol
+            out[i] = in[0];
+            acc |= in[0];
+        }
+        if (acc & 0xF0F0F0F0F0F0F0F0ull) orAll.fetch_or(1, std::memory_order_relaxed);
+        if (hipMemcpyAsync(c->nibPats.ptr + lo, out + lo, hi - lo, hipMemcpyHostToDevice, c->st) != hipSuccess)
+            failed.store(1);
+    };
+    auto worker = [&](unsigned t) {  // pieces t, t + nt, ...: the DMA queue fills front to back
+        for (size_t k = t; k < pieces; k += nt) pack(k * kPiece, std::min(nb, (k + 1) * kPiece));
+    };
+    std::vector<std::thread> ts;
+    for (unsigned t = 1; t < nt && t < pieces; ++t) ts.emplace_back(worker, t);
+    worker(0);
+    for (auto& t : ts) t.join();
+    if (failed.load()) throw Error("pattern upload failed");
+    launchUnpackNibbles(c->nibPats.ptr, dst, n, c->st);
+    return orAll.load() == 0;
+}
+
 void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l,
            const uint32_t* u, uint32_t ns, int edit) {
     if (npat == 0) throw Error("no patterns");
@@ -267,7 +340,10 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
     {
         DevBuf<uint8_t>& raw = c->rawPats;  // kept: no 2 GB allocate / free per call at C3
         raw.reserve(npat * m);
-        SH_HIP(hipMemcpyAsync(raw.ptr, ranks, npat * m, hipMemcpyHostToDevice, c->st));
+        if (!stageIn(c, raw.ptr, ranks, npat * m)) {
+            c->staged = false;
+            throw Error("pattern rank out of range for this index");
+        }
         c->pats.reserve(npat * c->patWords + 4);  // + tail words read by paired loads
         SH_HIP(hipMemsetAsync(c->small.ptr, 0, sizeof(uint32_t), c->st));
         launchPackPatterns(raw.ptr, npat, m, c->patWords, c->I.sigma, c->pats.ptr, c->small.ptr, c->st);

@@ -125,6 +125,8 @@ void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const
                         hipStream_t st);
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st);
+// n symbols, two per byte of nib (low nibble first) -> one per byte of dst
+void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream_t st);
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                   hipStream_t st);
 // locate + canonical order, per batch: querySegments (rows per query ->

@@ -1503,6 +1503,31 @@ void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const
     SH_HIP(hipGetLastError());
 }
 
+// Host upload format -> one byte per symbol: byte i of `nib` holds symbols 2i
+// (low nibble) and 2i + 1 (high nibble). A thread expands 8 bytes into 16.
+__global__ void kUnpackNibbles(const uint8_t* __restrict__ nib, uint8_t* __restrict__ dst, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w * 16 < n; w += stride) {
+        if (w * 16 + 16 <= n) {
+            const uint64_t x = *reinterpret_cast<const uint64_t*>(nib + w * 8);
+            uint32_t o[4];
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t b = (uint32_t)(x >> (16 * q));   // two packed bytes -> four symbols
+                o[q] = (b & 0xFu) | ((b >> 4) & 0xFu) << 8 | ((b >> 8) & 0xFu) << 16 | ((b >> 12) & 0xFu) << 24;
+            }
+            *reinterpret_cast<uint4*>(dst + w * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (uint64_t i = w * 16; i < n; ++i) dst[i] = (nib[i >> 1] >> ((i & 1) * 4)) & 0xFu;
+        }
+    }
+}
+
+void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>((n / 16 + 256) / 256, 65536);
+    hipLaunchKernelGGL(kUnpackNibbles, dim3((unsigned)blocks), dim3(256), 0, st, nib, dst, n);
+    SH_HIP(hipGetLastError());
+}
+
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st) {
     const uint64_t blocks = std::min<uint64_t>((npat * patWords + 255) / 256, 65536);

@@ -290,3 +290,30 @@ def test_kmer_depths_and_seed_tasks(gpu_device, monkeypatch, kmer):
     assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want)
     monkeypatch.setenv("SAHARA_SEED_TASKS", "0")
     assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want)
+
+
+def test_nibble_upload_matches_byte_upload(gpu_device, monkeypatch):
+    """Inputs of >= 64M symbols cross PCIe two symbols per byte (capi.cpp
+    stageIn) and are expanded on the device: the hits equal those of the
+    byte-for-byte upload (SAHARA_NIBBLE_UPLOAD=0), at an odd pattern length
+    and an odd pattern count (a lone last nibble). A byte of 16 or more is no
+    rank of any alphabet and is refused like any out-of-range rank."""
+    flat, lens = sa.synth_reference([600_000, 400_000], sigma=6, seed=5)
+    reads = sa.synth_reads(flat, lens, 350_000, 101, 2, sigma=6, seed=13)
+    pats = np.ascontiguousarray(sa.interleave_rc(reads, 6)[:-1])
+    assert pats.size >= 64 << 20 and pats.size % 2 == 1
+    sch = sa.search_scheme("h2-k2", 0, 2, 101)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    monkeypatch.setenv("SAHARA_NIBBLE_UPLOAD", "1")
+    got = hits_as_rows(sa.search(gpu, pats, sch))
+    monkeypatch.setenv("SAHARA_NIBBLE_UPLOAD", "0")
+    want = hits_as_rows(sa.search(gpu, pats, sch))
+    assert len(want) >= len(pats) // 2 and np.array_equal(got, want)
+    monkeypatch.setenv("SAHARA_NIBBLE_UPLOAD", "1")
+    bad = pats.copy()
+    bad[-1, -1] = 17
+    with pytest.raises(Exception, match="out of range"):
+        sa.search(gpu, bad, sch)
+    bad[-1, -1] = 7  # a nibble, but no rank of sigma 6: the device check
+    with pytest.raises(Exception, match="out of range"):
+        sa.search(gpu, bad, sch)
