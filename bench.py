@@ -47,6 +47,9 @@ CONFIGS = {
 
 METRIC = "reads/s at k=2 edit, 10M×100bp vs 3Gbp index; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# wave64 VALU instructions per second: 256 CUs x 4 SIMDs x 2.4 GHz, one
+# instruction per SIMD every 2 cycles (MI355X_MICROARCH.md: 32 lanes/cycle)
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 
 
 def log(*a):
@@ -93,6 +96,12 @@ def main():
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host buffers) pass")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed RCCL gather of hit records")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the full-size checks (origin recall; GPU suffix array against the text)")
+    ap.add_argument("--no-ref-path", action="store_true",
+                    help="skip the timed reference-execution pass (FM ranks from the root + LF locate)")
+    ap.add_argument("--execution", default="default", choices=["default", "reference"],
+                    help="reference: the timed steps run the reference's execution model (profiling its kernels)")
     ap.add_argument("--traffic-json", default=None,
                     help="measured HBM bytes per launch per kernel (tools/traffic.sh + tools/traffic_summary.py); "
                          "default profiles/traffic_<config>.json when it exists")
@@ -131,13 +140,16 @@ def main():
     t = time.time()
     # exactly k errors per read, of uniform type S/I/D for edit
     # distance and substitutions for Hamming (C2)
-    reads = sa.synth_reads(flat, lens, nreads, rlen, k if edit else 0, sigma=sigma, seed=7 + 1000003 * rank,
-                           substitutions=0 if edit else k)
+    reads, origin = sa.synth_reads(flat, lens, nreads, rlen, k if edit else 0, sigma=sigma, seed=7 + 1000003 * rank,
+                                   substitutions=0 if edit else k, with_origin=True)
     pats = sa.interleave_rc(reads, sigma)
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
     idx.stage(pats, scheme, edit=edit)
     log(f"rank {rank}: {nreads} reads (+RC) simulated and staged in HBM ({time.time()-t:.1f}s), "
         f"{scheme[0].shape[0]} searches")
+    if args.execution == "reference":  # profiling aid: the timed steps are the reference's execution model
+        idx.set_mode(verify=False, locate_sa=False)
+        args.no_count = args.no_ref_path = True
 
     def barrier():
         if world > 1:
@@ -168,14 +180,32 @@ def main():
     digest = idx.digest()
 
     gather = None
+    per_rank = None
     if world > 1:
-        from sahara_amd.dist import max_over_ranks, sum_over_ranks
+        from sahara_amd.dist import max_over_ranks, sum_over_ranks, values_of_ranks
+        per_rank = {"index_build_s": [round(v, 2) for v in values_of_ranks(build_s, device="cuda")],
+                    "ms_per_step": [round(v * 1e3 / args.steps, 3) for v in values_of_ranks(elapsed, device="cuda")],
+                    "hits": [int(v) for v in values_of_ranks(nh, device="cuda")]}
         elapsed = max_over_ranks(elapsed, device="cuda")  # RCCL over xGMI
         total_hits = sum_over_ranks(nh, device="cuda")
         if not args.no_gather:
             gather = gather_step(idx, nh, nreads, world, rank, barrier, dist, torch)
     else:
         total_hits = nh
+
+    # full-size checks that do not lean on the GPU's own index: every read is
+    # found where it was sampled (all ranks), and rank 0 checks the whole GPU
+    # suffix array, BWT and samples against the synthetic text with torch ops
+    checks = {}
+    if not args.no_verify:
+        t = time.time()
+        checks["origin_recall"] = origin_recall(idx.fetch(), origin, k)
+        if world > 1:
+            from sahara_amd.dist import values_of_ranks
+            checks["origin_recall"] = min(values_of_ranks(checks["origin_recall"], device="cuda"))
+        if rank == 0:
+            checks.update(verify_index(idx, flat, lens, torch, f"cuda:{local}"))
+        log(f"rank {rank}: full-size checks {checks} ({time.time()-t:.1f}s)")
 
     ms_per_step = elapsed * 1000.0 / args.steps
     reads_per_s = nreads * world * args.steps / elapsed
@@ -245,6 +275,21 @@ def main():
                 roofline["traffic"] = tr["bytes_per_launch"]
                 roofline["traffic_GBs"] = tr["traffic_GBs"]
                 roofline["traffic_source"] = os.path.relpath(tj, ROOT)
+        # the bound that applies to kSearchText: VALU issue. Its instruction
+        # count per launch comes from the committed SQ counter pass of the
+        # same build and workload (tools/pmc_text.sh -> profiles/pmc_<config>.json)
+        pj = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pj):
+            pm = json.load(open(pj)).get(dom)
+            if pm and pm.get("SQ_INSTS_VALU"):
+                roofline["valu_issue"] = {
+                    "valu_per_launch": pm["SQ_INSTS_VALU"],
+                    "frac": round(pm["SQ_INSTS_VALU"] / (launch_ms / 1e3) / VALU_ISSUE_PEAK, 3),
+                    "peak_per_s": VALU_ISSUE_PEAK,
+                    "basis": "wave64 VALU instructions per launch / (launch time x 256 CU x 4 SIMD x 2.4 GHz / 2 "
+                             "cycles per instruction)",
+                    **{kk: v for kk, v in pm.items() if kk != "SQ_INSTS_VALU"},
+                    "source": os.path.relpath(pj, ROOT)}
         extra = {"bytes_per_read": round((search_bytes + text_bytes + locate_bytes) / nreads, 1),
                  "kernels": {n: {"ms": v["ms"], "algorithmic_GBs": v["GBs"],
                                  "bytes_per_read": round(v["bytes"] / nreads, 1)} for n, v in kern.items()},
@@ -275,19 +320,22 @@ def main():
                                          "same_hits": ref_cnt["hits"] == cnt["hits"]},
                  }
 
-    # PCIe-inclusive rate (SURVEY §8(d)'s definition; not `value`): host ranks
-    # in, located hits in host memory, through sahara_gpu_search
-    if rank == 0 and not args.no_e2e:
-        t = time.perf_counter()
-        h = sa.search(idx, pats, scheme, edit=edit)
-        dt = time.perf_counter() - t
-        st = idx.stats()
-        extra["pcie_inclusive"] = {
-            "reads_per_s": round(nreads / dt, 1), "ms": round(dt * 1e3, 1), "hits": int(len(h)),
-            "stage_ms": round(st["stage_ms"], 1), "search_ms": round(st["total_ms"], 1),
-            "output_ms": round(st["output_ms"], 1),
-            "path": "sahara_gpu_search from host ranks: H2D + pack, search, locate, sort, hits D2H into host memory"}
-        del h
+    # PCIe-inclusive rate (not `value`): SURVEY §8(d)'s search wall time, host
+    # ranks in through located hits in host memory (sahara_gpu_search), timed
+    # like `value`: warmup calls, then --steps calls, each handing its hit
+    # buffer back before the next (sahara_gpu_free)
+    if not args.no_e2e:
+        extra["pcie_inclusive"] = pcie_inclusive(sa, idx, pats, scheme, edit, nreads, args.steps,
+                                                 min(args.warmup, 2), world, barrier, nh)
+    # the reference's execution model timed on the same reads (north_star's
+    # kernels: the FM DFS ranking every node from the root, LF walks to the
+    # rate-16 samples); its roofline is SURVEY §8(d)'s B_read
+    if not args.no_ref_path and ref_cnt:
+        extra["reference_path"] = reference_path(idx, ref_cnt, nreads, pats.size, min(args.steps, 3), world,
+                                                 barrier, args.config)
+    extra.update(checks)
+    if per_rank:
+        extra["per_rank"] = per_rank
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -355,6 +403,213 @@ def gather_step(idx, nh, nreads, world, rank, barrier, dist, torch, device="cuda
     return {"ms": round(el * 1e3, 2), "records": nrec, "bytes": nrec * 24,
             "GBs_into_rank0": round(nrec * 24 / el / 1e9, 1), "verified": ok,
             "collective": "all_gather of counts + gather of padded 24-B records to rank 0 (RCCL over xGMI)"}
+
+
+def origin_recall(h, origin, k):
+    """Fraction of reads with a forward-strand hit (qid 2i) in the record they
+    were sampled from, within k positions of the sampled start (a leading
+    I or D moves the reported start by up to k) and with at most k errors."""
+    fwd = h[(h["qid"] & np.uint64(1)) == 0]
+    read = (fwd["qid"] >> np.uint64(1)).astype(np.int64)
+    ok = ((fwd["seq_id"].astype(np.uint64) == origin[read, 0]) & (fwd["err"] <= k) &
+          (np.abs(fwd["pos"].astype(np.int64) - origin[read, 1].astype(np.int64)) <= k))
+    found = np.zeros(len(origin), bool)
+    found[read[ok]] = True
+    return float(found.mean())
+
+
+def verify_index(idx, flat, lens, torch, dev, W=21):
+    """Checks the GPU-built forward index of the bench text row by row,
+    independently of the code that built it (torch ops on the device):
+
+    - the suffix array is strictly increasing in suffix order over all n rows
+      (adjacent suffixes compared 21 symbols at a time as 63-bit keys; '$' is
+      rank 0 and a suffix that ends sorts before its extensions, as
+      oracle/oracle.cpp suffixArray) with every entry < n — so it is the
+      suffix array of the text;
+    - BWT[i] == T[SA[i] - 1] for every row (index.cpp:87's BWT);
+    - the sampled-row bits and the samples are exactly the rows whose text
+      position is a multiple of the rate within its record or a delimiter,
+      in row order, i.e. the row -> position -> row
+      round trip of LocateLinear;
+    - C[] and the symbol counts of the reverse BWT match the text's."""
+    t0 = time.time()
+    inf = idx.info()
+    n, rate = int(inf["n"]), int(inf["sampling_rate"])
+    ex = idx.export()
+    sa_h = idx.export_sa()
+    lens64 = np.asarray(lens, np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens64 + 1)]).astype(np.int64)
+    mask = 0xFFFFFFFF
+    # text ranks + 1 ('$' = 1, past the end = 0)
+    Tp = torch.zeros(n + 4 * W, dtype=torch.uint8, device=dev)
+    off = 0
+    for r, L in enumerate(lens64.tolist()):
+        s = int(starts[r])
+        Tp[s:s + L] = torch.from_numpy(flat[off:off + L]).to(dev) + 1
+        Tp[s + L] = 1
+        off += L
+    CH = 1 << 27
+    K = torch.empty(n + 2 * W, dtype=torch.int64, device=dev)
+    for s in range(0, n + 2 * W, CH):
+        e = min(n + 2 * W, s + CH)
+        kk = torch.zeros(e - s, dtype=torch.int64, device=dev)
+        for j in range(W):
+            kk = (kk << 3) | Tp[s + j:e + j].to(torch.int64)
+        K[s:e] = kk
+    del kk
+    sa_d = torch.from_numpy(sa_h.view(np.int32)).to(dev)
+    del sa_h
+    bwt_d = torch.from_numpy(ex["bwt_f"]).to(dev)
+    words = torch.from_numpy(ex["sampled"].view(np.int64)).to(dev)
+    samples_d = torch.from_numpy(ex["samples"].view(np.int32)).to(dev)
+    starts_d = torch.from_numpy(starts).to(dev)
+    ok = {"sa_sorted": True, "sa_in_range": True, "bwt": True, "samples": True}
+    seen = 0
+    max_lcp = 0
+    for s in range(0, n, CH):
+        e = min(n, s + CH)
+        a = sa_d[s:e].to(torch.int64) & mask
+        if bool((a >= n).any()):
+            ok["sa_in_range"] = False
+            break
+        prev = torch.where(a == 0, torch.full_like(a, n - 1), a - 1)
+        if not torch.equal(Tp[prev].to(torch.int16) - 1, bwt_d[s:e].to(torch.int16)):
+            ok["bwt"] = False
+        del prev
+        # sampled rows: in-record offset a multiple of the rate, or the delimiter
+        rec = torch.searchsorted(starts_d, a, right=True) - 1
+        offr = a - starts_d[rec]
+        want = ((offr % rate) == 0) | (offr == starts_d[rec + 1] - starts_d[rec] - 1)
+        rows = torch.arange(s, e, device=dev, dtype=torch.int64)
+        bit = ((words[rows >> 6] >> (rows & 63)) & 1).bool()
+        if not torch.equal(bit, want):
+            ok["samples"] = False
+        pos = a[want]
+        if not torch.equal(samples_d[seen:seen + pos.numel()].to(torch.int64) & mask, pos):
+            ok["samples"] = False
+        seen += pos.numel()
+        del rec, offr, want, rows, bit, pos
+        # adjacent rows (i, i + 1) for i in [s, min(e, n - 1))
+        b = sa_d[s + 1:min(n, e + 1)].to(torch.int64) & mask
+        x = a[:b.numel()]
+        d = 0
+        while x.numel():
+            ka = K[torch.clamp(x + d, max=n)]
+            kb = K[torch.clamp(b + d, max=n)]
+            if bool((ka > kb).any()):
+                ok["sa_sorted"] = False
+                break
+            eq = ka == kb
+            x, b = x[eq], b[eq]
+            d += W
+            if d > 200 * W:
+                ok["sa_sorted"] = False
+                break
+        max_lcp = max(max_lcp, d)
+        del a, b, x
+    ok["samples"] = ok["samples"] and seen == len(ex["samples"])
+    cnt = torch.bincount(Tp[:n], minlength=8).cpu().numpy()[1:].astype(np.uint64)  # per rank
+    sigma = int(inf["sigma"])
+    C = np.concatenate([[0], np.cumsum(cnt[:sigma])]).astype(np.uint64)
+    ok["C"] = bool(np.array_equal(C, ex["C"][:sigma + 1].astype(np.uint64)))
+    rc = torch.bincount(torch.from_numpy(ex["bwt_r"]).to(dev), minlength=sigma).cpu().numpy()[:sigma].astype(np.uint64)
+    ok["bwt_r_counts"] = bool(np.array_equal(rc, cnt[:sigma]))
+    del Tp, K, sa_d, bwt_d, words, samples_d, starts_d
+    torch.cuda.empty_cache()
+    out = {"sa_probe_ok": all(ok.values()), "index_checks": ok, "index_check_rows": n,
+           "index_check_s": round(time.time() - t0, 1), "index_check_max_lcp_blocks": max_lcp // W}
+    return out
+
+
+def pcie_inclusive(sa, idx, pats, scheme, edit, nreads, steps, warmup, world, barrier, local_hits):
+    """sahara_gpu_search from host ranks to located hits in host memory (SURVEY
+    §8(d)'s search wall time), timed over `steps` calls after `warmup` calls.
+    Each call's hit buffer is released (sahara_gpu_free) before the next."""
+    n = 0
+    for _ in range(warmup):
+        h = sa.search(idx, pats, scheme, edit=edit)
+        n = len(h)
+        del h
+    barrier()
+    t0 = time.perf_counter()
+    acc = {"stage_ms": 0.0, "total_ms": 0.0, "output_ms": 0.0}
+    for _ in range(steps):
+        h = sa.search(idx, pats, scheme, edit=edit)
+        st = idx.stats()
+        for kk in acc:
+            acc[kk] += st[kk]
+        n = len(h)
+        del h
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        from sahara_amd.dist import max_over_ranks
+        el = max_over_ranks(el, device="cuda")
+    return {"reads_per_s": round(nreads * world * steps / el, 1), "ms_per_step": round(el * 1e3 / steps, 2),
+            "steps": steps, "warmup": warmup, "hits": int(n), "same_hits": int(n) == int(local_hits),
+            "stage_ms": round(acc["stage_ms"] / steps, 2), "search_ms": round(acc["total_ms"] / steps, 2),
+            "output_ms": round(acc["output_ms"] / steps, 2),
+            "path": "sahara_gpu_search from host ranks: H2D + pack, search, locate, sort, hits D2H into host "
+                    "memory (pinned, recycled through sahara_gpu_free)"}
+
+
+def reference_path(idx, ref_cnt, nreads, pat_bytes, steps, world, barrier, config):
+    """The reference's execution model on the same staged reads: every DFS node
+    ranked on the FM-index from the root (kSearchFM, no k-mer table, no text
+    phase) and LocateLinear's LF walk to the rate-16 samples (kLocate<false>).
+    Its roofline is SURVEY §8(d)'s B_read over HBM peak."""
+    idx.set_mode(verify=False, locate_sa=False)
+    try:
+        idx.run()
+        barrier()
+        t0 = time.perf_counter()
+        launches = 0
+        for _ in range(steps):
+            idx.run()
+            launches += idx.stats()["search_launches"]
+        barrier()
+        el = time.perf_counter() - t0
+    finally:
+        idx.set_mode(verify=True, locate_sa=True)
+    if world > 1:
+        from sahara_amd.dist import max_over_ranks
+        el = max_over_ranks(el, device="cuda")
+    rps = nreads * world * steps / el
+    fm_bytes = 64.0 * ref_cnt["ext_lines"] + pat_bytes        # per step: Occ lines + query bytes
+    loc_bytes = 64.0 * (ref_cnt["lf_steps"] + ref_cnt["hits"])  # LF lines + one SA-sample line per row
+    b_read = (fm_bytes + loc_bytes) / nreads
+    per_gpu = b_read * rps / world / 1e9
+    out = {"reads_per_s": round(rps, 1), "ms_per_step": round(el * 1e3 / steps, 2), "steps": steps,
+           "B_read": round(b_read, 1),
+           "roofline": {"bound": "hbm", "achieved": round(per_gpu, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(per_gpu / HBM_PEAK_GBS, 4),
+                        "basis": "SURVEY 8(d) B_read (64 B per Occ line ranked, per LF step and per SA-sample "
+                                 "line, + query bytes) x reads/s per GPU, over the whole step"},
+           "kernels": {"kSearchFM": {"launches_per_step": launches // steps,
+                                     "algorithmic_bytes_per_step": round(fm_bytes)},
+                       "kLocate": {"algorithmic_bytes_per_step": round(loc_bytes)}},
+           "mode": "set_mode(verify=0, locate_sa=0)"}
+    # per-launch durations and FETCH_SIZE of both kernels from the committed
+    # profile of this mode (tools/traffic_ref.sh: rocprofv3 kernel trace +
+    # FETCH_SIZE pass of `bench.py --execution reference`)
+    tj = os.path.join(ROOT, "profiles", f"traffic_{config}_ref.json")
+    if os.path.exists(tj):
+        tr = json.load(open(tj))
+        for kn in ("kSearchFM", "kLocate"):
+            if kn in tr:
+                kk = out["kernels"][kn]
+                per_step = kk["algorithmic_bytes_per_step"]
+                kk.update({"avg_launch_us": tr[kn]["avg_launch_us"], "launches_per_step_profiled":
+                           tr[kn]["dispatches"] / tr.get("steps", 1),
+                           "traffic_bytes_per_launch": tr[kn]["bytes_per_launch"],
+                           "traffic_GBs": tr[kn]["traffic_GBs"]})
+                launches_k = tr[kn]["dispatches"] / tr.get("steps", 1)
+                alg = per_step / max(launches_k, 1)
+                kk["algorithmic_GBs"] = round(alg / (tr[kn]["avg_launch_us"] / 1e6) / 1e9, 1)
+                kk["frac"] = round(kk["algorithmic_GBs"] / HBM_PEAK_GBS, 4)
+        out["traffic_source"] = os.path.relpath(tj, ROOT)
+    return out
 
 
 def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):

@@ -11,7 +11,8 @@
  *       src/sahara/search.cpp:218-231           -> sahara_gpu_search (search half)
  *   - fmc::LocateLinear{index, cursor}
  *       src/sahara/search.cpp:244-250           -> sahara_gpu_search (locate half)
- *   - search_n (--max_hits)  src/sahara/search.cpp:228,231 -> max_hits argument (reserved, must be 0 this round)
+ *   - search_n (--max_hits)  src/sahara/search.cpp:228,231 -> max_hits argument of sahara_gpu_search
+ *   - search_ng21::search_best[_n]  src/sahara/search.cpp:233-241 -> sahara_gpu_search_best
  *
  * Conventions: plain C types only; 0 on success, negative on error with a
  * thread-local message from sahara_gpu_last_error(); no exceptions cross the
@@ -163,6 +164,10 @@ int  sahara_gpu_copy_hits(void* ctx, void* dst_device, uint64_t capacity, uint64
 int  sahara_gpu_digest(void* ctx, uint64_t* digest);
 int  sahara_gpu_stats(void* ctx, sahara_stats* stats);
 
+/* Releases a hit buffer returned by sahara_gpu_search / sahara_gpu_search_best.
+ * Large buffers (>= 64 MB) are page-locked host memory; freeing one hands it
+ * back to a small process-wide pool, so the next search of a similar size
+ * writes into memory that is already pinned and faulted in. */
 void sahara_gpu_free(void* p);
 void sahara_gpu_close(void* ctx);
 

@@ -14,7 +14,9 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <mutex>
 #include <random>
+#include <unordered_map>
 #include <string>
 #include <atomic>
 #include <thread>
@@ -1017,16 +1019,83 @@ int sahara_gpu_stats(void* ctx, sahara_stats* stats) {
     return guarded([&] { *stats = ctxOf(ctx)->stats; });
 }
 
-// Host buffer for n hits, freed with std::free (sahara_gpu_free). Large ones
-// are 2 MB-aligned and asked for transparent huge pages: the copy-in then
-// takes one page fault per 2 MB instead of one per 4 KB.
-static void* allocHits(uint64_t n) {
+// Hit buffers handed to the caller. Buffers of >= 64 MB are page-locked
+// (hipHostMalloc), so the device-to-host copy runs at the link's rate straight
+// into them, and sahara_gpu_free hands them back to a small pool instead of
+// unpinning them: pinning (and first-touching) 0.6 GB costs more than copying
+// into it, and a fresh box without transparent huge pages paid 28.6 ms for
+// the page faults of a pageable buffer against 13 ms for the copy.
+struct HitPool {
+    std::mutex mu;
+    std::unordered_map<void*, size_t> live;       // pinned buffers the callers hold
+    std::vector<std::pair<void*, size_t>> idle;   // pinned buffers ready for reuse
+    static constexpr size_t kKeep = 2;
+};
+static HitPool& hitPool() {
+    static HitPool* p = new HitPool;  // never destroyed: callers may free after static destructors ran
+    return *p;
+}
+
+// Host buffer for n hits (released with sahara_gpu_free); *pinned tells
+// whether the device can copy into it directly.
+static void* allocHits(uint64_t n, bool* pinned) {
     const size_t bytes = std::max<uint64_t>(n, 1) * sizeof(sahara_hit);
+    *pinned = false;
     if (bytes < (64u << 20)) return std::malloc(bytes);
-    const size_t huge = 2u << 20, rounded = (bytes + huge - 1) / huge * huge;
-    void* p = std::aligned_alloc(huge, rounded);
-    if (p) (void)madvise(p, rounded, MADV_HUGEPAGE);
+    HitPool& P = hitPool();
+    std::vector<void*> unpin;
+    void* p = nullptr;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        size_t best = SIZE_MAX;
+        for (size_t i = 0; i < P.idle.size(); ++i)
+            if (P.idle[i].second >= bytes && (best == SIZE_MAX || P.idle[i].second < P.idle[best].second)) best = i;
+        if (best != SIZE_MAX) {
+            p = P.idle[best].first;
+            P.live[p] = P.idle[best].second;
+            P.idle.erase(P.idle.begin() + (long)best);
+        } else {  // none fits: the smaller idle ones will not fit later calls of this size either
+            for (auto& e : P.idle) unpin.push_back(e.first);
+            P.idle.clear();
+        }
+    }
+    for (void* q : unpin) (void)hipHostFree(q);
+    if (p) {
+        *pinned = true;
+        return p;
+    }
+    const size_t huge = 2u << 20, cap = (bytes + bytes / 8 + huge - 1) / huge * huge;  // room for a run with more hits
+    if (hipHostMalloc(&p, cap, hipHostMallocPortable) == hipSuccess && p) {
+        std::lock_guard<std::mutex> g(P.mu);
+        P.live[p] = cap;
+        *pinned = true;
+        return p;
+    }
+    (void)hipGetLastError();
+    p = std::aligned_alloc(huge, (bytes + huge - 1) / huge * huge);  // pageable fallback
+    if (p) (void)madvise(p, (bytes + huge - 1) / huge * huge, MADV_HUGEPAGE);
     return p;
+}
+
+static void freeHits(void* p) {
+    if (!p) return;
+    HitPool& P = hitPool();
+    void* drop = nullptr;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto it = P.live.find(p);
+        if (it == P.live.end()) {
+            std::free(p);
+            return;
+        }
+        P.idle.emplace_back(p, it->second);
+        P.live.erase(it);
+        if (P.idle.size() > HitPool::kKeep) {
+            drop = P.idle.front().first;
+            P.idle.erase(P.idle.begin());
+        }
+    }
+    if (drop) (void)hipHostFree(drop);
 }
 
 // memcpy from several threads (host copies out of the pinned staging chunks)
@@ -1085,13 +1154,19 @@ int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint
             limitHits(v, max_hits);
             handOver(v, hits, n_hits);
         } else {  // straight into the caller-owned buffer
-            auto* buf = static_cast<sahara_hit*>(allocHits(c->nout));
+            bool pinned = false;
+            auto* buf = static_cast<sahara_hit*>(allocHits(c->nout, &pinned));
             if (!buf) throw Error("out of host memory for hits");
             if (c->nout) {
                 try {
-                    copyOut(c, buf, c->out.ptr, c->nout * sizeof(sahara_hit));
+                    if (pinned) {
+                        SH_HIP(hipMemcpyAsync(buf, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost, c->st));
+                        SH_HIP(hipStreamSynchronize(c->st));
+                    } else {
+                        copyOut(c, buf, c->out.ptr, c->nout * sizeof(sahara_hit));
+                    }
                 } catch (...) {
-                    std::free(buf);
+                    freeHits(buf);
                     throw;
                 }
             }
@@ -1152,7 +1227,7 @@ int sahara_gpu_search_best(void* ctx, const uint8_t* ranks, uint64_t n_patterns,
     });
 }
 
-void sahara_gpu_free(void* p) { std::free(p); }
+void sahara_gpu_free(void* p) { freeHits(p); }
 
 void sahara_gpu_close(void* ctx) {
     if (!ctx) return;

@@ -114,6 +114,18 @@ def max_over_ranks(x: float, device="cpu") -> float:
     return float(t.item())
 
 
+def values_of_ranks(x: float, device="cpu") -> list[float]:
+    """Every rank's value of x, in rank order (per-rank timings: a slow or
+    imbalanced rank shows up by name the first time N GPUs run)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def sum_over_ranks(x: int, device="cpu") -> int:
     import torch
     import torch.distributed as dist

@@ -1,0 +1,110 @@
+"""bench.py's full-size checks, run on CPU against the oracle's index.
+
+bench.verify_index checks the GPU index of the 3 Gbp bench text with torch
+ops (suffix order of every adjacent row pair, BWT, samples, C); here the same
+function runs on torch's CPU device over an index the CPU restatement built,
+and must pass it and catch planted corruptions. bench.origin_recall is held
+to reads simulated with their origins.
+"""
+import sys
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import sahara_amd as sa
+from helpers import hits_as_rows
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+class _OracleIdx:
+    """The three BiFMIndex calls verify_index makes, served from the oracle."""
+
+    def __init__(self, ref, lens, sigma=6, rate=16, corrupt=None):
+        self.ex = ref.export()
+        self.lens, self.sigma, self.rate = lens, sigma, rate
+        if corrupt:
+            corrupt(self.ex)
+
+    def info(self):
+        return {"n": len(self.ex["bwt_f"]), "sampling_rate": self.rate, "sigma": self.sigma}
+
+    def export(self):
+        e = dict(self.ex)
+        e["C"] = e["C"][: self.sigma + 1]
+        return e
+
+    def export_sa(self):
+        return self.ex["sa"].copy()
+
+
+def _text(seed=3, lengths=(3000, 17, 900, 2500)):
+    flat, lens = sa.synth_reference(list(lengths), sigma=6, seed=seed)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return flat, lens, [flat[offs[i]:offs[i + 1]] for i in range(len(lens))]
+
+
+def test_verify_index_passes_on_a_correct_index():
+    flat, lens, recs = _text()
+    ref = O.Index.build(recs, 6, 16)
+    out = bench.verify_index(_OracleIdx(ref, lens), flat, lens, torch, "cpu", W=5)
+    assert out["sa_probe_ok"], out
+    assert out["index_check_rows"] == len(flat) + len(lens)
+
+
+def test_verify_index_repetitive_text_needs_many_key_blocks():
+    flat, lens, recs = _text()
+    flat[:2000] = 1  # long poly-A run (recs are views of flat): adjacent suffixes agree for hundreds of symbols
+    ref = O.Index.build(recs, 6, 16)
+    out = bench.verify_index(_OracleIdx(ref, lens), flat, lens, torch, "cpu", W=21)
+    assert out["sa_probe_ok"], out
+    assert out["index_check_max_lcp_blocks"] > 50
+
+
+def _swap_sa(ex):
+    ex["sa"][[100, 2000]] = ex["sa"][[2000, 100]]
+
+
+def _bwt(ex):
+    ex["bwt_f"][77] = 1 if ex["bwt_f"][77] != 1 else 2
+
+
+def _sample(ex):
+    ex["samples"][5] += 1
+
+
+def _bit(ex):
+    ex["sampled"][3] ^= np.uint64(1 << 9)
+
+
+def _c(ex):
+    ex["C"][2] += 1
+
+
+@pytest.mark.parametrize("corrupt,key", [(_swap_sa, "sa_sorted"), (_bwt, "bwt"), (_sample, "samples"),
+                                         (_bit, "samples"), (_c, "C")])
+def test_verify_index_catches_corruption(corrupt, key):
+    flat, lens, recs = _text()
+    ref = O.Index.build(recs, 6, 16)
+    out = bench.verify_index(_OracleIdx(ref, lens, corrupt=corrupt), flat, lens, torch, "cpu", W=5)
+    assert not out["sa_probe_ok"] and not out["index_checks"][key], out
+
+
+def test_origin_recall():
+    flat, lens, recs = _text(lengths=(200_000, 100_000))
+    reads, origin = sa.synth_reads(flat, lens, 400, 60, 2, sigma=6, seed=9, with_origin=True)
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme("h2-k2", 0, 2, 60)
+    rows = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch, nthreads=4)[0])
+    h = np.zeros(len(rows), sa.HIT_DTYPE)
+    h["qid"], h["seq_id"], h["pos"], h["err"] = rows[:, 0], rows[:, 1], rows[:, 2], rows[:, 3]
+    assert bench.origin_recall(h, origin, 2) == 1.0
+    drop = h[h["qid"] != 10]  # read 5's forward hits gone
+    assert bench.origin_recall(drop, origin, 2) == pytest.approx(399 / 400)
+    moved = h.copy()
+    moved["pos"][moved["qid"] == 10] += 50
+    assert bench.origin_recall(moved, origin, 2) == pytest.approx(399 / 400)
