@@ -137,6 +137,16 @@ int  sahara_gpu_set_mode(void* ctx, int verify, int locate_sa);
 int  sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len,
                        const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,
                        int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits);
+/* The same search from the reads themselves: query ingest's reverse-complement
+ * interleave (search.cpp:121-127) runs on the device, so only the reads cross
+ * PCIe. Qid 2i = read i, 2i + 1 = its reverse complement, as in the
+ * reference's `queries`; reverse == 0 (--no-reverse) searches the reads as
+ * given (qid i = read i). limit > 0 cuts the query list after the interleave
+ * (--limit_queries). Requires a dna4 / dna5 index. Same hits, order and
+ * ownership as sahara_gpu_search over the interleaved patterns. */
+int  sahara_gpu_search_reads(void* ctx, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
+                             uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                             uint32_t n_searches, int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits);
 /* --search_mode besthits (search_ng21::search_best[_n], search.cpp:233-241):
  * n_schemes expanded schemes, scheme j covering exactly j errors, stored one
  * after another in pi/l/u (n_searches[j] rows of len entries each). A pattern's

@@ -20,7 +20,7 @@ import os
 import numpy as np
 
 __all__ = [
-    "BiFMIndex", "HIT_DTYPE", "search", "search_scheme", "scheme_parts", "scheme_generators",
+    "BiFMIndex", "HIT_DTYPE", "search", "search_reads", "search_scheme", "scheme_parts", "scheme_generators",
     "scheme_counts", "synth_reference", "synth_reads", "interleave_rc", "load_fasta",
     "library_path", "lib", "SaharaError", "DNA5", "DNA4",
 ]
@@ -83,6 +83,9 @@ EXPORTED = {
     "sahara_gpu_search": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                     C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_uint64)]),
+    "sahara_gpu_search_reads": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, u32p, u32p,
+                                          u32p, C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_uint64)]),
     "sahara_gpu_search_best": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                          u32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_uint64)]),
@@ -327,6 +330,25 @@ def search(index, queries, scheme, edit=True, max_hits=0):
     _check(lib().sahara_gpu_search(index._h, _p(q, u8p), q.shape[0], q.shape[1], _p(pi, u32p),
                                    _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit), max_hits,
                                    C.byref(out), C.byref(n)))
+    return _hits_array(out, n.value)
+
+
+def search_reads(index, reads, scheme, edit=True, reverse=True, limit=0, max_hits=0):
+    """Query ingest + search + locate in one call (search.cpp:111-127, 218-250):
+    the reverse complements are interleaved on the device (qid 2i = read i,
+    2i + 1 = its reverse complement; reverse=False: qid i = read i), and
+    limit > 0 cuts the query list after the interleave (--limit_queries).
+    Returns the same sorted HIT_DTYPE array as search() over the interleaved
+    patterns."""
+    r = np.ascontiguousarray(reads, dtype=np.uint8)
+    if r.ndim != 2 or r.shape[0] == 0:
+        raise SaharaError("reads must be a non-empty (n_reads, len) array")
+    pi, l, u = (np.ascontiguousarray(a, dtype=np.uint32) for a in scheme)
+    out = C.c_void_p()
+    n = C.c_uint64()
+    _check(lib().sahara_gpu_search_reads(index._h, _p(r, u8p), r.shape[0], r.shape[1], int(reverse), int(limit),
+                                         _p(pi, u32p), _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit), max_hits,
+                                         C.byref(out), C.byref(n)))
     return _hits_array(out, n.value)
 
 

@@ -514,6 +514,9 @@ void help() {
 }  // namespace
 
 int main(int argc, char** argv) {
+    // six streams per device context: their own hardware queues (HIP's default
+    // is 4 per process), set before the first HIP call
+    setenv("GPU_MAX_HW_QUEUES", "8", 0);
     try {
         if (argc < 2 || !std::strcmp(argv[1], "--help") || !std::strcmp(argv[1], "-h")) {
             help();

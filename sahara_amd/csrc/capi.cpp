@@ -5,6 +5,7 @@
 // search + locate (search.cpp:218-250). No C++ types or exceptions cross it.
 
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -14,6 +15,8 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <random>
 #include <unordered_map>
@@ -32,6 +35,64 @@ using namespace sahara;
 namespace {
 
 thread_local std::string g_err;
+
+// Host worker threads of a context (pattern packing for the upload), started
+// once: a streamed upload packs several chunks per call, and fresh threads per
+// chunk measured slower than the link.
+class HostPool {
+public:
+    explicit HostPool(unsigned workers) {
+        for (unsigned i = 1; i <= workers; ++i) ts_.emplace_back([this, i] { loop(i); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : ts_) t.join();
+    }
+    unsigned size() const { return (unsigned)ts_.size() + 1; }
+    // f(t) for every t in [0, size()), t = 0 on the calling thread; f must not throw
+    void run(const std::function<void(unsigned)>& f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &f;
+            pending_ = (unsigned)ts_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(id);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> ts_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    unsigned pending_ = 0;
+    bool stop_ = false;
+};
 
 struct Ctx {
     int device = 0;
@@ -80,6 +141,7 @@ struct Ctx {
     DevBuf<uint8_t> nibPats;              // the same, two symbols per byte as uploaded (stageIn)
     bool nibbleUpload = true;             // SAHARA_NIBBLE_UPLOAD=0: pattern bytes go up as given
     uint8_t* nibHost = nullptr;           // pinned: the packed patterns on their way up
+    const uint8_t* nibDev = nullptr;      // the same memory as the device addresses it
     size_t nibHostCap = 0;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
@@ -94,9 +156,44 @@ struct Ctx {
     sahara_stats stats{};
     hipEvent_t ev[8] = {};
 
+    // Streamed query upload (sahara_gpu_search, sahara_gpu_search_reads): the
+    // source rows go up in chunks, each packed on the host (two symbols per
+    // byte, ranks checked) and enqueued on stream stE when the first batch that
+    // needs it is issued, so that the upload of later batches overlaps the
+    // search of earlier ones. upEv[j] fires once chunk j's patterns are packed
+    // on the device; a batch's seed kernel waits for it.
+    struct Upload {
+        const uint8_t* src = nullptr;  // host symbols: the patterns, or the reads (rc)
+        bool rc = false;               // reads: reverse complements interleaved on the device
+        bool nibble = true;
+        bool zeroCopy = false;         // kUnpackNibbles reads the pinned host buffer (no DMA); else DMA on stE
+        uint64_t rows = 0;             // source rows
+        uint64_t chunk = 0;            // source rows per chunk (even: chunks start at even symbols)
+        uint64_t done = 0;             // source rows enqueued
+        int64_t last = -1;             // chunk of the last event recorded
+        bool bad = false;              // a chunk held a byte that is no rank of this index
+        double hostMs = 0;             // host time spent packing and enqueueing
+    } up;
+    bool streaming = false;
+    hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
+    std::vector<hipEvent_t> upEv;
+    DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
+    DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
+    std::unique_ptr<HostPool> pool;
+    // host sink of sahara_gpu_search: each batch's sorted hits go to host
+    // memory (pinned) on stF while later batches search
+    sahara_hit* sink = nullptr;
+    uint64_t sinkCap = 0, sinkDone = 0;
+    bool sinkOk = false;
+    uint64_t lastHits = 0;                // hits of the previous sahara_gpu_search (sink size estimate)
+
     ~Ctx() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& e : upEv)
+            if (e) (void)hipEventDestroy(e);
+        if (stE) (void)hipStreamDestroy(stE);
+        if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
             for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmDone, sl.textStart, sl.textDone, sl.free})
                 if (e) (void)hipEventDestroy(e);
@@ -180,6 +277,8 @@ Ctx* newCtx(int device) {
     SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stD, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stF, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
@@ -282,6 +381,9 @@ static bool stageIn(Ctx* c, uint8_t* dst, const uint8_t* src, size_t n) {
         c->nibHostCap = 0;
         SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->nibHost), nb));
         c->nibHostCap = nb;
+        void* d = nullptr;
+        SH_HIP(hipHostGetDevicePointer(&d, c->nibHost, 0));
+        c->nibDev = static_cast<const uint8_t*>(d);
     }
     c->nibPats.reserve(nb + 8);
     SH_HIP(hipStreamSynchronize(c->st));  // the pinned buffer may still feed the last call's DMA
@@ -329,9 +431,280 @@ static bool stageIn(Ctx* c, uint8_t* dst, const uint8_t* src, size_t n) {
     return orAll.load() == 0;
 }
 
+// Any byte of 8 that is no rank of a sigma-letter alphabet (0, or >= sigma;
+// ivs::verify_rank, search.cpp:118-120): nonzero high bits. Exact: with every
+// byte in [1, 16) the subtraction borrows nowhere and the addition carries
+// out of no byte.
+static inline uint64_t badRanks8(uint64_t v, uint64_t big) {
+    constexpr uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
+    return (v & 0xF0F0F0F0F0F0F0F0ull) | ((v - ones) & ~v & highs) | ((v + big) & highs);
+}
+
+// Symbols [2 lo, 2 hi) of src (one per byte) -> bytes [lo, hi) of out, two per
+// byte (low nibble first); nsym = all symbols of the upload (an odd last one
+// is packed alone). Returns nonzero if any symbol is no rank in [1, sigma).
+static uint64_t packNibblesScalar(const uint8_t* src, uint8_t* out, uint64_t lo, uint64_t hi, uint64_t nsym,
+                                  uint32_t sigma) {
+    const uint64_t big = (uint64_t)(0x80u - sigma) * 0x0101010101010101ull;
+    const uint64_t full = std::min(hi, nsym / 2);  // bytes with both symbols
+    const uint8_t* in = src + 2 * lo;
+    uint64_t acc = 0, i = lo;
+    for (; i + 4 <= full; i += 4, in += 8) {  // 8 symbols -> 4 bytes
+        uint64_t v;
+        std::memcpy(&v, in, 8);
+        acc |= badRanks8(v, big);
+        v = (v | (v >> 4)) & 0x00FF00FF00FF00FFull;
+        v = (v | (v >> 8)) & 0x0000FFFF0000FFFFull;
+        const uint32_t w = (uint32_t)(v | (v >> 16));
+        std::memcpy(out + i, &w, 4);
+    }
+    for (; i < full; ++i, in += 2) {
+        out[i] = (uint8_t)(in[0] | (in[1] << 4));
+        acc |= (uint64_t)(in[0] == 0 || in[0] >= sigma || in[1] == 0 || in[1] >= sigma);
+    }
+    for (; i < hi; ++i, in += 2) {  // the odd last symbol
+        out[i] = in[0];
+        acc |= (uint64_t)(in[0] == 0 || in[0] >= sigma);
+    }
+    return acc;
+}
+
+// The same with AVX2, 64 symbols per step: pairs combined by one multiply-add
+// (lo * 1 + hi * 16), packed to bytes; ranks checked as max(v - 1, sigma - 2)
+// == sigma - 2. About a tenth of the scalar instructions per byte, so that
+// 16 host threads pack faster than the GPU searches (the streamed upload).
+__attribute__((target("avx2"))) static uint64_t packNibblesAvx2(const uint8_t* src, uint8_t* out, uint64_t lo,
+                                                                uint64_t hi, uint64_t nsym, uint32_t sigma) {
+    const __m256i mult = _mm256_set1_epi16(0x1001), one = _mm256_set1_epi8(1);
+    const __m256i lim = _mm256_set1_epi8((char)(sigma - 2));
+    __m256i bad = _mm256_setzero_si256();
+    const uint64_t full = std::min(hi, nsym / 2);
+    uint64_t i = lo;
+    for (; i + 32 <= full; i += 32) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 2 * i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 2 * i + 32));
+        const __m256i ta = _mm256_sub_epi8(a, one), tb = _mm256_sub_epi8(b, one);
+        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(ta, lim), lim));
+        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(tb, lim), lim));
+        const __m256i pa = _mm256_maddubs_epi16(a, mult), pb = _mm256_maddubs_epi16(b, mult);
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i),
+                            _mm256_permute4x64_epi64(_mm256_packus_epi16(pa, pb), 0xD8));
+    }
+    return (uint64_t)!_mm256_testz_si256(bad, bad) | packNibblesScalar(src, out, i, hi, nsym, sigma);
+}
+
+// Nonzero if any byte of [p, p + n) is no rank in [1, sigma).
+static uint64_t badRanksScalar(const uint8_t* p, uint64_t n, uint32_t sigma) {
+    const uint64_t big = (uint64_t)(0x80u - sigma) * 0x0101010101010101ull;
+    uint64_t acc = 0, i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t v;
+        std::memcpy(&v, p + i, 8);
+        acc |= badRanks8(v, big);
+    }
+    for (; i < n; ++i) acc |= (uint64_t)(p[i] == 0 || p[i] >= sigma);
+    return acc;
+}
+
+__attribute__((target("avx2"))) static uint64_t badRanksAvx2(const uint8_t* p, uint64_t n, uint32_t sigma) {
+    const __m256i one = _mm256_set1_epi8(1), lim = _mm256_set1_epi8((char)(sigma - 2));
+    __m256i bad = _mm256_setzero_si256();
+    uint64_t i = 0;
+    for (; i + 32 <= n; i += 32) {
+        const __m256i t = _mm256_sub_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + i)), one);
+        bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(t, lim), lim));
+    }
+    return (uint64_t)!_mm256_testz_si256(bad, bad) | badRanksScalar(p + i, n - i, sigma);
+}
+
+static bool hostHasAvx2() {
+    static const bool has = __builtin_cpu_supports("avx2");
+    return has;
+}
+
+HostPool& hostPool(Ctx* c) {
+    if (!c->pool) c->pool = std::make_unique<HostPool>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+    return *c->pool;
+}
+
+// Packs the next chunk of the streamed upload (Ctx::Upload) on the host,
+// enqueues its DMA on stE (nothing else: the DMAs run back to back at the
+// link's rate) and, on stream `kst` after the DMA's event, the unpack (and
+// reverse-complement interleave) kernel and both pattern packings. A chunk
+// with a byte that is no rank sets up.bad and enqueues nothing.
+void uploadChunk(Ctx* c, hipStream_t kst) {
+    Ctx::Upload& U = c->up;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t r0 = U.done, r1 = std::min(U.rows, r0 + U.chunk);
+    const uint32_t m = c->m, sigma = c->I.sigma;
+    const uint64_t s0 = r0 * m, s1 = r1 * m, nsym = U.rows * m;  // symbols
+    uint8_t* raw = U.rc ? c->readRaw.ptr : c->rawPats.ptr;
+    HostPool& P = hostPool(c);
+    hipStream_t dst = c->stE;  // (two upload streams, alternating chunks, measured no faster)
+    const unsigned nt = P.size();
+    std::atomic<int> bad{0};
+    // pieces of 1 MB of packed bytes spread over the pool (a chunk at C3 is
+    // ~25 MB packed); one DMA per chunk, overlapping the next chunk's packing
+    constexpr uint64_t kPiece = 1u << 20;
+    const bool avx2 = hostHasAvx2();
+    if (U.nibble) {
+        const uint64_t b0 = s0 / 2, b1 = (s1 + 1) / 2;  // packed bytes (s0 is even)
+        const uint64_t pieces = (b1 - b0 + kPiece - 1) / kPiece;
+        uint8_t* out = c->nibHost;
+        P.run([&](unsigned t) {
+            for (uint64_t k = t; k < pieces; k += nt) {
+                const uint64_t lo = b0 + k * kPiece, hi = std::min(b1, lo + kPiece);
+                const uint64_t acc = avx2 ? packNibblesAvx2(U.src, out, lo, hi, nsym, sigma)
+                                          : packNibblesScalar(U.src, out, lo, hi, nsym, sigma);
+                if (acc) bad.store(1, std::memory_order_relaxed);
+            }
+        });
+        if (!bad.load() && !U.zeroCopy)
+            SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out + b0, b1 - b0, hipMemcpyHostToDevice, dst));
+    } else {  // one byte per symbol (SAHARA_NIBBLE_UPLOAD=0): check, then copy as given
+        const uint64_t pieces = (s1 - s0 + kPiece - 1) / kPiece;
+        P.run([&](unsigned t) {
+            for (uint64_t k = t; k < pieces; k += nt) {
+                const uint64_t lo = s0 + k * kPiece, hi = std::min(s1, lo + kPiece);
+                const uint64_t acc = avx2 ? badRanksAvx2(U.src + lo, hi - lo, sigma)
+                                          : badRanksScalar(U.src + lo, hi - lo, sigma);
+                if (acc) bad.store(1, std::memory_order_relaxed);
+            }
+        });
+        if (!bad.load()) SH_HIP(hipMemcpyAsync(raw + s0, U.src + s0, s1 - s0, hipMemcpyHostToDevice, dst));
+    }
+    U.hostMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (bad.load()) {
+        U.bad = true;
+        return;
+    }
+    const uint64_t j = r0 / U.chunk;
+    while (c->upEv.size() <= j) {
+        hipEvent_t e;
+        SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->upEv.push_back(e);
+    }
+    if (U.nibble && U.zeroCopy) {  // the unpack kernel reads the pinned host buffer over PCIe itself
+        launchUnpackNibbles(c->nibDev + s0 / 2, raw + s0, s1 - s0, kst);
+    } else {
+        SH_HIP(hipEventRecord(c->upEv[j], dst));  // the chunk's DMA
+        SH_HIP(hipStreamWaitEvent(kst, c->upEv[j], 0));
+        if (U.nibble) launchUnpackNibbles(c->nibPats.ptr + s0 / 2, raw + s0, s1 - s0, kst);
+    }
+    const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
+    if (U.rc) launchInterleaveRC(c->readRaw.ptr, r0, r1, m, sigma, c->npat, c->rawPats.ptr, kst);
+    if (p1 > p0) {
+        launchPackPatterns(c->rawPats.ptr + p0 * m, p1 - p0, m, c->patWords, sigma, c->pats.ptr + p0 * c->patWords,
+                           c->badFlag.ptr, kst);
+        launchPackPatterns3(c->rawPats.ptr + p0 * m, p1 - p0, m, c->patBlocks, c->pats3.ptr + p0 * c->patBlocks, kst);
+    }
+    U.last = (int64_t)j;
+    U.done = r1;
+}
+
+// Streamed upload: makes sure the patterns [0, patEnd) are enqueued, their
+// device-side packing on stream kst (a no-op when the patterns were staged
+// whole).
+void ensureUploaded(Ctx* c, uint64_t patEnd, hipStream_t kst) {
+    if (!c->streaming) return;
+    Ctx::Upload& U = c->up;
+    auto covered = [&] { return U.rc ? std::min(2 * U.done, c->npat) : U.done; };
+    while (covered() < patEnd) {
+        uploadChunk(c, kst);
+        if (U.bad) throw Error("pattern rank out of range for this index");
+    }
+}
+
+// The scheme half of staging: host tables, their upload, the k-mer starts.
+void stageScheme(Ctx* c, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                 uint32_t ns, int edit) {
+    if (npat == 0) throw Error("no patterns");
+    std::vector<uint32_t> packed, cover;
+    packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);
+    if ((size_t)ns * m * 4 > 60 * 1024) throw Error("scheme too large for LDS (searches * len > 15360)");
+    if (ns > 255) throw Error("at most 255 searches per scheme");
+    textTable(pi, l, u, ns, m, packed, cover);
+    c->scheme.reserve(packed.size());
+    SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
+    c->cover.reserve(cover.size());
+    SH_HIP(hipMemcpyAsync(c->cover.ptr, cover.data(), cover.size() * 4, hipMemcpyHostToDevice, c->st));
+    // searches whose first kmerK steps admit no error start from the k-mer table
+    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu);
+    const uint32_t K = c->I.kmerK;
+    for (uint32_t s = 0; K && K <= m && s < ns; ++s) {
+        bool exact = true;
+        uint32_t lo = pi[(size_t)s * m];
+        for (uint32_t p = 0; p < K; ++p) {
+            exact = exact && u[(size_t)s * m + p] == 0;
+            lo = std::min(lo, pi[(size_t)s * m + p]);
+        }
+        if (exact) kst[s] = lo;
+    }
+    c->kmerStart.reserve(ns);
+    SH_HIP(hipMemcpyAsync(c->kmerStart.ptr, kst.data(), ns * 4, hipMemcpyHostToDevice, c->st));
+    SH_HIP(hipStreamSynchronize(c->st));
+    c->nsearch = ns;
+    c->edit = edit != 0;
+}
+
+// Staging for a streamed search: the scheme now, the patterns chunk by chunk
+// during the pass (uploadChunk). src holds `rows` rows of m symbols: the
+// patterns, or (rc) the reads whose interleave with their reverse
+// complements, cut to npat, is the query list.
+void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t m,
+                   const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit) {
+    c->staged = c->streaming = false;
+    if (m == 0 || m > kMaxPatternLen) throw Error("pattern length out of range");
+    stageScheme(c, npat, m, pi, l, u, ns, edit);
+    c->m = m;
+    c->npat = npat;
+    c->patWords = (m + 7) / 8;
+    c->patBlocks = (m + 31) / 32;
+    c->rawPats.reserve(npat * m);
+    c->pats.reserve(npat * c->patWords + 4);  // + tail words read by paired loads
+    c->pats3.reserve(npat * c->patBlocks);
+    if (rc) c->readRaw.reserve(rows * m);
+    c->badFlag.reserve(1);
+    Ctx::Upload& U = c->up;
+    U = Ctx::Upload{};
+    U.src = src;
+    U.rc = rc;
+    U.rows = rows;
+    if (const char* e = std::getenv("SAHARA_NIBBLE_UPLOAD")) c->nibbleUpload = std::atoi(e) != 0;
+    U.nibble = c->nibbleUpload;
+    // 1M patterns per chunk (~50 MB packed at m = 100; SAHARA_UPLOAD_CHUNK)
+    uint64_t chunkPats = 1u << 20;
+    if (const char* e = std::getenv("SAHARA_UPLOAD_CHUNK")) chunkPats = std::max<uint64_t>(2, std::atoll(e));
+    U.chunk = std::max<uint64_t>(2, (rc ? chunkPats / 2 : chunkPats) & ~uint64_t(1));
+    SH_HIP(hipStreamSynchronize(c->stE));  // the pinned staging buffer may still feed the last call's DMA
+    if (U.nibble) {
+        const size_t nb = (rows * m + 1) / 2;
+        if (c->nibHostCap < nb) {
+            if (c->nibHost) SH_HIP(hipHostFree(c->nibHost));
+            c->nibHost = nullptr;
+            c->nibHostCap = 0;
+            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->nibHost), nb));
+            c->nibHostCap = nb;
+            void* d = nullptr;
+            SH_HIP(hipHostGetDevicePointer(&d, c->nibHost, 0));
+            c->nibDev = static_cast<const uint8_t*>(d);
+        }
+        // default: one DMA per chunk into device memory, unpacked there;
+        // SAHARA_UPLOAD_DMA=0: the unpack kernel reads the pinned host buffer
+        // itself (measured slower at C3: 296M against 358M reads/s)
+        const char* dmaEnv = std::getenv("SAHARA_UPLOAD_DMA");
+        U.zeroCopy = dmaEnv && std::atoi(dmaEnv) == 0;
+        if (!U.zeroCopy) c->nibPats.reserve(nb + 8);
+    }
+    SH_HIP(hipMemsetAsync(c->badFlag.ptr, 0, sizeof(uint32_t), c->stE));
+    c->stageMs = 0;
+    c->staged = c->streaming = true;
+}
+
 void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l,
            const uint32_t* u, uint32_t ns, int edit) {
     if (npat == 0) throw Error("no patterns");
+    c->staged = c->streaming = false;
     std::vector<uint32_t> packed, cover;
     packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);
     if ((size_t)ns * m * 4 > 60 * 1024) throw Error("scheme too large for LDS (searches * len > 15360)");
@@ -432,7 +805,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // k-mer table the FM phase is light, its stack lives in L2, and its 1.2 KB
     // fit beside four text workgroups per CU (measured: depth 0 846M, 1 845M,
     // 4 817M reads/s at C3)
-    uint32_t fmLdsDepth = 0;
+    // In the reference execution (verify off) every node is ranked from the
+    // root, the DFS runs ~100x deeper trees and nothing else needs the LDS:
+    // the bottom four levels there took C3 from 44.4M to 53.3M reads/s
+    // (2: 49.9M, 8: 53.1M; profiles/r02_v1_sweep_ref_fm_lds_depth.txt).
+    uint32_t fmLdsDepth = c->verify ? 0u : 4u;
     if (const char* e = std::getenv("SAHARA_FM_LDS_DEPTH")) fmLdsDepth = (uint32_t)std::max(0, std::min(8, std::atoi(e)));
     const size_t lds = (size_t)((c->nsearch * c->m + 3u) & ~3u) * 4 + (size_t)fmLdsDepth * 256 * 16;
     const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
@@ -560,6 +937,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     SH_HIP(hipStreamSynchronize(c->stD));
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
+    c->sinkDone = 0;
+    c->sinkOk = c->sink != nullptr;
     // a slot's counters and queues are zero when its `free` event fires:
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
@@ -631,6 +1010,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // seeds on their own stream (sD), so that they run ahead of the FM
         // phase of the batch before (both are HBM-latency bound and light)
         SH_HIP(hipStreamWaitEvent(sD, sl.free, 0));
+        // streamed upload: the batch's patterns (packed here on the host while
+        // the batches before it search; unpacked on sD ahead of its seeds)
+        ensureUploaded(c, bstart[b + 1], sD);
         SH_HIP(hipEventRecord(sl.fmStart, sD));
         launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sD);
         if (early && b == 0)  // the seed tasks end here: the text phase may start on them
@@ -771,6 +1153,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             SH_HIP(hipMalloc(&np, want * sizeof(sahara_hit)));
             if (c->nout) SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, sC));
             SH_HIP(hipStreamSynchronize(sC));
+            SH_HIP(hipStreamSynchronize(c->stF));  // sink copies may still read the old buffer
             c->out.release();
             c->out.ptr = np;
             c->out.cap = want;
@@ -778,6 +1161,18 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, q0, c->I.dRecStarts.ptr,
                    (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, c->tmp.ptr, c->tmp.cap, sC);
         SH_HIP(hipEventRecord(c->ev[4], sC));
+        // sahara_gpu_search's host sink: the batch's hits go to host memory
+        // on stF while later batches search (while they fit the sink)
+        if (c->sinkOk && c->nout + rows <= c->sinkCap) {
+            if (rows) {
+                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[4], 0));
+                SH_HIP(hipMemcpyAsync(c->sink + c->nout, c->out.ptr + c->nout, rows * sizeof(sahara_hit),
+                                      hipMemcpyDeviceToHost, c->stF));
+            }
+            c->sinkDone = c->nout + rows;
+        } else {
+            c->sinkOk = false;
+        }
         SH_HIP(hipMemcpyAsync(c->pinned + b * 8 + 7, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(c->ev[5], sC));
         c->nout += rows;
@@ -817,6 +1212,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamSynchronize(sB));
         SH_HIP(hipStreamSynchronize(sC));
         SH_HIP(hipStreamSynchronize(sD));
+        SH_HIP(hipStreamSynchronize(c->stF));
         if (overflow) return;  // the caller redoes the pass serially with the grown buffers
     } else {
         for (uint64_t b = 0; b < nbatch; ++b) {
@@ -832,6 +1228,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             }
         }
         overflow = false;
+        SH_HIP(hipStreamSynchronize(c->stF));
     }
     if (count) {
         unsigned long long h[16];
@@ -1038,10 +1435,13 @@ static HitPool& hitPool() {
 
 // Host buffer for n hits (released with sahara_gpu_free); *pinned tells
 // whether the device can copy into it directly.
-static void* allocHits(uint64_t n, bool* pinned) {
+static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr) {
     const size_t bytes = std::max<uint64_t>(n, 1) * sizeof(sahara_hit);
     *pinned = false;
-    if (bytes < (64u << 20)) return std::malloc(bytes);
+    if (capHits) *capHits = std::max<uint64_t>(n, 1);
+    size_t pinMin = 64u << 20;  // SAHARA_PIN_MIN: smallest pinned buffer in bytes (tests pin every size)
+    if (const char* e = std::getenv("SAHARA_PIN_MIN")) pinMin = (size_t)std::atoll(e);
+    if (bytes < pinMin) return std::malloc(bytes);
     HitPool& P = hitPool();
     std::vector<void*> unpin;
     void* p = nullptr;
@@ -1053,6 +1453,7 @@ static void* allocHits(uint64_t n, bool* pinned) {
         if (best != SIZE_MAX) {
             p = P.idle[best].first;
             P.live[p] = P.idle[best].second;
+            if (capHits) *capHits = P.idle[best].second / sizeof(sahara_hit);
             P.idle.erase(P.idle.begin() + (long)best);
         } else {  // none fits: the smaller idle ones will not fit later calls of this size either
             for (auto& e : P.idle) unpin.push_back(e.first);
@@ -1069,6 +1470,7 @@ static void* allocHits(uint64_t n, bool* pinned) {
         std::lock_guard<std::mutex> g(P.mu);
         P.live[p] = cap;
         *pinned = true;
+        if (capHits) *capHits = cap / sizeof(sahara_hit);
         return p;
     }
     (void)hipGetLastError();
@@ -1140,40 +1542,110 @@ static void copyOut(Ctx* c, void* dst, const void* src, size_t bytes) {
     }
 }
 
-int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,
-                      const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit, uint32_t max_hits,
-                      sahara_hit** hits, uint64_t* n_hits) {
-    return guarded([&] {
-        Ctx* c = ctxOf(ctx);
-        stage(c, ranks, n_patterns, len, pi, l, u, n_searches, edit);
+// Waits for every stream of the context (after a failed streamed search: the
+// issued batches may still run and copy into the sink).
+static void drainAll(Ctx* c) {
+    for (hipStream_t s : {c->st, c->stB, c->stC, c->stD, c->stE, c->stF}) (void)hipStreamSynchronize(s);
+}
+
+// sahara_gpu_search / sahara_gpu_search_reads: streamed upload, the pipelined
+// pass, the hits streamed into a pinned host sink batch by batch, then handed
+// to the caller (search.cpp:218-250 from host queries to host hits).
+static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t len,
+                           const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit,
+                           uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits) {
+    stageStreamed(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit);
+    c->sink = nullptr;
+    c->sinkCap = 0;
+    if (!max_hits) {  // sized from the last call (the bench's steady state), else 2 hits per pattern
+        const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
+        bool pinned = false;
+        void* p = allocHits(est, &pinned, &c->sinkCap);
+        if (p && pinned) {
+            c->sink = static_cast<sahara_hit*>(p);
+        } else {
+            freeHits(p);
+            c->sinkCap = 0;
+        }
+    }
+    try {
         run(c, false);
-        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t bad = 0;
+        SH_HIP(hipMemcpy(&bad, c->badFlag.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (bad) throw Error("pattern rank out of range for this index");
+    } catch (...) {
+        drainAll(c);
+        freeHits(c->sink);
+        c->sink = nullptr;
+        c->staged = c->streaming = false;
+        throw;
+    }
+    c->streaming = false;  // every chunk is up: sahara_gpu_run may re-run the staged patterns
+    c->stats.stage_ms = c->up.hostMs;
+    const auto t0 = std::chrono::steady_clock::now();
+    sahara_hit* buf = c->sink;
+    c->sink = nullptr;
+    try {
         if (max_hits) {
             std::vector<sahara_hit> v(c->nout);
             if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
             limitHits(v, max_hits);
             handOver(v, hits, n_hits);
-        } else {  // straight into the caller-owned buffer
-            bool pinned = false;
-            auto* buf = static_cast<sahara_hit*>(allocHits(c->nout, &pinned));
-            if (!buf) throw Error("out of host memory for hits");
-            if (c->nout) {
-                try {
-                    if (pinned) {
-                        SH_HIP(hipMemcpyAsync(buf, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost, c->st));
-                        SH_HIP(hipStreamSynchronize(c->st));
-                    } else {
-                        copyOut(c, buf, c->out.ptr, c->nout * sizeof(sahara_hit));
-                    }
-                } catch (...) {
-                    freeHits(buf);
-                    throw;
+        } else {
+            if (buf && c->nout > c->sinkCap) {  // more hits than the sink holds: a bigger buffer, copied whole
+                freeHits(buf);
+                buf = nullptr;
+                c->sinkDone = 0;
+            }
+            bool pinned = buf != nullptr;
+            if (!buf) {
+                c->sinkDone = 0;
+                buf = static_cast<sahara_hit*>(allocHits(c->nout, &pinned));
+                if (!buf) throw Error("out of host memory for hits");
+            }
+            if (c->nout > c->sinkDone) {  // the rest (or all) of the hits
+                const size_t bytes = (c->nout - c->sinkDone) * sizeof(sahara_hit);
+                if (pinned) {
+                    SH_HIP(hipMemcpyAsync(buf + c->sinkDone, c->out.ptr + c->sinkDone, bytes, hipMemcpyDeviceToHost,
+                                          c->st));
+                    SH_HIP(hipStreamSynchronize(c->st));
+                } else {
+                    copyOut(c, buf + c->sinkDone, c->out.ptr + c->sinkDone, bytes);
                 }
             }
             *hits = buf;
             *n_hits = c->nout;
+            buf = nullptr;
         }
-        c->stats.output_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    } catch (...) {
+        freeHits(buf);
+        throw;
+    }
+    freeHits(buf);  // the sink of a max_hits call
+    c->lastHits = c->nout;
+    c->stats.output_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,
+                      const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit, uint32_t max_hits,
+                      sahara_hit** hits, uint64_t* n_hits) {
+    return guarded([&] {
+        searchStreamed(ctxOf(ctx), ranks, n_patterns, false, n_patterns, len, pi, l, u, n_searches, edit, max_hits,
+                       hits, n_hits);
+    });
+}
+
+int sahara_gpu_search_reads(void* ctx, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
+                            uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                            uint32_t n_searches, int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (c->I.sigma != 5 && c->I.sigma != 6) throw Error("reverse complements need a dna4 or dna5 index");
+        uint64_t npat = reverse ? 2 * n_reads : n_reads;
+        if (limit && limit < npat) npat = limit;  // --limit_queries cuts the interleaved list (search.cpp:125-127)
+        if (npat == 0) throw Error("no patterns");
+        const uint64_t rows = reverse ? (npat + 1) / 2 : npat;
+        searchStreamed(c, reads, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit, max_hits, hits, n_hits);
     });
 }
 

@@ -1528,6 +1528,38 @@ void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream
     SH_HIP(hipGetLastError());
 }
 
+// Query ingest's reverse-complement interleave (search.cpp:121-127) on the
+// device: pattern 2r = read r, 2r + 1 = its reverse complement (A<->T, C<->G,
+// N->N; ivs::reverse_complement_rank), for the patterns [2 * r0, pEnd) of the
+// reads [r0, r1). One wave per read: lane j copies symbol j and writes its
+// complement to position m - 1 - j of the next pattern (coalesced bytes).
+__global__ void kInterleaveRC(const uint8_t* __restrict__ reads, uint64_t r0, uint64_t r1, uint32_t m,
+                              uint32_t sigma, uint64_t pEnd, uint8_t* __restrict__ pats) {
+    const uint32_t comp = sigma == 6 ? 0x142350u : 0x12340u;  // nibble c: complement of rank c (0 past sigma)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t r = r0 + (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < r1; r += waves) {
+        const uint8_t* src = reads + r * m;
+        uint8_t* fwd = pats + 2 * r * m;
+        uint8_t* rev = fwd + m;
+        const bool withRev = 2 * r + 1 < pEnd;
+        for (uint32_t j = lane; j < m; j += 64) {
+            const uint32_t s = src[j];
+            fwd[j] = (uint8_t)s;
+            if (withRev) rev[m - 1 - j] = s < 8 ? (uint8_t)((comp >> (4 * s)) & 0xFu) : (uint8_t)0;
+        }
+    }
+}
+
+void launchInterleaveRC(const uint8_t* reads, uint64_t r0, uint64_t r1, uint32_t m, uint32_t sigma, uint64_t pEnd,
+                        uint8_t* pats, hipStream_t st) {
+    r1 = std::min(r1, (pEnd + 1) / 2);  // reads whose forward pattern is within the limit
+    if (r1 <= r0) return;
+    const uint64_t blocks = std::min<uint64_t>((r1 - r0 + 3) / 4, 65536);
+    hipLaunchKernelGGL(kInterleaveRC, dim3((unsigned)blocks), dim3(256), 0, st, reads, r0, r1, m, sigma, pEnd, pats);
+    SH_HIP(hipGetLastError());
+}
+
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st) {
     const uint64_t blocks = std::min<uint64_t>((npat * patWords + 255) / 256, 65536);

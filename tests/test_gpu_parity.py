@@ -317,3 +317,81 @@ def test_nibble_upload_matches_byte_upload(gpu_device, monkeypatch):
     bad[-1, -1] = 7  # a nibble, but no rank of sigma 6: the device check
     with pytest.raises(Exception, match="out of range"):
         sa.search(gpu, bad, sch)
+
+
+def _streamed_inputs(n_reads=2000, m=60, k=2):
+    flat, lens = sa.synth_reference([300_000, 200_000], sigma=6, seed=17)
+    reads = sa.synth_reads(flat, lens, n_reads, m, k, sigma=6, seed=19)
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme("h2-k2", 0, k, m)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
+    return flat, lens, reads, pats, sch, ref
+
+
+@pytest.mark.parametrize("chunk,batch,nibble", [(None, None, "1"), ("64", "97", "1"), ("7", None, "1"),
+                                                ("64", "97", "0")])
+def test_search_reads_and_streamed_upload(gpu_device, monkeypatch, chunk, batch, nibble):
+    """sahara_gpu_search_reads (reverse complements interleaved on the device,
+    search.cpp:121-127) and sahara_gpu_search both upload the queries chunk by
+    chunk while earlier batches search (SAHARA_UPLOAD_CHUNK patterns per
+    chunk, SAHARA_BATCH per batch): same hits as the oracle over the
+    interleaved patterns, also cut by --limit_queries (odd: the last read's
+    reverse complement dropped) and with --no-reverse."""
+    for var, val in (("SAHARA_UPLOAD_CHUNK", chunk), ("SAHARA_BATCH", batch)):
+        if val:
+            monkeypatch.setenv(var, val)
+    monkeypatch.setenv("SAHARA_NIBBLE_UPLOAD", nibble)
+    flat, lens, reads, pats, sch, ref = _streamed_inputs()
+    want = hits_as_rows(ref.search(pats, sch, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want)
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+    lim = 2 * 1500 - 1
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch, limit=lim)), want[want[:, 0] < lim])
+    fwd = hits_as_rows(ref.search(reads, sch, nthreads=8)[0])
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch, reverse=False)), fwd)
+    # the device-resident run over what the streamed call left staged
+    gpu.run()
+    assert np.array_equal(hits_as_rows(gpu.fetch()), fwd)
+
+
+@pytest.mark.parametrize("bad_value", [0, 6, 17])
+def test_streamed_upload_refuses_bad_rank_in_a_late_chunk(gpu_device, monkeypatch, bad_value):
+    """A byte that is no rank (0, >= sigma) in a chunk uploaded while earlier
+    batches already search: the call fails loudly, nothing of the bad chunk is
+    searched, and the context serves the next call."""
+    monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "64")
+    monkeypatch.setenv("SAHARA_BATCH", "97")
+    flat, lens, reads, pats, sch, ref = _streamed_inputs()
+    want = hits_as_rows(ref.search(pats, sch, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    bad = reads.copy()
+    bad[1900, 5] = bad_value
+    with pytest.raises(sa.SaharaError, match="out of range"):
+        sa.search_reads(gpu, bad, sch)
+    badp = pats.copy()
+    badp[3801, 7] = bad_value
+    with pytest.raises(sa.SaharaError, match="out of range"):
+        sa.search(gpu, badp, sch)
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+
+
+def test_pinned_hit_sink_grows_and_is_recycled(gpu_device, monkeypatch):
+    """Hits go to pinned host memory batch by batch (SAHARA_PIN_MIN=0 pins
+    every size): a call with more hits than the last call's estimate falls
+    back to a bigger buffer, freed buffers are reused, and every result is
+    the oracle's."""
+    monkeypatch.setenv("SAHARA_PIN_MIN", "0")
+    monkeypatch.setenv("SAHARA_BATCH", "97")
+    flat, lens, reads, pats, sch, ref = _streamed_inputs()
+    want = hits_as_rows(ref.search(pats, sch, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    small = sa.search_reads(gpu, reads[:40], sch)
+    assert np.array_equal(hits_as_rows(small), want[want[:, 0] < 80])
+    kept = sa.search_reads(gpu, reads, sch)  # more hits than the estimate from 40 reads
+    assert np.array_equal(hits_as_rows(kept), want)
+    for _ in range(3):  # steady state: the sink comes back from the pool
+        assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+    assert np.array_equal(hits_as_rows(kept), want)  # a held buffer is never handed out again
+    del small, kept
