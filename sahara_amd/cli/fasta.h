@@ -9,11 +9,20 @@
 // d_dna4 = {$, A, C, G, T} (sigma 5); lower case maps like upper case; every
 // other character is invalid (rank 255).
 #pragma once
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 namespace sahara_cli {
@@ -109,6 +118,180 @@ inline std::vector<uint8_t> toRanks(const std::string& s, uint32_t sigma) {
     std::vector<uint8_t> r(s.size());
     for (size_t i = 0; i < s.size(); ++i) r[i] = charToRank(s[i], sigma);
     return r;
+}
+
+// ----------------------------------------------------------------------------
+// Whole-file FASTA ingest on several threads: the same records, ranks and
+// validation as FastaReader + toRanks + firstInvalid, for the 3 Gbp reference
+// of `sahara index` and the 10M-read query files of `sahara search`
+// (single-threaded parsing dominates at that scale).
+// The file is mapped and cut into pieces of ~8 MB that start at line starts.
+// A line starting with '>' is a header (a new record), any other line is
+// sequence. Pass 1 counts each piece's sequence characters and notes where
+// its records start; pass 2 converts them into one flat rank array
+// (255 = no rank of the alphabet) at the prefix-summed offsets.
+struct FastaData {
+    std::vector<uint64_t> offs;     // record i's ranks = ranks[offs[i], offs[i+1])
+    std::vector<uint8_t> ranks;
+    // the first byte that is no rank of the alphabet, if any
+    bool bad = false;
+    size_t badRecord = 0;
+    uint64_t badPos = 0;            // position in its record
+    unsigned char badChar = 0;
+    std::string badId;              // its record's header text after '>'
+    size_t records() const { return offs.empty() ? 0 : offs.size() - 1; }
+};
+
+template <typename F>
+inline void parallelFor(unsigned nt, size_t n, F&& f) {  // f(i) for i in [0, n), interleaved over nt threads
+    if (nt <= 1 || n < 2) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (unsigned t = 0; t < nt && t < n; ++t)
+        ts.emplace_back([&, t] {
+            for (size_t i = t; i < n; i += nt) f(i);
+        });
+    for (auto& t : ts) t.join();
+}
+
+inline unsigned hostThreads() {
+    const char* e = std::getenv("OMP_NUM_THREADS");  // the GPU box's CPU share (16 per GPU)
+    unsigned n = e ? (unsigned)std::atoi(e) : 0;
+    if (n == 0) n = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(n, 32u));
+}
+
+inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, unsigned nt,
+                                    size_t kPiece = 8u << 20) {
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("can not open file " + path);
+    struct stat sb {};
+    if (::fstat(fd, &sb) != 0) {
+        ::close(fd);
+        throw std::runtime_error("can not stat file " + path);
+    }
+    const size_t n = (size_t)sb.st_size;
+    FastaData D;
+    if (n == 0) {
+        ::close(fd);
+        return D;
+    }
+    void* mp = ::mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (mp == MAP_FAILED) throw std::runtime_error("can not map file " + path);
+    (void)::madvise(mp, n, MADV_WILLNEED);
+    const char* b = static_cast<const char*>(mp);
+    struct Unmap {
+        void* p;
+        size_t n;
+        ~Unmap() { ::munmap(p, n); }
+    } unmap{mp, n};
+    // pieces of ~kPiece bytes starting at line starts
+    std::vector<size_t> bound{0};
+    for (size_t p = kPiece; p < n;) {
+        const void* nl = std::memchr(b + p, '\n', n - p);
+        if (!nl) break;
+        const size_t q = (size_t)(static_cast<const char*>(nl) - b) + 1;
+        if (q >= n) break;
+        bound.push_back(q);
+        p = q + kPiece;
+    }
+    bound.push_back(n);
+    const size_t P = bound.size() - 1;
+    struct Piece {
+        uint64_t seq = 0;                                    // sequence characters
+        uint64_t lead = 0;                                   // ... before its first header
+        std::vector<std::pair<uint64_t, uint64_t>> heads;    // (header position, sequence characters before it)
+        uint64_t badAt = UINT64_MAX;                         // first invalid rank (piece-local sequence index)
+        unsigned char badChar = 0;
+    };
+    std::vector<Piece> pc(P);
+    // a line's sequence bytes end before its '\n', and before a '\r' right
+    // in front of it (FastaReader::readLine; not at a last line without '\n')
+    auto lineEnd = [&](size_t p, size_t eol, bool hasNl) { return hasNl && eol > p && b[eol - 1] == '\r' ? eol - 1 : eol; };
+    // pass 1: count
+    parallelFor(nt, P, [&](size_t i) {
+        Piece& c = pc[i];
+        uint64_t k = 0;
+        for (size_t p = bound[i], e = bound[i + 1]; p < e;) {
+            const void* nl = std::memchr(b + p, '\n', e - p);
+            const size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : e;
+            if (b[p] == '>') {
+                if (c.heads.empty()) c.lead = k;
+                c.heads.emplace_back(p, k);
+            } else {
+                k += lineEnd(p, eol, nl != nullptr) - p;
+            }
+            p = eol + 1;
+        }
+        c.seq = k;
+        if (c.heads.empty()) c.lead = k;
+    });
+    // records and offsets
+    std::vector<uint64_t> base(P + 1, 0);
+    for (size_t i = 0; i < P; ++i) base[i + 1] = base[i] + pc[i].seq;
+    uint64_t lead = 0;  // sequence characters before the first header
+    for (size_t i = 0; i < P; ++i) {
+        lead += pc[i].lead;
+        if (!pc[i].heads.empty()) break;
+    }
+    if (lead > 0) throw std::runtime_error("malformed FASTA (sequence before header) in " + path);
+    std::vector<uint64_t> heads;
+    for (size_t i = 0; i < P; ++i)
+        for (auto& h : pc[i].heads) {
+            heads.push_back(h.first);
+            D.offs.push_back(base[i] + h.second);
+        }
+    if (heads.empty()) return D;
+    D.offs.push_back(base[P]);
+    // pass 2: convert
+    D.ranks.resize(base[P]);
+    uint8_t table[256];
+    for (int c = 0; c < 256; ++c) table[c] = charToRank((char)c, sigma);
+    parallelFor(nt, P, [&](size_t i) {
+        Piece& c = pc[i];
+        uint8_t* const o0 = D.ranks.data() + base[i];
+        uint8_t* o = o0;
+        for (size_t p = bound[i], e = bound[i + 1]; p < e;) {
+            const void* nl = std::memchr(b + p, '\n', e - p);
+            const size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : e;
+            if (b[p] != '>') {
+                for (size_t q = p, qe = lineEnd(p, eol, nl != nullptr); q < qe; ++q) {
+                    const unsigned char ch = (unsigned char)b[q];
+                    const uint8_t v = table[ch];
+                    if (v >= sigma && c.badAt == UINT64_MAX) {
+                        c.badAt = (uint64_t)(o - o0);
+                        c.badChar = ch;
+                    }
+                    *o++ = v;
+                }
+            }
+            p = eol + 1;
+        }
+    });
+    for (size_t i = 0; i < P; ++i)
+        if (pc[i].badAt != UINT64_MAX) {
+            const uint64_t at = base[i] + pc[i].badAt;
+            D.bad = true;
+            D.badRecord = (size_t)(std::upper_bound(D.offs.begin(), D.offs.end(), at) - D.offs.begin()) - 1;
+            D.badPos = at - D.offs[D.badRecord];
+            D.badChar = pc[i].badChar;
+            const size_t h = heads[D.badRecord] + 1;
+            const void* nl = std::memchr(b + h, '\n', n - h);
+            size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : n;
+            if (eol > h && b[eol - 1] == '\r') --eol;
+            D.badId.assign(b + h, eol - h);
+            break;
+        }
+    return D;
+}
+
+// ivs::reverse_complement_rank of one rank: A<->T, C<->G, N->N
+inline uint8_t complementRank(uint8_t c, uint32_t sigma) {
+    if (sigma == 6) return c == 1 ? 5 : c == 2 ? 3 : c == 3 ? 2 : c == 5 ? 1 : c;
+    return c == 1 ? 4 : c == 2 ? 3 : c == 3 ? 2 : c == 4 ? 1 : c;
 }
 
 inline std::vector<uint8_t> reverseComplement(const std::vector<uint8_t>& r, uint32_t sigma) {

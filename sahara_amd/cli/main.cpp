@@ -142,32 +142,28 @@ int cmdIndex(int argc, char** argv) {
     std::vector<std::tuple<std::string, double>> timing;
     StopWatch sw;
 
-    std::vector<uint8_t> ranks;
-    std::vector<uint64_t> lens;
-    uint64_t totalSize = 0;
-    {
-        FastaReader rd(path);
-        Record rec;
-        size_t n = 0;
-        while (rd.next(rec)) {
-            ++n;
-            totalSize += rec.seq.size();
-            std::vector<uint8_t> r = toRanks(rec.seq, sigma);
-            if (ignore.given) {  // index.cpp:56-68
-                for (auto& v : r) {
-                    if (v != 255 && v != 0 && v < sigma) continue;
-                    v = dna4.given ? (uint8_t)(1 + std::rand() % 4) : (uint8_t)4;
-                }
-            }
-            if (long pos = firstInvalid(r, sigma); pos >= 0) {
-                const unsigned char ch = (unsigned char)rec.seq[(size_t)pos];
-                throw CliError(fmtStr("ref '%s' (%zu) has invalid character '%c' (0x%02x) at position %ld",
-                                      rec.id.c_str(), n, ch, ch, pos));
-            }
-            ranks.insert(ranks.end(), r.begin(), r.end());
-            lens.push_back(r.size());
+    // parallel whole-file ingest (fasta.h parseFastaParallel): records, ranks, first invalid character
+    const unsigned nt = hostThreads();
+    FastaData D = parseFastaParallel(path, sigma, nt);
+    const uint64_t totalSize = D.ranks.size();
+    if (ignore.given) {  // index.cpp:56-68: unknown characters become N (dna5) or a random base (dna4)
+        if (dna4.given) {
+            for (auto& v : D.ranks)
+                if (v == 255 || v == 0 || v >= sigma) v = (uint8_t)(1 + std::rand() % 4);
+        } else {
+            parallelFor(nt, nt, [&](size_t t) {
+                for (size_t i = D.ranks.size() * t / nt; i < D.ranks.size() * (t + 1) / nt; ++i)
+                    if (D.ranks[i] == 255 || D.ranks[i] == 0 || D.ranks[i] >= sigma) D.ranks[i] = 4;
+            });
         }
+    } else if (D.bad) {
+        const unsigned char ch = D.badChar;
+        throw CliError(fmtStr("ref '%s' (%zu) has invalid character '%c' (0x%02x) at position %ld", D.badId.c_str(),
+                              D.badRecord + 1, ch, ch, (long)D.badPos));
     }
+    std::vector<uint64_t> lens(D.records());
+    for (size_t r = 0; r < lens.size(); ++r) lens[r] = D.offs[r + 1] - D.offs[r];
+    std::vector<uint8_t>& ranks = D.ranks;
     if (lens.empty()) throw CliError("reference file " + path + " was empty - abort\n");
     std::printf("config:\n");
     std::printf("  file: %s\n", path.c_str());
@@ -198,37 +194,85 @@ int cmdIndex(int argc, char** argv) {
 
 // --------------------------------------------------------------- search ----
 
-// Fast text output of hits: "qid seqId pos[ e]\n" (search.cpp:254-261).
-void writeHits(const std::string& path, const std::vector<std::vector<sahara_hit>>& parts, bool emitErrors) {
+// One device's hits as the library hands them over: qids local to its shard.
+struct HitPart {
+    sahara_hit* hits = nullptr;
+    uint64_t n = 0;
+    uint64_t qidOffset = 0;
+};
+
+// Text output of hits: "qid seqId pos[ e]\n" (search.cpp:254-261). Blocks of
+// hits are formatted on nt threads, then written in order.
+void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool emitErrors, unsigned nt) {
     std::FILE* f = std::fopen(path.c_str(), "w");
     if (!f) throw CliError("can not open output file " + path);
-    std::vector<char> buf(1 << 22);
-    size_t used = 0;
-    auto put = [&](uint64_t v) {
-        auto r = std::to_chars(buf.data() + used, buf.data() + buf.size(), v);
-        used = (size_t)(r.ptr - buf.data());
+    struct Block {
+        const HitPart* part;
+        uint64_t lo, hi;
     };
-    for (const auto& hits : parts) {
-        for (const sahara_hit& h : hits) {
-            if (used + 96 > buf.size()) {
-                std::fwrite(buf.data(), 1, used, f);
-                used = 0;
+    std::vector<Block> blocks;
+    constexpr uint64_t kBlock = 1u << 18;  // hits per block (~7 MB of text)
+    for (const auto& hp : parts)
+        for (uint64_t lo = 0; lo < hp.n; lo += kBlock) blocks.push_back({&hp, lo, std::min(hp.n, lo + kBlock)});
+    const size_t wave = (size_t)nt * 2;  // blocks formatted per round (bounds the memory held)
+    std::vector<std::vector<char>> text(std::min(wave, blocks.size()));
+    for (size_t b0 = 0; b0 < blocks.size(); b0 += wave) {
+        const size_t nb = std::min(wave, blocks.size() - b0);
+        parallelFor(nt, nb, [&](size_t i) {
+            const Block& B = blocks[b0 + i];
+            std::vector<char>& buf = text[i];
+            buf.resize((B.hi - B.lo) * 96);
+            char* o = buf.data();
+            char* e = o + buf.size();
+            for (uint64_t k = B.lo; k < B.hi; ++k) {
+                const sahara_hit& h = B.part->hits[k];
+                o = std::to_chars(o, e, h.qid + B.part->qidOffset).ptr;
+                *o++ = ' ';
+                o = std::to_chars(o, e, h.seq_id).ptr;
+                *o++ = ' ';
+                o = std::to_chars(o, e, h.pos).ptr;
+                if (emitErrors) {
+                    *o++ = ' ';
+                    o = std::to_chars(o, e, h.err).ptr;
+                }
+                *o++ = '\n';
             }
-            put(h.qid);
-            buf[used++] = ' ';
-            put(h.seq_id);
-            buf[used++] = ' ';
-            put(h.pos);
-            if (emitErrors) {
-                buf[used++] = ' ';
-                put(h.err);
+            buf.resize((size_t)(o - buf.data()));
+        });
+        for (size_t i = 0; i < nb; ++i)
+            if (std::fwrite(text[i].data(), 1, text[i].size(), f) != text[i].size()) {
+                std::fclose(f);
+                throw CliError("can not write output file " + path);
             }
-            buf[used++] = '\n';
-        }
     }
-    std::fwrite(buf.data(), 1, used, f);
-    std::fclose(f);
+    if (std::fclose(f) != 0) throw CliError("can not write output file " + path);
 }
+
+// A read-only mapping of a whole file (the .idx image every device loads).
+struct MappedFile {
+    const void* data = nullptr;
+    size_t size = 0;
+    explicit MappedFile(const std::string& path) {
+        const int fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) throw CliError("no valid index path at " + path);
+        struct stat sb {};
+        if (::fstat(fd, &sb) != 0 || sb.st_size == 0) {
+            ::close(fd);
+            throw CliError("can not read index " + path);
+        }
+        size = (size_t)sb.st_size;
+        void* p = ::mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+        ::close(fd);
+        if (p == MAP_FAILED) throw CliError("can not map index " + path);
+        (void)::madvise(p, size, MADV_WILLNEED);
+        data = p;
+    }
+    ~MappedFile() {
+        if (data) ::munmap(const_cast<void*>(data), size);
+    }
+    MappedFile(const MappedFile&) = delete;
+    MappedFile& operator=(const MappedFile&) = delete;
+};
 
 uint64_t readSigma(const std::string& path) {
     std::ifstream f(path, std::ios::binary);
@@ -294,23 +338,23 @@ int cmdSearch(int argc, char** argv) {
     std::vector<std::tuple<std::string, double>> timing;
     StopWatch sw;
 
-    // queries (search.cpp:111-130): ranks, verification, RC interleave, limit
-    std::vector<std::vector<uint8_t>> queries;
-    {
-        FastaReader rd(query.value);
-        Record rec;
-        while (rd.next(rec)) {
-            queries.emplace_back(toRanks(rec.seq, (uint32_t)sigma));
-            if (long pos = firstInvalid(queries.back(), (uint32_t)sigma); pos >= 0) {
-                const unsigned char ch = (unsigned char)rec.seq[(size_t)pos];
-                throw CliError(fmtStr("query '%s' (%zu) has invalid character at position %ld '%c'(%x)",
-                                      rec.id.c_str(), queries.size(), pos, ch, ch));
-            }
-            if (!noRev.given) queries.emplace_back(reverseComplement(queries.back(), (uint32_t)sigma));
-        }
+    // queries (search.cpp:111-130): ranks and verification on the host (parallel
+    // whole-file ingest); the reverse-complement interleave and --limit_queries
+    // cut happen on the device (sahara_gpu_search_reads), so only the reads
+    // cross PCIe. Query numbers in messages count the interleaved list.
+    const unsigned nt = hostThreads();
+    FastaData Q = parseFastaParallel(query.value, (uint32_t)sigma, nt);
+    const size_t nrec = Q.records();
+    const size_t per = noRev.given ? 1 : 2;  // patterns per read
+    if (Q.bad) {
+        const unsigned char ch = Q.badChar;
+        throw CliError(fmtStr("query '%s' (%zu) has invalid character at position %ld '%c'(%x)", Q.badId.c_str(),
+                              per * Q.badRecord + 1, (long)Q.badPos, ch, ch));
     }
-    if (limit.given) queries.resize(std::min<size_t>(toU64(limit.value, "--limit_queries"), queries.size()));
-    if (queries.empty()) throw CliError("query file " + query.value + " was empty - abort\n");
+    size_t nq = per * nrec;  // the interleaved query list, cut by --limit_queries
+    if (limit.given) nq = std::min<size_t>(toU64(limit.value, "--limit_queries"), nq);
+    if (nq == 0) throw CliError("query file " + query.value + " was empty - abort\n");
+    const size_t nreads = (nq + per - 1) / per;  // reads that contribute a query
     timing.emplace_back("ld queries", sw.reset());
 
     std::printf(
@@ -327,14 +371,29 @@ int cmdSearch(int argc, char** argv) {
         query.value.c_str(), index.value.c_str(), gen.value.c_str(), dyn.given ? "true" : "false", k,
         noRev.given ? "false" : "true", besthits ? "besthits" : "all", mh, output.value.c_str());
     {
-        const size_t fwd = queries.size() / (noRev.given ? 1 : 2);
-        std::printf("fwd queries: %zu\nbwd queries: %zu\n", fwd, queries.size() - fwd);
+        const size_t fwd = nq / per;
+        std::printf("fwd queries: %zu\nbwd queries: %zu\n", fwd, nq - fwd);
     }
     std::fflush(stdout);
 
-    // index residency (search.cpp:162-169): one context per device
+    // index residency (search.cpp:162-169): one context per device, the
+    // devices loading the one mapped .idx image side by side
     std::vector<void*> ctx(ngpu, nullptr);
-    for (uint32_t g = 0; g < ngpu; ++g) check(sahara_gpu_open_file((int)g, index.value.c_str(), &ctx[g]), "loading index");
+    {
+        MappedFile img(index.value);
+        std::vector<std::string> errs(ngpu);
+        std::vector<std::thread> th;
+        for (uint32_t g = 0; g < ngpu; ++g)
+            th.emplace_back([&, g] {
+                if (sahara_gpu_open((int)g, img.data, img.size, &ctx[g]) != 0) errs[g] = sahara_gpu_last_error();
+            });
+        for (auto& t : th) t.join();
+        for (uint32_t g = 0; g < ngpu; ++g)
+            if (!errs[g].empty()) {
+                for (void* c : ctx) sahara_gpu_close(c);
+                throw CliError("loading index: " + errs[g]);
+            }
+    }
     if (fmOnly.given)
         for (void* c : ctx) check(sahara_gpu_set_mode(c, 0, 0), "set mode");
     sahara_index_info info{};
@@ -354,17 +413,13 @@ int cmdSearch(int argc, char** argv) {
         if (!known)
             throw CliError("unknown search scheme generetaror \"" + gen.value + "\", valid generators are: " + all);
     }
-    const uint32_t len = (uint32_t)queries[0].size();
-    for (size_t i = 0; i < queries.size(); ++i)
-        if (queries[i].size() != len)
+    const uint32_t len = (uint32_t)(Q.offs[1] - Q.offs[0]);
+    for (size_t r = 0; r < nreads; ++r)
+        if (Q.offs[r + 1] - Q.offs[r] != len)
             throw CliError(fmtStr("query %zu has length %zu, but all queries must have the length of the first "
                                   "(%u): sahara expands one search scheme for queries[0].size()",
-                                  i, queries[i].size(), len));
-    std::vector<uint8_t> flat;
-    flat.reserve(queries.size() * len);
-    for (auto& q : queries) flat.insert(flat.end(), q.begin(), q.end());
-    const size_t nq = queries.size();
-    std::vector<std::vector<uint8_t>>().swap(queries);
+                                  per * r, (size_t)(Q.offs[r + 1] - Q.offs[r]), len));
+    const uint8_t* reads = Q.ranks.data();  // nreads x len, back to back
 
     std::vector<Scheme> schemes;  // all: [0..k]; besthits: one per exact error count j
     // --dynamic_generator: part sizes by weighted node count (search.cpp:192-195, 202-205)
@@ -403,25 +458,38 @@ int cmdSearch(int argc, char** argv) {
         for (int j = 0; j <= k; ++j) add(build(j, j, false));
     timing.emplace_back("searchScheme", sw.reset());
 
-    // search + locate (search.cpp:218-250), queries sharded over the devices
-    std::vector<std::vector<sahara_hit>> parts(ngpu);
+    // search + locate (search.cpp:218-250), reads sharded over the devices
+    // (a read and its reverse complement stay together; qids stay global)
+    std::vector<HitPart> parts(ngpu);
     std::vector<double> devLocate(ngpu, 0.0);
     std::vector<std::string> errs(ngpu);
     {
         std::vector<std::thread> th;
         for (uint32_t g = 0; g < ngpu; ++g) {
             th.emplace_back([&, g] {
-                const size_t q0 = nq * g / ngpu, q1 = nq * (g + 1) / ngpu;
-                if (q0 == q1) return;
+                const size_t r0 = nreads * g / ngpu, r1 = nreads * (g + 1) / ngpu;
+                if (r0 == r1) return;
+                const size_t q0 = per * r0, q1 = std::min(nq, per * r1);  // this shard's queries
                 sahara_hit* hits = nullptr;
                 uint64_t nh = 0;
                 int rc;
                 const uint32_t cap = (uint32_t)std::max(0L, mh);
                 if (!besthits) {
                     const Scheme& s = schemes[0];
-                    rc = sahara_gpu_search(ctx[g], flat.data() + q0 * len, q1 - q0, len, s.pi.data(), s.l.data(),
-                                           s.u.data(), s.n, edit ? 1 : 0, cap, &hits, &nh);
-                } else {
+                    rc = sahara_gpu_search_reads(ctx[g], reads + r0 * len, r1 - r0, len, noRev.given ? 0 : 1, q1 - q0,
+                                                 s.pi.data(), s.l.data(), s.u.data(), s.n, edit ? 1 : 0, cap, &hits,
+                                                 &nh);
+                } else {  // search_best takes the interleaved patterns
+                    std::vector<uint8_t> pats((q1 - q0) * len);
+                    for (size_t q = q0; q < q1; ++q) {
+                        const uint8_t* src = reads + (q / per) * len;
+                        uint8_t* dst = pats.data() + (q - q0) * len;
+                        if (per == 2 && (q & 1)) {
+                            for (uint32_t j = 0; j < len; ++j) dst[j] = complementRank(src[len - 1 - j], (uint32_t)sigma);
+                        } else {
+                            std::memcpy(dst, src, len);
+                        }
+                    }
                     std::vector<uint32_t> pi, l, u, ns;
                     for (const Scheme& s : schemes) {
                         pi.insert(pi.end(), s.pi.begin(), s.pi.end());
@@ -429,8 +497,8 @@ int cmdSearch(int argc, char** argv) {
                         u.insert(u.end(), s.u.begin(), s.u.end());
                         ns.push_back(s.n);
                     }
-                    rc = sahara_gpu_search_best(ctx[g], flat.data() + q0 * len, q1 - q0, len, pi.data(), l.data(),
-                                                u.data(), ns.data(), (uint32_t)ns.size(), cap, &hits, &nh);
+                    rc = sahara_gpu_search_best(ctx[g], pats.data(), q1 - q0, len, pi.data(), l.data(), u.data(),
+                                                ns.data(), (uint32_t)ns.size(), cap, &hits, &nh);
                 }
                 if (rc != 0) {
                     errs[g] = sahara_gpu_last_error();
@@ -438,25 +506,26 @@ int cmdSearch(int argc, char** argv) {
                 }
                 sahara_stats st{};
                 sahara_gpu_stats(ctx[g], &st);
-                std::vector<sahara_hit> got(hits, hits + nh);
-                sahara_gpu_free(hits);
-                for (auto& h : got) h.qid += q0;
                 devLocate[g] = (st.locate_ms + st.sort_ms) / 1e3;
-                parts[g] = std::move(got);
+                parts[g] = HitPart{hits, nh, q0};  // released after writing
             });
         }
         for (auto& t : th) t.join();
     }
     for (auto& e : errs)
-        if (!e.empty()) throw CliError("search: " + e);
+        if (!e.empty()) {
+            for (auto& hp : parts) sahara_gpu_free(hp.hits);
+            throw CliError("search: " + e);
+        }
     double wall = sw.reset();
     const double loc = *std::max_element(devLocate.begin(), devLocate.end());
     timing.emplace_back("search", std::max(0.0, wall - loc));
     timing.emplace_back("locate", loc);
 
     uint64_t nhits = 0;
-    for (auto& p2 : parts) nhits += p2.size();
-    writeHits(output.value, parts, emitErr.given);
+    for (auto& hp : parts) nhits += hp.n;
+    writeHits(output.value, parts, emitErr.given, nt);
+    for (auto& hp : parts) sahara_gpu_free(hp.hits);
     timing.emplace_back("result", sw.reset());
     for (void* c : ctx) sahara_gpu_close(c);
 

@@ -140,8 +140,7 @@ struct Ctx {
     DevBuf<uint8_t> rawPats;              // staged pattern bytes before packing
     DevBuf<uint8_t> nibPats;              // the same, two symbols per byte as uploaded (stageIn)
     bool nibbleUpload = true;             // SAHARA_NIBBLE_UPLOAD=0: pattern bytes go up as given
-    uint8_t* nibHost = nullptr;           // pinned: the packed patterns on their way up
-    const uint8_t* nibDev = nullptr;      // the same memory as the device addresses it
+    uint8_t* nibHost = nullptr;           // pinned: the packed patterns on their way up (stage)
     size_t nibHostCap = 0;
     DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
@@ -158,25 +157,29 @@ struct Ctx {
 
     // Streamed query upload (sahara_gpu_search, sahara_gpu_search_reads): the
     // source rows go up in chunks, each packed on the host (two symbols per
-    // byte, ranks checked) and enqueued on stream stE when the first batch that
-    // needs it is issued, so that the upload of later batches overlaps the
-    // search of earlier ones. upEv[j] fires once chunk j's patterns are packed
-    // on the device; a batch's seed kernel waits for it.
+    // byte, ranks checked) into a slot of a pinned ring and copied on stream
+    // stE when the first batch that needs it is issued, so that the upload of
+    // later batches overlaps the search of earlier ones. ringEv[s] fires once
+    // slot s's last DMA is done: the device-side unpacking waits for it, and
+    // the host waits for it before packing into the slot again. The ring is
+    // pinned once per context, in the background while the index loads.
     struct Upload {
         const uint8_t* src = nullptr;  // host symbols: the patterns, or the reads (rc)
         bool rc = false;               // reads: reverse complements interleaved on the device
         bool nibble = true;
-        bool zeroCopy = false;         // kUnpackNibbles reads the pinned host buffer (no DMA); else DMA on stE
         uint64_t rows = 0;             // source rows
         uint64_t chunk = 0;            // source rows per chunk (even: chunks start at even symbols)
         uint64_t done = 0;             // source rows enqueued
-        int64_t last = -1;             // chunk of the last event recorded
         bool bad = false;              // a chunk held a byte that is no rank of this index
         double hostMs = 0;             // host time spent packing and enqueueing
     } up;
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
-    std::vector<hipEvent_t> upEv;
+    static constexpr size_t kRingSlots = 8, kRingSlot = 32u << 20;  // 256 MB pinned
+    uint8_t* ring = nullptr;
+    hipEvent_t ringEv[kRingSlots] = {};
+    std::thread ringInit;                 // pins the ring (started by newCtx)
+    bool ringFailed = false;
     DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
     DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
     std::unique_ptr<HostPool> pool;
@@ -190,8 +193,10 @@ struct Ctx {
     ~Ctx() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
-        for (auto& e : upEv)
+        if (ringInit.joinable()) ringInit.join();
+        for (auto& e : ringEv)
             if (e) (void)hipEventDestroy(e);
+        if (ring) (void)hipHostFree(ring);
         if (stE) (void)hipStreamDestroy(stE);
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
@@ -280,6 +285,18 @@ Ctx* newCtx(int device) {
     SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stF, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
+    for (auto& e : c->ringEv) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // the streamed upload's pinned ring, pinned while the caller builds or
+    // loads the index (pinning 256 MB takes ~50 ms)
+    Ctx* raw = c.get();
+    raw->ringInit = std::thread([raw] {
+        (void)hipSetDevice(raw->device);
+        if (hipHostMalloc(reinterpret_cast<void**>(&raw->ring), Ctx::kRingSlots * Ctx::kRingSlot, hipHostMallocPortable) !=
+            hipSuccess) {
+            raw->ring = nullptr;
+            raw->ringFailed = true;
+        }
+    });
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
             SH_HIP(hipEventCreate(e));
@@ -381,9 +398,6 @@ static bool stageIn(Ctx* c, uint8_t* dst, const uint8_t* src, size_t n) {
         c->nibHostCap = 0;
         SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->nibHost), nb));
         c->nibHostCap = nb;
-        void* d = nullptr;
-        SH_HIP(hipHostGetDevicePointer(&d, c->nibHost, 0));
-        c->nibDev = static_cast<const uint8_t*>(d);
     }
     c->nibPats.reserve(nb + 8);
     SH_HIP(hipStreamSynchronize(c->st));  // the pinned buffer may still feed the last call's DMA
@@ -440,15 +454,13 @@ static inline uint64_t badRanks8(uint64_t v, uint64_t big) {
     return (v & 0xF0F0F0F0F0F0F0F0ull) | ((v - ones) & ~v & highs) | ((v + big) & highs);
 }
 
-// Symbols [2 lo, 2 hi) of src (one per byte) -> bytes [lo, hi) of out, two per
-// byte (low nibble first); nsym = all symbols of the upload (an odd last one
-// is packed alone). Returns nonzero if any symbol is no rank in [1, sigma).
-static uint64_t packNibblesScalar(const uint8_t* src, uint8_t* out, uint64_t lo, uint64_t hi, uint64_t nsym,
-                                  uint32_t sigma) {
+// 2 * count symbols of `in` (one per byte) -> count bytes of `out`, two per
+// byte (low nibble first); the bytes from `full` on hold one symbol each (the
+// odd last symbol of an upload). Returns nonzero if any symbol is no rank in
+// [1, sigma).
+static uint64_t packNibblesScalar(const uint8_t* in, uint8_t* out, uint64_t full, uint64_t count, uint32_t sigma) {
     const uint64_t big = (uint64_t)(0x80u - sigma) * 0x0101010101010101ull;
-    const uint64_t full = std::min(hi, nsym / 2);  // bytes with both symbols
-    const uint8_t* in = src + 2 * lo;
-    uint64_t acc = 0, i = lo;
+    uint64_t acc = 0, i = 0;
     for (; i + 4 <= full; i += 4, in += 8) {  // 8 symbols -> 4 bytes
         uint64_t v;
         std::memcpy(&v, in, 8);
@@ -462,7 +474,7 @@ static uint64_t packNibblesScalar(const uint8_t* src, uint8_t* out, uint64_t lo,
         out[i] = (uint8_t)(in[0] | (in[1] << 4));
         acc |= (uint64_t)(in[0] == 0 || in[0] >= sigma || in[1] == 0 || in[1] >= sigma);
     }
-    for (; i < hi; ++i, in += 2) {  // the odd last symbol
+    for (; i < count; ++i, in += 2) {  // the odd last symbol
         out[i] = in[0];
         acc |= (uint64_t)(in[0] == 0 || in[0] >= sigma);
     }
@@ -473,16 +485,15 @@ static uint64_t packNibblesScalar(const uint8_t* src, uint8_t* out, uint64_t lo,
 // (lo * 1 + hi * 16), packed to bytes; ranks checked as max(v - 1, sigma - 2)
 // == sigma - 2. About a tenth of the scalar instructions per byte, so that
 // 16 host threads pack faster than the GPU searches (the streamed upload).
-__attribute__((target("avx2"))) static uint64_t packNibblesAvx2(const uint8_t* src, uint8_t* out, uint64_t lo,
-                                                                uint64_t hi, uint64_t nsym, uint32_t sigma) {
+__attribute__((target("avx2"))) static uint64_t packNibblesAvx2(const uint8_t* in, uint8_t* out, uint64_t full,
+                                                                uint64_t count, uint32_t sigma) {
     const __m256i mult = _mm256_set1_epi16(0x1001), one = _mm256_set1_epi8(1);
     const __m256i lim = _mm256_set1_epi8((char)(sigma - 2));
     __m256i bad = _mm256_setzero_si256();
-    const uint64_t full = std::min(hi, nsym / 2);
-    uint64_t i = lo;
+    uint64_t i = 0;
     for (; i + 32 <= full; i += 32) {
-        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 2 * i));
-        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 2 * i + 32));
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + 2 * i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + 2 * i + 32));
         const __m256i ta = _mm256_sub_epi8(a, one), tb = _mm256_sub_epi8(b, one);
         bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(ta, lim), lim));
         bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(tb, lim), lim));
@@ -490,7 +501,8 @@ __attribute__((target("avx2"))) static uint64_t packNibblesAvx2(const uint8_t* s
         _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i),
                             _mm256_permute4x64_epi64(_mm256_packus_epi16(pa, pb), 0xD8));
     }
-    return (uint64_t)!_mm256_testz_si256(bad, bad) | packNibblesScalar(src, out, i, hi, nsym, sigma);
+    return (uint64_t)!_mm256_testz_si256(bad, bad) |
+           packNibblesScalar(in + 2 * i, out + i, full - i, count - i, sigma);
 }
 
 // Nonzero if any byte of [p, p + n) is no rank in [1, sigma).
@@ -527,11 +539,12 @@ HostPool& hostPool(Ctx* c) {
     return *c->pool;
 }
 
-// Packs the next chunk of the streamed upload (Ctx::Upload) on the host,
-// enqueues its DMA on stE (nothing else: the DMAs run back to back at the
-// link's rate) and, on stream `kst` after the DMA's event, the unpack (and
-// reverse-complement interleave) kernel and both pattern packings. A chunk
-// with a byte that is no rank sets up.bad and enqueues nothing.
+// Packs the next chunk of the streamed upload (Ctx::Upload) on the host into
+// its ring slot, enqueues the slot's DMA on stE (nothing else: the DMAs run
+// back to back at the link's rate) and, on stream `kst` after the DMA's event,
+// the unpack (and reverse-complement interleave) kernel and both pattern
+// packings. A chunk with a byte that is no rank sets up.bad and enqueues
+// nothing.
 void uploadChunk(Ctx* c, hipStream_t kst) {
     Ctx::Upload& U = c->up;
     const auto t0 = std::chrono::steady_clock::now();
@@ -540,27 +553,30 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     const uint64_t s0 = r0 * m, s1 = r1 * m, nsym = U.rows * m;  // symbols
     uint8_t* raw = U.rc ? c->readRaw.ptr : c->rawPats.ptr;
     HostPool& P = hostPool(c);
-    hipStream_t dst = c->stE;  // (two upload streams, alternating chunks, measured no faster)
     const unsigned nt = P.size();
     std::atomic<int> bad{0};
     // pieces of 1 MB of packed bytes spread over the pool (a chunk at C3 is
     // ~25 MB packed); one DMA per chunk, overlapping the next chunk's packing
     constexpr uint64_t kPiece = 1u << 20;
     const bool avx2 = hostHasAvx2();
+    const uint64_t j = r0 / U.chunk;
+    const size_t slot = (size_t)(j % Ctx::kRingSlots);
     if (U.nibble) {
         const uint64_t b0 = s0 / 2, b1 = (s1 + 1) / 2;  // packed bytes (s0 is even)
         const uint64_t pieces = (b1 - b0 + kPiece - 1) / kPiece;
-        uint8_t* out = c->nibHost;
+        SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
+        uint8_t* out = c->ring + slot * Ctx::kRingSlot;
         P.run([&](unsigned t) {
             for (uint64_t k = t; k < pieces; k += nt) {
                 const uint64_t lo = b0 + k * kPiece, hi = std::min(b1, lo + kPiece);
-                const uint64_t acc = avx2 ? packNibblesAvx2(U.src, out, lo, hi, nsym, sigma)
-                                          : packNibblesScalar(U.src, out, lo, hi, nsym, sigma);
+                const uint64_t full = std::min(hi, std::max(lo, nsym / 2)) - lo;  // bytes with two symbols
+                const uint8_t* in = U.src + 2 * lo;
+                const uint64_t acc = avx2 ? packNibblesAvx2(in, out + (lo - b0), full, hi - lo, sigma)
+                                          : packNibblesScalar(in, out + (lo - b0), full, hi - lo, sigma);
                 if (acc) bad.store(1, std::memory_order_relaxed);
             }
         });
-        if (!bad.load() && !U.zeroCopy)
-            SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out + b0, b1 - b0, hipMemcpyHostToDevice, dst));
+        if (!bad.load()) SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, b1 - b0, hipMemcpyHostToDevice, c->stE));
     } else {  // one byte per symbol (SAHARA_NIBBLE_UPLOAD=0): check, then copy as given
         const uint64_t pieces = (s1 - s0 + kPiece - 1) / kPiece;
         P.run([&](unsigned t) {
@@ -571,26 +587,16 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
                 if (acc) bad.store(1, std::memory_order_relaxed);
             }
         });
-        if (!bad.load()) SH_HIP(hipMemcpyAsync(raw + s0, U.src + s0, s1 - s0, hipMemcpyHostToDevice, dst));
+        if (!bad.load()) SH_HIP(hipMemcpyAsync(raw + s0, U.src + s0, s1 - s0, hipMemcpyHostToDevice, c->stE));
     }
     U.hostMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (bad.load()) {
         U.bad = true;
         return;
     }
-    const uint64_t j = r0 / U.chunk;
-    while (c->upEv.size() <= j) {
-        hipEvent_t e;
-        SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->upEv.push_back(e);
-    }
-    if (U.nibble && U.zeroCopy) {  // the unpack kernel reads the pinned host buffer over PCIe itself
-        launchUnpackNibbles(c->nibDev + s0 / 2, raw + s0, s1 - s0, kst);
-    } else {
-        SH_HIP(hipEventRecord(c->upEv[j], dst));  // the chunk's DMA
-        SH_HIP(hipStreamWaitEvent(kst, c->upEv[j], 0));
-        if (U.nibble) launchUnpackNibbles(c->nibPats.ptr + s0 / 2, raw + s0, s1 - s0, kst);
-    }
+    SH_HIP(hipEventRecord(c->ringEv[slot], c->stE));  // the chunk's DMA
+    SH_HIP(hipStreamWaitEvent(kst, c->ringEv[slot], 0));
+    if (U.nibble) launchUnpackNibbles(c->nibPats.ptr + s0 / 2, raw + s0, s1 - s0, kst);
     const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
     if (U.rc) launchInterleaveRC(c->readRaw.ptr, r0, r1, m, sigma, c->npat, c->rawPats.ptr, kst);
     if (p1 > p0) {
@@ -598,7 +604,6 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
                            c->badFlag.ptr, kst);
         launchPackPatterns3(c->rawPats.ptr + p0 * m, p1 - p0, m, c->patBlocks, c->pats3.ptr + p0 * c->patBlocks, kst);
     }
-    U.last = (int64_t)j;
     U.done = r1;
 }
 
@@ -672,30 +677,16 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     U.rows = rows;
     if (const char* e = std::getenv("SAHARA_NIBBLE_UPLOAD")) c->nibbleUpload = std::atoi(e) != 0;
     U.nibble = c->nibbleUpload;
-    // 1M patterns per chunk (~50 MB packed at m = 100; SAHARA_UPLOAD_CHUNK)
+    // 1M patterns per chunk (SAHARA_UPLOAD_CHUNK), at most one ring slot of packed bytes
     uint64_t chunkPats = 1u << 20;
     if (const char* e = std::getenv("SAHARA_UPLOAD_CHUNK")) chunkPats = std::max<uint64_t>(2, std::atoll(e));
-    U.chunk = std::max<uint64_t>(2, (rc ? chunkPats / 2 : chunkPats) & ~uint64_t(1));
-    SH_HIP(hipStreamSynchronize(c->stE));  // the pinned staging buffer may still feed the last call's DMA
-    if (U.nibble) {
-        const size_t nb = (rows * m + 1) / 2;
-        if (c->nibHostCap < nb) {
-            if (c->nibHost) SH_HIP(hipHostFree(c->nibHost));
-            c->nibHost = nullptr;
-            c->nibHostCap = 0;
-            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->nibHost), nb));
-            c->nibHostCap = nb;
-            void* d = nullptr;
-            SH_HIP(hipHostGetDevicePointer(&d, c->nibHost, 0));
-            c->nibDev = static_cast<const uint8_t*>(d);
-        }
-        // default: one DMA per chunk into device memory, unpacked there;
-        // SAHARA_UPLOAD_DMA=0: the unpack kernel reads the pinned host buffer
-        // itself (measured slower at C3: 296M against 358M reads/s)
-        const char* dmaEnv = std::getenv("SAHARA_UPLOAD_DMA");
-        U.zeroCopy = dmaEnv && std::atoi(dmaEnv) == 0;
-        if (!U.zeroCopy) c->nibPats.reserve(nb + 8);
-    }
+    uint64_t chunk = rc ? chunkPats / 2 : chunkPats;
+    if (U.nibble) chunk = std::min<uint64_t>(chunk, Ctx::kRingSlot * 2 / m);
+    U.chunk = std::max<uint64_t>(2, chunk & ~uint64_t(1));
+    if (c->ringInit.joinable()) c->ringInit.join();
+    if (U.nibble && !c->ring) throw Error("could not pin the upload ring buffer");
+    for (hipEvent_t e : c->ringEv) SH_HIP(hipEventSynchronize(e));  // the last call's DMAs
+    if (U.nibble) c->nibPats.reserve((rows * m + 1) / 2 + 8);
     SH_HIP(hipMemsetAsync(c->badFlag.ptr, 0, sizeof(uint32_t), c->stE));
     c->stageMs = 0;
     c->staged = c->streaming = true;
@@ -1435,7 +1426,7 @@ static HitPool& hitPool() {
 
 // Host buffer for n hits (released with sahara_gpu_free); *pinned tells
 // whether the device can copy into it directly.
-static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr) {
+static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr, bool mayPin = true) {
     const size_t bytes = std::max<uint64_t>(n, 1) * sizeof(sahara_hit);
     *pinned = false;
     if (capHits) *capHits = std::max<uint64_t>(n, 1);
@@ -1465,6 +1456,7 @@ static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr) {
         *pinned = true;
         return p;
     }
+    if (!mayPin) return std::malloc(bytes);  // a one-off caller: pinning would cost more than it saves
     const size_t huge = 2u << 20, cap = (bytes + bytes / 8 + huge - 1) / huge * huge;  // room for a run with more hits
     if (hipHostMalloc(&p, cap, hipHostMallocPortable) == hipSuccess && p) {
         std::lock_guard<std::mutex> g(P.mu);
@@ -1554,13 +1546,18 @@ static void drainAll(Ctx* c) {
 static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t len,
                            const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit,
                            uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits) {
+    using clk = std::chrono::steady_clock;
+    const auto tA = clk::now();
     stageStreamed(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit);
+    const auto tB = clk::now();
     c->sink = nullptr;
     c->sinkCap = 0;
     if (!max_hits) {  // sized from the last call (the bench's steady state), else 2 hits per pattern
+        // a first call takes a pooled buffer if there is one, but pins none:
+        // pinning ~1 GB costs ~200 ms, ten times the pageable copy-out
         const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
         bool pinned = false;
-        void* p = allocHits(est, &pinned, &c->sinkCap);
+        void* p = allocHits(est, &pinned, &c->sinkCap, c->lastHits != 0);
         if (p && pinned) {
             c->sink = static_cast<sahara_hit*>(p);
         } else {
@@ -1568,6 +1565,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
             c->sinkCap = 0;
         }
     }
+    const auto tC = clk::now();
     try {
         run(c, false);
         uint32_t bad = 0;
@@ -1600,7 +1598,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
             bool pinned = buf != nullptr;
             if (!buf) {
                 c->sinkDone = 0;
-                buf = static_cast<sahara_hit*>(allocHits(c->nout, &pinned));
+                buf = static_cast<sahara_hit*>(allocHits(c->nout, &pinned, nullptr, c->lastHits != 0));
                 if (!buf) throw Error("out of host memory for hits");
             }
             if (c->nout > c->sinkDone) {  // the rest (or all) of the hits
@@ -1624,6 +1622,11 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
     freeHits(buf);  // the sink of a max_hits call
     c->lastHits = c->nout;
     c->stats.output_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (std::getenv("SAHARA_TIMING")) {  // where a call's wall time goes (stderr)
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[sahara] stage %.1f ms, sink %.1f ms, pass %.1f ms (host packing %.1f ms), output %.1f ms\n",
+                     ms(tA, tB), ms(tB, tC), ms(tC, t0), c->up.hostMs, c->stats.output_ms);
+    }
 }
 
 int sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,

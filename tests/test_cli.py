@@ -84,6 +84,27 @@ def test_search_invalid_query_character(tmp_path):
     assert "query 'q2' (3) has invalid character at position 5 'X'(58)" in err
 
 
+def test_index_crlf_multiline_records_count_positions_in_sequence(tmp_path):
+    """The parallel ingest (fasta.h parseFastaParallel) reads records across
+    lines and CRLF breaks like ivio's reader: positions count sequence
+    characters only, and the header keeps its text after '>'."""
+    fa = write(tmp_path / "r.fa", ">r1\r\nACGT\r\nACGT\r\n>r2 x>y\r\nAC\r\n\r\nGTXA\r\n")
+    rc, _, err = run("index", fa)
+    assert rc == 1 and "ref 'r2 x>y' (2) has invalid character 'X' (0x58) at position 4" in err
+
+
+def test_fasta_sequence_before_header_is_an_error(tmp_path):
+    fa = write(tmp_path / "r.fa", "ACGT\n>r1\nACGT\n")
+    rc, _, err = run("index", fa)
+    assert rc == 1 and "malformed FASTA" in err
+
+
+def test_search_invalid_query_numbering_without_reverse(tmp_path):
+    q = write(tmp_path / "q.fa", ">q1\nACGTACGT\n>q2\nACGTAXGT\n")
+    rc, _, err = run("search", "-q", q, "-i", os.path.join(GOLD, IDX["a"]), "--no-reverse")
+    assert rc == 1 and "query 'q2' (2) has invalid character at position 5 'X'(58)" in err
+
+
 def test_search_empty_queries(tmp_path):
     q = write(tmp_path / "q.fa", "")
     rc, _, err = run("search", "-q", q, "-i", os.path.join(GOLD, IDX["a"]))
@@ -162,6 +183,24 @@ def test_cli_limit_queries_and_max_hits(tmp_path, gpu_device):
     want = limit_rows(want[want[:, 0] < 33], 2)
     assert np.array_equal(hits_as_rows(read_hits(out, 4)), want)
     assert "fwd queries: 16\nbwd queries: 17\n" in so
+
+
+@pytest.mark.gpu
+def test_cli_crlf_wrapped_queries_equal_golden(tmp_path, gpu_device):
+    """The same reads as CRLF records wrapped at 7 columns: the same hits."""
+    recs = []
+    for line in open(os.path.join(GOLD, "reads_a.fa")):
+        line = line.rstrip("\n")
+        if line.startswith(">"):
+            recs.append([line, ""])
+        else:
+            recs[-1][1] += line
+    text = "".join(h + "\r\n" + "".join(s[i:i + 7] + "\r\n" for i in range(0, len(s), 7)) for h, s in recs)
+    q = write(tmp_path / "q.fa", text)
+    out = tmp_path / "h.txt"
+    rc, _, err = run("search", "-q", q, "-i", os.path.join(GOLD, IDX["a"]), "-e", 2, "--emit-errors", "-o", out)
+    assert rc == 0, err
+    assert np.array_equal(hits_as_rows(read_hits(out, 4)), expected("a_lev_k2"))
 
 
 @pytest.mark.gpu
