@@ -30,6 +30,7 @@
 
 #include "../../include/sahara_hip.h"
 #include "fasta.h"
+#include "shard.h"
 
 using namespace sahara_cli;
 
@@ -379,13 +380,16 @@ int cmdSearch(int argc, char** argv) {
     // index residency (search.cpp:162-169): one context per device, the
     // devices loading the one mapped .idx image side by side
     std::vector<void*> ctx(ngpu, nullptr);
+    std::vector<double> devLoad(ngpu, 0.0);
     {
         MappedFile img(index.value);
         std::vector<std::string> errs(ngpu);
         std::vector<std::thread> th;
         for (uint32_t g = 0; g < ngpu; ++g)
             th.emplace_back([&, g] {
+                const auto t0 = std::chrono::steady_clock::now();
                 if (sahara_gpu_open((int)g, img.data, img.size, &ctx[g]) != 0) errs[g] = sahara_gpu_last_error();
+                devLoad[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             });
         for (auto& t : th) t.join();
         for (uint32_t g = 0; g < ngpu; ++g)
@@ -461,15 +465,16 @@ int cmdSearch(int argc, char** argv) {
     // search + locate (search.cpp:218-250), reads sharded over the devices
     // (a read and its reverse complement stay together; qids stay global)
     std::vector<HitPart> parts(ngpu);
-    std::vector<double> devLocate(ngpu, 0.0);
+    std::vector<double> devLocate(ngpu, 0.0), devSearch(ngpu, 0.0);
     std::vector<std::string> errs(ngpu);
     {
         std::vector<std::thread> th;
         for (uint32_t g = 0; g < ngpu; ++g) {
             th.emplace_back([&, g] {
-                const size_t r0 = nreads * g / ngpu, r1 = nreads * (g + 1) / ngpu;
+                const QueryShard sh = queryShard(nq, per, ngpu, g);
+                const size_t r0 = sh.r0, r1 = sh.r1, q0 = sh.q0, q1 = sh.q1;
                 if (r0 == r1) return;
-                const size_t q0 = per * r0, q1 = std::min(nq, per * r1);  // this shard's queries
+                const auto t0 = std::chrono::steady_clock::now();
                 sahara_hit* hits = nullptr;
                 uint64_t nh = 0;
                 int rc;
@@ -507,6 +512,7 @@ int cmdSearch(int argc, char** argv) {
                 sahara_stats st{};
                 sahara_gpu_stats(ctx[g], &st);
                 devLocate[g] = (st.locate_ms + st.sort_ms) / 1e3;
+                devSearch[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 parts[g] = HitPart{hits, nh, q0};  // released after writing
             });
         }
@@ -538,6 +544,10 @@ int cmdSearch(int argc, char** argv) {
     std::printf("  total time:          %10.2fs\n", total);
     std::printf("  queries per second:  %10.0fq/s\n", (double)nq / total);
     std::printf("  number of hits:      %10llu\n", (unsigned long long)nhits);
+    if (ngpu > 1)  // --gpus N: each device's index load and search (an imbalance shows by name)
+        for (uint32_t g = 0; g < ngpu; ++g)
+            std::printf("  device %u:            ld index %.2fs, search %.2fs, hits %llu\n", g, devLoad[g],
+                        devSearch[g], (unsigned long long)parts[g].n);
     return 0;
 }
 
