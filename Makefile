@@ -46,8 +46,34 @@ tools/gather_bench: tools/gather_bench.hip
 oracle:
 	$(MAKE) -C oracle
 
+# Host sanitizer builds: AddressSanitizer + UBSan on the host code
+# only (no GPU sanitizer on this pool). tools/asan_cpu_tests.sh runs the CPU
+# test suite against them.
+ASAN_HOST := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
+ASANDIR   := build/asan
+ASAN_OBJS := $(ASANDIR)/index_build.o $(ASANDIR)/search.o $(ASANDIR)/capi.o $(ASANDIR)/host_util.o $(ASANDIR)/scheme.o
+
+$(ASANDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(ASANDIR)
+	$(HIPCC) $(HIPFLAGS) -O1 $(ASAN_HOST) -c $< -o $@
+
+$(ASANDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(ASANDIR)
+	$(HIPCC) $(HIPFLAGS) -O1 $(ASAN_HOST) -c $< -o $@
+
+$(ASANDIR)/libsahara_hip.so: $(ASAN_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(ASAN_OBJS) -o $@ -lpthread
+
+bin/sahara_asan: $(CLI_SRC) $(wildcard sahara_amd/cli/*.h) include/sahara_hip.h $(LIB)
+	@mkdir -p bin
+	g++ -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer -Iinclude $(CLI_SRC) -o $@ \
+	    -L$(LIBDIR) -lsahara_hip -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+asan: $(ASANDIR)/libsahara_hip.so bin/sahara_asan
+	$(MAKE) -C oracle asan
+
 clean:
 	rm -rf build $(LIBDIR) bin
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle asan

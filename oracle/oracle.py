@@ -30,7 +30,8 @@ class Counters(C.Structure):
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        # ORACLE_LIB: another build of the same restatement (the sanitizer build, tools/asan_cpu_tests.sh)
+        path = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(path):
             raise RuntimeError(f"oracle not built: {path} missing (run `make -C oracle`)")
         L = C.CDLL(path)

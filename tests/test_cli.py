@@ -12,7 +12,7 @@ from helpers import hits_as_rows
 from test_golden import CASES, GOLD, IDX, expected, limit_rows
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SAHARA = os.path.join(ROOT, "bin", "sahara")
+SAHARA = os.environ.get("SAHARA_CLI") or os.path.join(ROOT, "bin", "sahara")  # SAHARA_CLI: e.g. bin/sahara_asan
 
 
 def run(*args, cwd=None):
