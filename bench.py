@@ -330,12 +330,15 @@ def main():
     # like `value`: warmup calls, then --steps calls, each handing its hit
     # buffer back before the next (sahara_gpu_free)
     if not args.no_e2e:
-        w2 = min(args.warmup, 2)
+        # two warmup calls whatever --warmup says: the first sizes the hit
+        # buffer from its own result, the second pins it into the pool that
+        # every later call draws from (capi.cpp allocHits)
+        w2 = 2
         # the reads cross PCIe, reverse complements interleaved on the device
         # (sahara_gpu_search_reads: what `sahara search` calls)
         extra["pcie_inclusive"] = pcie_inclusive(
             lambda: sa.search_reads(idx, reads, scheme, edit=edit), idx, nreads, args.steps, w2, world, barrier, nh,
-            "sahara_gpu_search_reads from host reads: streamed upload (two symbols per byte) + device RC interleave, "
+            "sahara_gpu_search_reads from host reads: streamed upload (four symbols per byte, N listed) + device RC interleave, "
             "search, locate, sort, hits D2H batch by batch into pinned host memory recycled through sahara_gpu_free")
         # the interleaved patterns cross PCIe (the reference's queries vector, sahara_gpu_search)
         extra["pcie_inclusive_patterns"] = pcie_inclusive(
@@ -564,7 +567,8 @@ def pcie_inclusive(search, idx, nreads, steps, warmup, world, barrier, local_hit
     return {"reads_per_s": round(nreads * world * steps / el, 1), "ms_per_step": round(el * 1e3 / steps, 2),
             "steps": steps, "warmup": warmup, "hits": int(n), "same_hits": int(n) == int(local_hits),
             "stage_ms": round(acc["stage_ms"] / steps, 2), "search_ms": round(acc["total_ms"] / steps, 2),
-            "output_ms": round(acc["output_ms"] / steps, 2), "path": path}
+            "output_ms": round(acc["output_ms"] / steps, 2),
+            "upload_chunks_2_4_8_bits": list(idx.stats()["upload_chunks"]), "path": path}
 
 
 def reference_path(idx, ref_cnt, nreads, pat_bytes, steps, world, barrier, config):

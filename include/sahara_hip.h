@@ -88,9 +88,10 @@ typedef struct sahara_stats {
     uint32_t pipelined;          /* 1 if FM and text phases of consecutive batches overlapped */
     double   seed_ms;            /* starting cursors (k-mer table lookups) */
     uint64_t text_steps;         /* text-kernel micro-steps, lane count (count=1) */
-    double   stage_ms;           /* wall time of staging the patterns: H2D, 4-bit packing, rank check */
+    double   stage_ms;           /* host time of staging the patterns: 2- / 4-bit packing, rank check, H2D enqueue */
     double   output_ms;          /* sahara_gpu_search: wall time of handing the hits to the host */
     uint64_t text_launches;      /* text-phase kernel launches in the pass */
+    uint64_t upload_chunks[3];   /* streamed upload chunks sent at 2 / 4 / 8 bits per symbol */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);
@@ -225,6 +226,14 @@ int  sahara_synth_reads(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t
 int  sahara_synth_reads_typed(const uint8_t* ranks, const uint64_t* rec_lens, uint64_t n_records, uint32_t sigma,
                               uint64_t n_reads, uint32_t len, uint32_t substitutions, uint32_t insertions,
                               uint32_t deletions, uint32_t errors, uint64_t seed, uint8_t* out, uint64_t* origin);
+/* Host half of the streamed upload at two bits per symbol (test hook; the
+ * search calls do this themselves): n ranks -> (n + 3) / 4 bytes in out,
+ * symbol i at bits 2 (i % 4) of byte i / 4, A C G T coded 0 1 2 3; dna5's N
+ * (rank 4 of sigma 6) is coded 0 and its position listed in n_pos (first
+ * pos_cap of them), *n_count = how many. scalar != 0 skips the AVX2 packer.
+ * Returns 1 if a symbol is no rank in [1, sigma), 0 if all are, -1 on error. */
+int  sahara_pack_2bit(const uint8_t* ranks, uint64_t n, uint32_t sigma, int scalar, uint8_t* out, uint32_t* n_pos,
+                      uint64_t pos_cap, uint64_t* n_count);
 /* Reverse complement interleave of search.cpp:121-123: out[2i] = read i,
  * out[2i+1] = its reverse complement (A<->T, C<->G, N->N). */
 int  sahara_interleave_rc(const uint8_t* reads, uint64_t n_reads, uint32_t len, uint32_t sigma, uint8_t* out);

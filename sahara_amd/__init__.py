@@ -60,10 +60,12 @@ class Stats(C.Structure):
                 ("text_cycles_step", C.c_uint64), ("text_cycles_emit", C.c_uint64),
                 ("text_compare_steps", C.c_uint64), ("text_grid", C.c_uint32), ("pipelined", C.c_uint32),
                 ("seed_ms", C.c_double), ("text_steps", C.c_uint64), ("stage_ms", C.c_double),
-                ("output_ms", C.c_double), ("text_launches", C.c_uint64)]
+                ("output_ms", C.c_double), ("text_launches", C.c_uint64),
+                ("upload_chunks", C.c_uint64 * 3)]
 
     def as_dict(self):
-        return {n: getattr(self, n) for n, _ in self._fields_}
+        return {n: (list(v) if isinstance(v, C.Array) else v) for n, v in
+                ((n, getattr(self, n)) for n, _ in self._fields_)}
 
 
 EXPORTED = {
@@ -114,6 +116,8 @@ EXPORTED = {
     "sahara_synth_reads_typed": (C.c_int, [u8p, u64p, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
                                            C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, u8p, u64p]),
     "sahara_interleave_rc": (C.c_int, [u8p, C.c_uint64, C.c_uint32, C.c_uint32, u8p]),
+    "sahara_pack_2bit": (C.c_int, [u8p, C.c_uint64, C.c_uint32, C.c_int, u8p, u32p, C.c_uint64,
+                                   C.POINTER(C.c_uint64)]),
 }
 
 
@@ -460,6 +464,21 @@ def synth_reads(flat, rec_lens, n_reads, length, errors, sigma=6, seed=7, with_o
                                           substitutions, insertions, deletions, errors, seed, _p(out, u8p),
                                           _p(origin, u64p)))
     return (out, origin) if with_origin else out
+
+
+def pack_2bit(ranks, sigma=6, scalar=False):
+    """Host half of the streamed upload at two bits per symbol (capi.cpp
+    pack2Avx2 / pack2Scalar): (packed bytes, N positions, bad-rank flag)."""
+    r = np.ascontiguousarray(ranks, dtype=np.uint8).ravel()
+    out = np.zeros((r.size + 3) // 4, np.uint8)
+    cnt = C.c_uint64(0)
+    rc = lib().sahara_pack_2bit(_p(r, u8p), r.size, sigma, int(scalar), _p(out, u8p), None, 0, C.byref(cnt))
+    if rc < 0:
+        _check(rc)
+    pos = np.zeros(max(1, cnt.value), np.uint32)
+    lib().sahara_pack_2bit(_p(r, u8p), r.size, sigma, int(scalar), _p(out, u8p), _p(pos, u32p), pos.size,
+                           C.byref(cnt))
+    return out, pos[:cnt.value], bool(rc)
 
 
 def interleave_rc(reads, sigma=6):

@@ -94,6 +94,125 @@ private:
     bool stop_ = false;
 };
 
+// Host side of sahara_gpu_search's compact hit download: batch by batch, the
+// 8-B records (search.hip kCompactHits) land in pinned staging memory on
+// stream stF, and this thread expands them into the caller's sahara_hit
+// buffer (record id by binary search over the record starts) on a few worker
+// threads while later batches still search. Cuts the PCIe download to a third
+// (8 of 24 B per hit).
+class Expander {
+public:
+    struct Job {
+        hipEvent_t ev;           // the batch's download is done
+        const uint64_t* src;     // compact records (pinned staging)
+        sahara_hit* dst;
+        uint64_t n, q0;          // records; the batch's first qid
+    };
+    Expander(int device, unsigned workers) : device_(device), pool_(workers) {
+        th_ = std::thread([this] { loop(); });
+    }
+    ~Expander() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void setStarts(const std::vector<uint64_t>* starts) { starts_ = starts; }
+    std::function<void(const char*, uint64_t)> mark;  // SAHARA_TIMING=2 trace
+    void submit(const Job& j) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(j);
+            ++submitted_;
+        }
+        cv_.notify_all();
+    }
+    // waits until the first n jobs submitted since reset() are expanded
+    void waitFor(uint64_t n) {
+        std::unique_lock<std::mutex> lk(mu_);
+        idle_.wait(lk, [&] { return done_ >= n || err_; });
+    }
+    void reset() {
+        drain();
+        std::lock_guard<std::mutex> g(mu_);
+        submitted_ = done_ = 0;
+    }
+    // waits until every submitted batch is expanded; rethrows the first failure
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu_);
+        idle_.wait(lk, [&] { return q_.empty() && !busy_; });
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            std::rethrow_exception(e);
+        }
+    }
+
+private:
+    void loop() {
+        (void)hipSetDevice(device_);
+        for (;;) {
+            Job j{};
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                j = q_.front();
+                q_.erase(q_.begin());
+                busy_ = true;
+            }
+            try {
+                SH_HIP(hipEventSynchronize(j.ev));
+                if (mark) mark("expand", done_);
+                expand(j);
+                if (mark) mark("expanded", done_);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!err_) err_ = std::current_exception();
+            }
+            std::lock_guard<std::mutex> g(mu_);
+            busy_ = false;
+            ++done_;
+            idle_.notify_all();
+        }
+    }
+    void expand(const Job& j) {
+        const std::vector<uint64_t>& S = *starts_;
+        const unsigned nt = pool_.size();
+        const uint64_t per = (j.n + nt - 1) / nt;
+        pool_.run([&](unsigned t) {
+            const uint64_t b = std::min(j.n, (uint64_t)t * per), e = std::min(j.n, b + per);
+            uint32_t seq = 0;
+            uint64_t lo = 1, hi = 0;  // the current record's [start, next start): empty
+            for (uint64_t i = b; i < e; ++i) {
+                const uint64_t v = j.src[i], g = (v >> 4) & 0xFFFFFFFFull;
+                if (g < lo || g >= hi) {  // hits come sorted by (qid, seq_id, pos): mostly the same record
+                    seq = (uint32_t)(std::upper_bound(S.begin(), S.end(), g) - S.begin() - 1);
+                    lo = S[seq];
+                    hi = seq + 1 < S.size() ? S[seq + 1] : UINT64_MAX;
+                }
+                sahara_hit& h = j.dst[i];
+                h.qid = j.q0 + (v >> 36);
+                h.seq_id = seq;
+                h.err = (uint32_t)(v & 15u);
+                h.pos = g - lo;
+            }
+        });
+    }
+    int device_;
+    HostPool pool_;
+    const std::vector<uint64_t>* starts_ = nullptr;
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_, idle_;
+    std::vector<Job> q_;
+    bool stop_ = false, busy_ = false;
+    uint64_t submitted_ = 0, done_ = 0;
+    std::exception_ptr err_;
+};
+
 struct Ctx {
     int device = 0;
     hipStream_t st = nullptr;
@@ -166,13 +285,15 @@ struct Ctx {
     struct Upload {
         const uint8_t* src = nullptr;  // host symbols: the patterns, or the reads (rc)
         bool rc = false;               // reads: reverse complements interleaved on the device
-        bool nibble = true;
+        uint32_t bits = 4;             // 2: ACGT codes + N list, 4: nibbles, 8: bytes as given
         uint64_t rows = 0;             // source rows
         uint64_t chunk = 0;            // source rows per chunk (even: chunks start at even symbols)
         uint64_t done = 0;             // source rows enqueued
         bool bad = false;              // a chunk held a byte that is no rank of this index
         double hostMs = 0;             // host time spent packing and enqueueing
+        uint64_t chunks[3] = {0, 0, 0};  // chunks sent at 2 / 4 / 8 bits per symbol
     } up;
+    std::vector<std::vector<uint32_t>> excParts;  // per packing thread: N positions of a 2-bit chunk
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
     static constexpr size_t kRingSlots = 8, kRingSlot = 32u << 20;  // 256 MB pinned
@@ -189,8 +310,33 @@ struct Ctx {
     uint64_t sinkCap = 0, sinkDone = 0;
     bool sinkOk = false;
     uint64_t lastHits = 0;                // hits of the previous sahara_gpu_search (sink size estimate)
+    // compact download into the sink (Expander): device records of the
+    // pass, their pinned host staging, one event per batch's download
+    // (batch b's records land in slot b % kDownSlots of a pinned ring,
+    // pinned with the upload ring; the slot is reused once batch b is expanded)
+    bool compactSink = false, sinkPinned = false;
+    DevBuf<uint64_t> outC;
+    static constexpr size_t kDownSlots = 3, kDownSlot = 64u << 20;  // 8M records per batch
+    uint64_t* downRing = nullptr;
+    uint64_t downJobs = 0;                // batches handed to the expander this call
+    std::vector<hipEvent_t> downEv;
+    std::unique_ptr<Expander> expander;
+    // SAHARA_TIMING=2: host-side marks of one call (ms since its start, what)
+    bool traceOn = false;
+    std::chrono::steady_clock::time_point traceT0;
+    std::mutex traceMu;
+    std::vector<std::pair<double, std::string>> trace;
+    void mark(const char* what, uint64_t i) {
+        if (!traceOn) return;
+        const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - traceT0).count();
+        std::lock_guard<std::mutex> g(traceMu);
+        trace.emplace_back(t, std::string(what) + " " + std::to_string(i));
+    }
 
     ~Ctx() {
+        expander.reset();
+        for (hipEvent_t e : downEv) (void)hipEventDestroy(e);
+        if (downRing) (void)hipHostFree(downRing);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (ringInit.joinable()) ringInit.join();
@@ -296,6 +442,9 @@ Ctx* newCtx(int device) {
             raw->ring = nullptr;
             raw->ringFailed = true;
         }
+        if (hipHostMalloc(reinterpret_cast<void**>(&raw->downRing), Ctx::kDownSlots * Ctx::kDownSlot,
+                          hipHostMallocPortable) != hipSuccess)
+            raw->downRing = nullptr;  // no compact download: hits go to a pinned sink whole
     });
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
@@ -529,6 +678,68 @@ __attribute__((target("avx2"))) static uint64_t badRanksAvx2(const uint8_t* p, u
     return (uint64_t)!_mm256_testz_si256(bad, bad) | badRanksScalar(p + i, n - i, sigma);
 }
 
+// Two bits per symbol (SAHARA_UPLOAD_BITS=2, the default for DNA): `count`
+// symbols of `in` -> (count + 3) / 4 bytes of `out`, symbol i at bits
+// 2 (i % 4) of byte i / 4, coded A C G T = 0 1 2 3. dna5's N (rank 4 of
+// sigma 6) is coded 0 and its position (`base` + i) appended to `exc`; the
+// device unpacks through a 4-entry table and patches the listed N positions
+// (kUnpack2, kPatchRank). Returns nonzero if any symbol is no rank in [1, sigma).
+static uint64_t pack2Scalar(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
+                            std::vector<uint32_t>& exc) {
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < count; i += 4) {
+        uint32_t b = 0;
+        for (uint32_t q = 0; q < 4 && i + q < count; ++q) {
+            const uint32_t r = in[i + q];
+            bad |= (uint64_t)(r == 0 || r >= sigma);
+            uint32_t code = (r - 1u) & 3u;
+            if (sigma == 6 && r >= 4) {
+                if (r == 4) exc.push_back((uint32_t)(base + i + q));
+                code = r == 5 ? 3u : 0u;
+            }
+            b |= code << (2 * q);
+        }
+        out[i / 4] = (uint8_t)b;
+    }
+    return bad;
+}
+
+// The same with AVX2, 128 symbols -> 32 bytes per step: codes t = rank - 1
+// (dna5: T 4 -> 3, N 3 -> 0 and listed from a byte mask), pairs combined by
+// one multiply-add (t0 + 4 t1), pairs of pairs by another (+ 16), packed to
+// bytes and put back in order with one cross-lane permute.
+__attribute__((target("avx2"))) static uint64_t pack2Avx2(const uint8_t* in, uint8_t* out, uint64_t count,
+                                                          uint32_t sigma, uint64_t base, std::vector<uint32_t>& exc) {
+    const __m256i one = _mm256_set1_epi8(1), three = _mm256_set1_epi8(3), four = _mm256_set1_epi8(4);
+    const __m256i lim = _mm256_set1_epi8((char)(sigma - 2));
+    const __m256i m14 = _mm256_set1_epi16(0x0401), m116 = _mm256_set1_epi32(0x00100001);
+    const __m256i order = _mm256_setr_epi32(0, 4, 1, 5, 2, 6, 3, 7);
+    const bool dna5 = sigma == 6;
+    __m256i bad = _mm256_setzero_si256();
+    uint64_t i = 0;
+    for (; i + 128 <= count; i += 128) {
+        __m256i d[4];
+        for (int q = 0; q < 4; ++q) {
+            __m256i t = _mm256_sub_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + i + 32 * q)), one);
+            bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(t, lim), lim));
+            if (dna5) {
+                const __m256i isN = _mm256_cmpeq_epi8(t, three);
+                uint32_t msk = (uint32_t)_mm256_movemask_epi8(isN);
+                while (msk) {
+                    exc.push_back((uint32_t)(base + i + 32 * q + (uint32_t)__builtin_ctz(msk)));
+                    msk &= msk - 1u;
+                }
+                t = _mm256_andnot_si256(isN, _mm256_add_epi8(t, _mm256_cmpeq_epi8(t, four)));
+            }
+            t = _mm256_and_si256(t, three);
+            d[q] = _mm256_madd_epi16(_mm256_maddubs_epi16(t, m14), m116);
+        }
+        const __m256i b = _mm256_packus_epi16(_mm256_packus_epi32(d[0], d[1]), _mm256_packus_epi32(d[2], d[3]));
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i / 4), _mm256_permutevar8x32_epi32(b, order));
+    }
+    return (uint64_t)!_mm256_testz_si256(bad, bad) | pack2Scalar(in + i, out + i / 4, count - i, sigma, base + i, exc);
+}
+
 static bool hostHasAvx2() {
     static const bool has = __builtin_cpu_supports("avx2");
     return has;
@@ -548,6 +759,7 @@ HostPool& hostPool(Ctx* c) {
 void uploadChunk(Ctx* c, hipStream_t kst) {
     Ctx::Upload& U = c->up;
     const auto t0 = std::chrono::steady_clock::now();
+    c->mark("pack", U.done / std::max<uint64_t>(U.chunk, 1));
     const uint64_t r0 = U.done, r1 = std::min(U.rows, r0 + U.chunk);
     const uint32_t m = c->m, sigma = c->I.sigma;
     const uint64_t s0 = r0 * m, s1 = r1 * m, nsym = U.rows * m;  // symbols
@@ -561,11 +773,41 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     const bool avx2 = hostHasAvx2();
     const uint64_t j = r0 / U.chunk;
     const size_t slot = (size_t)(j % Ctx::kRingSlots);
-    if (U.nibble) {
-        const uint64_t b0 = s0 / 2, b1 = (s1 + 1) / 2;  // packed bytes (s0 is even)
+    // a chunk owns bytes [s0 / 2, (s1 + 1) / 2) of the ring slot and of the
+    // device staging buffer at any encoding (s0 is even)
+    const uint64_t b0 = s0 / 2, b1 = (s1 + 1) / 2;
+    uint32_t bits = U.bits;
+    uint64_t nExc = 0, excOff = 0;  // 2 bits: the N list, at byte excOff of the chunk's region
+    if (bits != 8) SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
+    uint8_t* out = c->ring + slot * Ctx::kRingSlot;
+    if (bits == 2) {
+        const uint64_t n = s1 - s0, pieces = (n + 4 * kPiece - 1) / (4 * kPiece);
+        if (c->excParts.size() < nt) c->excParts.resize(nt);
+        for (auto& v : c->excParts) v.clear();
+        P.run([&](unsigned t) {
+            for (uint64_t k = t; k < pieces; k += nt) {  // pieces of 4 MB of symbols (1 MB packed)
+                const uint64_t lo = k * 4 * kPiece, hi = std::min(n, lo + 4 * kPiece);
+                const uint8_t* in = U.src + s0 + lo;
+                const uint64_t acc = avx2 ? pack2Avx2(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[t])
+                                          : pack2Scalar(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[t]);
+                if (acc) bad.store(1, std::memory_order_relaxed);
+            }
+        });
+        for (auto& v : c->excParts) nExc += v.size();
+        excOff = ((b0 + (n + 3) / 4 + 3) & ~uint64_t(3)) - b0;  // 4-aligned on the device
+        if (excOff + 4 * nExc > b1 - b0) {
+            bits = 4;  // N-rich chunk: the list would not fit, go as nibbles
+        } else if (!bad.load()) {
+            uint8_t* e = out + excOff;
+            for (auto& v : c->excParts) {
+                if (!v.empty()) std::memcpy(e, v.data(), v.size() * 4);
+                e += v.size() * 4;
+            }
+            SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, excOff + 4 * nExc, hipMemcpyHostToDevice, c->stE));
+        }
+    }
+    if (bits == 4 && !bad.load()) {
         const uint64_t pieces = (b1 - b0 + kPiece - 1) / kPiece;
-        SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
-        uint8_t* out = c->ring + slot * Ctx::kRingSlot;
         P.run([&](unsigned t) {
             for (uint64_t k = t; k < pieces; k += nt) {
                 const uint64_t lo = b0 + k * kPiece, hi = std::min(b1, lo + kPiece);
@@ -577,7 +819,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
             }
         });
         if (!bad.load()) SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, b1 - b0, hipMemcpyHostToDevice, c->stE));
-    } else {  // one byte per symbol (SAHARA_NIBBLE_UPLOAD=0): check, then copy as given
+    } else if (bits == 8) {  // one byte per symbol (SAHARA_UPLOAD_BITS=8): check, then copy as given
         const uint64_t pieces = (s1 - s0 + kPiece - 1) / kPiece;
         P.run([&](unsigned t) {
             for (uint64_t k = t; k < pieces; k += nt) {
@@ -596,7 +838,12 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     }
     SH_HIP(hipEventRecord(c->ringEv[slot], c->stE));  // the chunk's DMA
     SH_HIP(hipStreamWaitEvent(kst, c->ringEv[slot], 0));
-    if (U.nibble) launchUnpackNibbles(c->nibPats.ptr + s0 / 2, raw + s0, s1 - s0, kst);
+    if (bits == 4) launchUnpackNibbles(c->nibPats.ptr + b0, raw + s0, s1 - s0, kst);
+    if (bits == 2) {
+        launchUnpack2(c->nibPats.ptr + b0, raw + s0, s1 - s0, sigma, kst);
+        if (nExc) launchPatchRank(reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff), nExc, raw + s0, 4, kst);
+    }
+    U.chunks[bits == 2 ? 0 : bits == 4 ? 1 : 2]++;
     const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
     if (U.rc) launchInterleaveRC(c->readRaw.ptr, r0, r1, m, sigma, c->npat, c->rawPats.ptr, kst);
     if (p1 > p0) {
@@ -605,6 +852,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
         launchPackPatterns3(c->rawPats.ptr + p0 * m, p1 - p0, m, c->patBlocks, c->pats3.ptr + p0 * c->patBlocks, kst);
     }
     U.done = r1;
+    c->mark("packed", r0 / U.chunk);
 }
 
 // Streamed upload: makes sure the patterns [0, patEnd) are enqueued, their
@@ -675,18 +923,26 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     U.src = src;
     U.rc = rc;
     U.rows = rows;
+    // symbols cross PCIe at 2 bits (DNA: A C G T codes, N positions listed),
+    // 4 bits (any alphabet) or 8 (as given): SAHARA_UPLOAD_BITS, or
+    // SAHARA_NIBBLE_UPLOAD=0 for 8
     if (const char* e = std::getenv("SAHARA_NIBBLE_UPLOAD")) c->nibbleUpload = std::atoi(e) != 0;
-    U.nibble = c->nibbleUpload;
-    // 1M patterns per chunk (SAHARA_UPLOAD_CHUNK), at most one ring slot of packed bytes
+    U.bits = !c->nibbleUpload ? 8u : (c->I.sigma == 5 || c->I.sigma == 6) ? 2u : 4u;
+    if (const char* e = std::getenv("SAHARA_UPLOAD_BITS")) {
+        const int b = std::atoi(e);
+        if (b == 2 || b == 4 || b == 8) U.bits = (uint32_t)b;
+    }
+    if (U.bits == 2 && c->I.sigma != 5 && c->I.sigma != 6) U.bits = 4;
+    // 1M patterns per chunk (SAHARA_UPLOAD_CHUNK), at most one ring slot of nibbles
     uint64_t chunkPats = 1u << 20;
     if (const char* e = std::getenv("SAHARA_UPLOAD_CHUNK")) chunkPats = std::max<uint64_t>(2, std::atoll(e));
     uint64_t chunk = rc ? chunkPats / 2 : chunkPats;
-    if (U.nibble) chunk = std::min<uint64_t>(chunk, Ctx::kRingSlot * 2 / m);
+    if (U.bits != 8) chunk = std::min<uint64_t>(chunk, Ctx::kRingSlot * 2 / m);
     U.chunk = std::max<uint64_t>(2, chunk & ~uint64_t(1));
     if (c->ringInit.joinable()) c->ringInit.join();
-    if (U.nibble && !c->ring) throw Error("could not pin the upload ring buffer");
+    if (U.bits != 8 && !c->ring) throw Error("could not pin the upload ring buffer");
     for (hipEvent_t e : c->ringEv) SH_HIP(hipEventSynchronize(e));  // the last call's DMAs
-    if (U.nibble) c->nibPats.reserve((rows * m + 1) / 2 + 8);
+    if (U.bits != 8) c->nibPats.reserve((rows * m + 1) / 2 + 8);
     SH_HIP(hipMemsetAsync(c->badFlag.ptr, 0, sizeof(uint32_t), c->stE));
     c->stageMs = 0;
     c->staged = c->streaming = true;
@@ -1077,15 +1333,18 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // sort, decode into the device-resident output, on stream sC. Needs the
     // batch's counts (host waits for its text phase). Returns false on
     // overflow; `finishCheck` then reads the locate flags and timings.
+    uint32_t seenTask = 0, seenHit = 0;  // pipelined overflow: the caps the re-run needs
     auto finish = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
+        c->mark("finish", b);
         // the batch's counters, copied on sC (a copy on sB would wait for CU
         // slots between two text phases)
         SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
         SH_HIP(hipMemcpyAsync(c->pinned + b * 8, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(c->ev[6], sC));
         SH_HIP(hipEventSynchronize(c->ev[6]));
+        c->mark("text done", b);
         const uint32_t* hs = c->pinned + b * 8;
         float ms = 0;
         SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
@@ -1097,8 +1356,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
         if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
         if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
-            if (hs[2] & 8u) growCap(c->taskCap, hs[4]);
-            if (hs[2] & 2u) growCap(c->hitCap, hs[1]);
+            // (pipelined: issueFM may be reading the caps on the other host
+            // thread; they grow after the pass, before the serial re-run)
+            if (hs[2] & 8u) growCap(serial ? c->taskCap : seenTask, hs[4]);
+            if (hs[2] & 2u) growCap(serial ? c->hitCap : seenHit, hs[1]);
             overflow = true;
             resetSlot(sl, sC);
             return false;
@@ -1117,6 +1378,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipMemcpyAsync(&rows, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipMemcpyAsync(&nbig, c->small.ptr + 4, 4, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipStreamSynchronize(sC));
+        c->mark("rows", b);
         if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
         c->k0.reserve(std::max<uint64_t>(rows, 1));
         if (nbig) c->k1.reserve(std::max<uint64_t>(rows, 1));
@@ -1155,12 +1417,34 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // sahara_gpu_search's host sink: the batch's hits go to host memory
         // on stF while later batches search (while they fit the sink)
         if (c->sinkOk && c->nout + rows <= c->sinkCap) {
-            if (rows) {
+            const bool compact = c->compactSink && rows * sizeof(uint64_t) <= Ctx::kDownSlot && nb < (1ull << 28);
+            if (rows && compact) {  // 8-B records, expanded on the host (Expander)
+                const uint64_t j = c->downJobs++;
+                const size_t slot = (size_t)(j % Ctx::kDownSlots);
+                if (j >= Ctx::kDownSlots) c->expander->waitFor(j + 1 - Ctx::kDownSlots);  // the slot is read
+                if (c->downEv.size() <= slot) {
+                    const size_t had = c->downEv.size();
+                    c->downEv.resize(Ctx::kDownSlots);
+                    for (size_t i = had; i < Ctx::kDownSlots; ++i)
+                        SH_HIP(hipEventCreateWithFlags(&c->downEv[i], hipEventDisableTiming));
+                }
+                uint64_t* stage = c->downRing + slot * (Ctx::kDownSlot / sizeof(uint64_t));
+                c->outC.reserve(Ctx::kDownSlots * (Ctx::kDownSlot / sizeof(uint64_t)));
+                uint64_t* dev = c->outC.ptr + slot * (Ctx::kDownSlot / sizeof(uint64_t));
+                launchCompactHits(c->out.ptr + c->nout, rows, q0, c->I.dRecStarts.ptr, dev, sC);
+                SH_HIP(hipEventRecord(c->ev[7], sC));
+                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[7], 0));
+                SH_HIP(hipMemcpyAsync(stage, dev, rows * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stF));
+                SH_HIP(hipEventRecord(c->downEv[slot], c->stF));
+                c->expander->submit({c->downEv[slot], stage, c->sink + c->nout, rows, q0});
+            } else if (rows && c->sinkPinned) {
                 SH_HIP(hipStreamWaitEvent(c->stF, c->ev[4], 0));
                 SH_HIP(hipMemcpyAsync(c->sink + c->nout, c->out.ptr + c->nout, rows * sizeof(sahara_hit),
                                       hipMemcpyDeviceToHost, c->stF));
+            } else if (rows) {  // neither fits: the rest goes after the pass
+                c->sinkOk = false;
             }
-            c->sinkDone = c->nout + rows;
+            if (c->sinkOk) c->sinkDone = c->nout + rows;
         } else {
             c->sinkOk = false;
         }
@@ -1181,24 +1465,81 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     };
 
     if (!serial) {
-        // FM(b) and text(b) are enqueued as soon as the slot of batch b-3 is
-        // released by its locate, so both streams always have work queued
-        // while the host waits for a text phase to finish.
-        bool pending = false;  // finishCheck owed for batch `owed`
-        uint64_t owed = 0;
-        auto drain = [&](uint64_t f) {
-            if (pending) finishCheck(owed);
-            pending = finish(f);
-            owed = f;
-        };
-        for (uint64_t b = 0; b < nbatch; ++b) {
-            if (b >= (uint64_t)Ctx::kSlots) drain(b - Ctx::kSlots);
-            issueFM(b);
-            issueText(b);
-            ++S.batches;
+        // Two host threads. This one packs the queries of a streamed upload
+        // and issues seeds, FM(b) and text(b) as soon as batch b's slot is
+        // free; a finisher thread waits for each batch's text phase and
+        // issues its locate, sort and hit download, so that batch b's hits
+        // leave while later batches are still being packed and searched.
+        // FM(b) reuses the slot that finish(b - kSlots) released.
+        std::mutex mu;
+        std::condition_variable cv;
+        uint64_t issued = 0, released = 0;  // batches issued; batches whose slot is released
+        bool stop = false;
+        std::exception_ptr finErr;
+        std::thread finisher([&] {
+            try {
+                SH_HIP(hipSetDevice(c->device));
+                bool pending = false;  // finishCheck owed for batch `owed`
+                uint64_t owed = 0;
+                for (uint64_t f = 0; f < nbatch; ++f) {
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return issued > f || stop; });
+                        if (issued <= f) break;
+                    }
+                    if (pending) finishCheck(owed);
+                    pending = finish(f);
+                    owed = f;
+                    {
+                        std::lock_guard<std::mutex> g(mu);
+                        released = f + 1;
+                        if (overflow) stop = true;  // the caller redoes the pass serially
+                    }
+                    cv.notify_all();
+                    if (overflow) break;
+                }
+                if (pending) finishCheck(owed);
+            } catch (...) {
+                finErr = std::current_exception();
+            }
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            cv.notify_all();
+        });
+        std::exception_ptr issueErr;
+        try {
+            for (uint64_t b = 0; b < nbatch; ++b) {
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return b < released + Ctx::kSlots || stop; });
+                    if (stop) break;
+                }
+                c->mark("issue", b);
+                issueFM(b);
+                issueText(b);
+                c->mark("issued", b);
+                ++S.batches;
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    issued = b + 1;
+                }
+                cv.notify_all();
+            }
+        } catch (...) {
+            issueErr = std::current_exception();
         }
-        for (uint64_t f = nbatch > (uint64_t)Ctx::kSlots ? nbatch - Ctx::kSlots : 0; f < nbatch; ++f) drain(f);
-        if (pending) finishCheck(owed);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (issueErr) stop = true;
+        }
+        cv.notify_all();
+        finisher.join();
+        if (issueErr) std::rethrow_exception(issueErr);
+        if (finErr) std::rethrow_exception(finErr);
+        if (overflow) {
+            c->taskCap = std::max(c->taskCap, seenTask);
+            c->hitCap = std::max(c->hitCap, seenHit);
+        }
         SH_HIP(hipStreamSynchronize(sA));
         SH_HIP(hipStreamSynchronize(sB));
         SH_HIP(hipStreamSynchronize(sC));
@@ -1548,21 +1889,41 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
                            uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits) {
     using clk = std::chrono::steady_clock;
     const auto tA = clk::now();
+    {
+        const char* te = std::getenv("SAHARA_TIMING");
+        c->traceOn = te && std::atoi(te) >= 2;
+        c->traceT0 = tA;
+        c->trace.clear();
+    }
     stageStreamed(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit);
     const auto tB = clk::now();
     c->sink = nullptr;
     c->sinkCap = 0;
+    c->compactSink = c->sinkPinned = false;
     if (!max_hits) {  // sized from the last call (the bench's steady state), else 2 hits per pattern
         // a first call takes a pooled buffer if there is one, but pins none:
         // pinning ~1 GB costs ~200 ms, ten times the pageable copy-out
         const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
         bool pinned = false;
         void* p = allocHits(est, &pinned, &c->sinkCap, c->lastHits != 0);
-        if (p && pinned) {
+        // hits go down as 8-B records and are expanded into the sink by host
+        // threads (any host memory), or whole into a pinned sink
+        const bool compact = c->downRing && c->maxErr < 16 && c->I.n < (1ull << 32) && !std::getenv("SAHARA_FULL_DOWNLOAD");
+        if (p && (pinned || compact)) {
             c->sink = static_cast<sahara_hit*>(p);
+            c->sinkPinned = pinned;
+            c->compactSink = compact;
         } else {
             freeHits(p);
             c->sinkCap = 0;
+        }
+        if (c->compactSink) {
+            if (!c->expander)
+                c->expander = std::make_unique<Expander>(c->device, std::max(1u, std::min(8u, std::thread::hardware_concurrency())) - 1);
+            c->expander->setStarts(&c->I.recStarts);
+            c->expander->mark = [c](const char* w, uint64_t i) { c->mark(w, i); };
+            c->expander->reset();
+            c->downJobs = 0;
         }
     }
     const auto tC = clk::now();
@@ -1573,13 +1934,30 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         if (bad) throw Error("pattern rank out of range for this index");
     } catch (...) {
         drainAll(c);
+        if (c->compactSink) {
+            try {
+                c->expander->drain();  // nothing may write into the sink once it is freed
+            } catch (...) {
+            }
+        }
         freeHits(c->sink);
         c->sink = nullptr;
         c->staged = c->streaming = false;
         throw;
     }
+    if (c->compactSink) {
+        try {
+            c->expander->drain();
+        } catch (...) {
+            freeHits(c->sink);
+            c->sink = nullptr;
+            throw;
+        }
+    }
+    c->mark("run end", 0);
     c->streaming = false;  // every chunk is up: sahara_gpu_run may re-run the staged patterns
     c->stats.stage_ms = c->up.hostMs;
+    for (int b = 0; b < 3; ++b) c->stats.upload_chunks[b] = c->up.chunks[b];
     const auto t0 = std::chrono::steady_clock::now();
     sahara_hit* buf = c->sink;
     c->sink = nullptr;
@@ -1595,7 +1973,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
                 buf = nullptr;
                 c->sinkDone = 0;
             }
-            bool pinned = buf != nullptr;
+            bool pinned = buf != nullptr && c->sinkPinned;
             if (!buf) {
                 c->sinkDone = 0;
                 buf = static_cast<sahara_hit*>(allocHits(c->nout, &pinned, nullptr, c->lastHits != 0));
@@ -1626,6 +2004,9 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::fprintf(stderr, "[sahara] stage %.1f ms, sink %.1f ms, pass %.1f ms (host packing %.1f ms), output %.1f ms\n",
                      ms(tA, tB), ms(tB, tC), ms(tC, t0), c->up.hostMs, c->stats.output_ms);
+        std::sort(c->trace.begin(), c->trace.end());
+        for (auto& m : c->trace) std::fprintf(stderr, "[sahara]   %8.2f %s\n", m.first, m.second.c_str());
+        c->traceOn = false;
     }
 }
 
@@ -1746,6 +2127,22 @@ int sahara_synth_reads_typed(const uint8_t* ranks, const uint64_t* rec_lens, uin
         synthReads(ranks, rec_lens, n_records, sigma, n_reads, len, substitutions, insertions, deletions, errors, seed,
                    out, origin);
     });
+}
+
+int sahara_pack_2bit(const uint8_t* ranks, uint64_t n, uint32_t sigma, int scalar, uint8_t* out, uint32_t* n_pos,
+                     uint64_t pos_cap, uint64_t* n_count) {
+    int bad = 0;
+    const int rc = guarded([&] {
+        if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 or 6");
+        if (n >= (1ull << 32)) throw Error("at most 2^32 - 1 symbols per chunk");
+        std::vector<uint32_t> pos;
+        const uint64_t acc = (!scalar && hostHasAvx2()) ? pack2Avx2(ranks, out, n, sigma, 0, pos)
+                                                        : pack2Scalar(ranks, out, n, sigma, 0, pos);
+        bad = acc ? 1 : 0;
+        *n_count = pos.size();
+        if (n_pos && !pos.empty()) std::memcpy(n_pos, pos.data(), std::min<uint64_t>(pos.size(), pos_cap) * 4);
+    });
+    return rc ? rc : bad;
 }
 
 int sahara_interleave_rc(const uint8_t* reads, uint64_t n_reads, uint32_t len, uint32_t sigma, uint8_t* out) {

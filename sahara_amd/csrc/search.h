@@ -127,6 +127,10 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
                         uint32_t* dst, uint32_t* bad, hipStream_t st);
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst
 void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream_t st);
+void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
+                       hipStream_t st);
+void launchUnpack2(const uint8_t* packed, uint8_t* dst, uint64_t n, uint32_t sigma, hipStream_t st);
+void launchPatchRank(const uint32_t* pos, uint64_t n, uint8_t* dst, uint32_t rank, hipStream_t st);
 // reads [r0, r1) (m bytes each) -> patterns [2 r0, min(2 r1, pEnd)): read, reverse complement, ...
 void launchInterleaveRC(const uint8_t* reads, uint64_t r0, uint64_t r1, uint32_t m, uint32_t sigma, uint64_t pEnd,
                         uint8_t* pats, hipStream_t st);

@@ -1528,6 +1528,67 @@ void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream
     SH_HIP(hipGetLastError());
 }
 
+// sahara_gpu_search's download form of a batch's hits, 8 B instead of 24:
+// (qid - qidBase) << 36 | text position << 4 | e (batches < 2^28 queries,
+// texts < 2^32, e < 16), expanded back on the host (capi.cpp expandHits).
+__global__ void kCompactHits(const sahara_hit* __restrict__ h, uint64_t n, uint64_t qidBase,
+                             const uint64_t* __restrict__ starts, uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sahara_hit x = h[i];
+        out[i] = ((x.qid - qidBase) << 36) | ((starts[x.seq_id] + x.pos) << 4) | x.err;
+    }
+}
+
+void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
+                       hipStream_t st) {
+    if (n == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(kCompactHits, dim3((unsigned)blocks), dim3(256), 0, st, h, n, qidBase, starts, out);
+    SH_HIP(hipGetLastError());
+}
+
+// Streamed queries sent two bits per symbol (capi.cpp pack2Avx2: symbol i at
+// bits 2 (i % 4) of byte i / 4) -> one rank per byte through a 4-entry table:
+// A C G T = 1 2 3 4 (dna4) or 1 2 3 5 (dna5, whose N positions kPatchRank
+// writes afterwards). 16 symbols per thread: one 4-B load, one 16-B store.
+__global__ void kUnpack2(const uint8_t* __restrict__ packed, uint8_t* __restrict__ dst, uint64_t n, uint32_t lut) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w * 16 < n; w += stride) {
+        if (w * 16 + 16 <= n) {
+            const uint32_t x = *reinterpret_cast<const uint32_t*>(packed + w * 4);
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t b = x >> (8 * q);  // four symbols
+                o[q] = ((lut >> (8 * (b & 3u))) & 0xFFu) | ((lut >> (8 * ((b >> 2) & 3u))) & 0xFFu) << 8 |
+                       ((lut >> (8 * ((b >> 4) & 3u))) & 0xFFu) << 16 | ((lut >> (8 * ((b >> 6) & 3u))) & 0xFFu) << 24;
+            }
+            *reinterpret_cast<uint4*>(dst + w * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (uint64_t i = w * 16; i < n; ++i) dst[i] = (lut >> (8 * ((packed[i >> 2] >> ((i & 3) * 2)) & 3u))) & 0xFFu;
+        }
+    }
+}
+
+void launchUnpack2(const uint8_t* packed, uint8_t* dst, uint64_t n, uint32_t sigma, hipStream_t st) {
+    const uint32_t lut = sigma == 6 ? 0x05030201u : 0x04030201u;
+    const uint64_t blocks = std::min<uint64_t>((n / 16 + 256) / 256, 65536);
+    hipLaunchKernelGGL(kUnpack2, dim3((unsigned)blocks), dim3(256), 0, st, packed, dst, n, lut);
+    SH_HIP(hipGetLastError());
+}
+
+// dst[pos[i]] = rank for the listed positions (the N symbols of a 2-bit chunk)
+__global__ void kPatchRank(const uint32_t* __restrict__ pos, uint64_t n, uint8_t* __restrict__ dst, uint32_t rank) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[pos[i]] = (uint8_t)rank;
+}
+
+void launchPatchRank(const uint32_t* pos, uint64_t n, uint8_t* dst, uint32_t rank, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(kPatchRank, dim3((unsigned)blocks), dim3(256), 0, st, pos, n, dst, rank);
+    SH_HIP(hipGetLastError());
+}
+
 // Query ingest's reverse-complement interleave (search.cpp:121-127) on the
 // device: pattern 2r = read r, 2r + 1 = its reverse complement (A<->T, C<->G,
 // N->N; ivs::reverse_complement_rank), for the patterns [2 * r0, pEnd) of the
