@@ -782,14 +782,15 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     uint8_t* out = c->ring + slot * Ctx::kRingSlot;
     if (bits == 2) {
         const uint64_t n = s1 - s0, pieces = (n + 4 * kPiece - 1) / (4 * kPiece);
-        if (c->excParts.size() < nt) c->excParts.resize(nt);
+        // one N list per piece: concatenated in piece order they are sorted
+        if (c->excParts.size() < pieces) c->excParts.resize(pieces);
         for (auto& v : c->excParts) v.clear();
         P.run([&](unsigned t) {
             for (uint64_t k = t; k < pieces; k += nt) {  // pieces of 4 MB of symbols (1 MB packed)
                 const uint64_t lo = k * 4 * kPiece, hi = std::min(n, lo + 4 * kPiece);
                 const uint8_t* in = U.src + s0 + lo;
-                const uint64_t acc = avx2 ? pack2Avx2(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[t])
-                                          : pack2Scalar(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[t]);
+                const uint64_t acc = avx2 ? pack2Avx2(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k])
+                                          : pack2Scalar(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k]);
                 if (acc) bad.store(1, std::memory_order_relaxed);
             }
         });
@@ -839,12 +840,20 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     SH_HIP(hipEventRecord(c->ringEv[slot], c->stE));  // the chunk's DMA
     SH_HIP(hipStreamWaitEvent(kst, c->ringEv[slot], 0));
     if (bits == 4) launchUnpackNibbles(c->nibPats.ptr + b0, raw + s0, s1 - s0, kst);
-    if (bits == 2) {
+    U.chunks[bits == 2 ? 0 : bits == 4 ? 1 : 2]++;
+    const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
+    if (bits == 2) {  // straight into both pattern forms (no byte pass); SAHARA_UPLOAD_BYTES=1: via bytes
+        if (!std::getenv("SAHARA_UPLOAD_BYTES")) {
+            launchPackFrom2(c->nibPats.ptr + b0, reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff),
+                            (uint32_t)nExc, r0, p0, p1, m, U.rc, sigma, c->patWords, c->patBlocks,
+                            c->pats.ptr + 0, c->pats3.ptr + 0, kst);
+            U.done = r1;
+            c->mark("packed", r0 / U.chunk);
+            return;
+        }
         launchUnpack2(c->nibPats.ptr + b0, raw + s0, s1 - s0, sigma, kst);
         if (nExc) launchPatchRank(reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff), nExc, raw + s0, 4, kst);
     }
-    U.chunks[bits == 2 ? 0 : bits == 4 ? 1 : 2]++;
-    const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
     if (U.rc) launchInterleaveRC(c->readRaw.ptr, r0, r1, m, sigma, c->npat, c->rawPats.ptr, kst);
     if (p1 > p0) {
         launchPackPatterns(c->rawPats.ptr + p0 * m, p1 - p0, m, c->patWords, sigma, c->pats.ptr + p0 * c->patWords,
@@ -942,7 +951,7 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     if (c->ringInit.joinable()) c->ringInit.join();
     if (U.bits != 8 && !c->ring) throw Error("could not pin the upload ring buffer");
     for (hipEvent_t e : c->ringEv) SH_HIP(hipEventSynchronize(e));  // the last call's DMAs
-    if (U.bits != 8) c->nibPats.reserve((rows * m + 1) / 2 + 8);
+    if (U.bits != 8) c->nibPats.reserve((rows * m + 1) / 2 + 16);  // + the 12 B the 2-bit packer's last loads may touch
     SH_HIP(hipMemsetAsync(c->badFlag.ptr, 0, sizeof(uint32_t), c->stE));
     c->stageMs = 0;
     c->staged = c->streaming = true;
@@ -1906,9 +1915,16 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
         bool pinned = false;
         void* p = allocHits(est, &pinned, &c->sinkCap, c->lastHits != 0);
-        // hits go down as 8-B records and are expanded into the sink by host
-        // threads (any host memory), or whole into a pinned sink
-        const bool compact = c->downRing && c->maxErr < 16 && c->I.n < (1ull << 32) && !std::getenv("SAHARA_FULL_DOWNLOAD");
+        // hits go whole into a pinned sink (DMA; no host CPU or memory traffic
+        // beyond the write), or, into pageable memory, as 8-B records that
+        // host threads expand (Expander): a third of the PCIe bytes, but the
+        // expansion reads and writes host memory the packing also needs
+        // (at C3 it took ~4 ms per batch beside the packing, 300M against
+        // 330M reads/s). SAHARA_COMPACT_DOWNLOAD=1 / SAHARA_FULL_DOWNLOAD=1 force one.
+        const bool compactOk = c->downRing && c->maxErr < 16 && c->I.n < (1ull << 32);
+        const char* fe = std::getenv("SAHARA_FULL_DOWNLOAD");
+        const char* ce = std::getenv("SAHARA_COMPACT_DOWNLOAD");
+        const bool compact = compactOk && !(fe && std::atoi(fe)) && (!pinned || (ce && std::atoi(ce)));
         if (p && (pinned || compact)) {
             c->sink = static_cast<sahara_hit*>(p);
             c->sinkPinned = pinned;

@@ -129,6 +129,9 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
 void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream_t st);
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
                        hipStream_t st);
+void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,
+                     uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks, uint32_t* pats,
+                     uint4* pats3, hipStream_t st);
 void launchUnpack2(const uint8_t* packed, uint8_t* dst, uint64_t n, uint32_t sigma, hipStream_t st);
 void launchPatchRank(const uint32_t* pos, uint64_t n, uint8_t* dst, uint32_t rank, hipStream_t st);
 // reads [r0, r1) (m bytes each) -> patterns [2 r0, min(2 r1, pEnd)): read, reverse complement, ...

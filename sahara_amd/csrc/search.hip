@@ -1577,6 +1577,87 @@ void launchUnpack2(const uint8_t* packed, uint8_t* dst, uint64_t n, uint32_t sig
     SH_HIP(hipGetLastError());
 }
 
+// A streamed 2-bit chunk straight into the search's two pattern forms, with
+// no byte pass: 4-bit words (FM phase) and 3-bit-plane blocks (text phase)
+// of the patterns [p0, p1). Pattern p is row p, or (rc) read p / 2 and, for
+// odd p, its reverse complement (search.cpp:121-123: reversed, codes
+// complemented as c ^ 3); read r starts at chunk-local symbol (r - r0) * m.
+// `exc` lists the chunk's N positions in ascending order (rank 4). One thread
+// per (pattern, 32-symbol block): 64 bits of codes from three word loads,
+// even / odd bits gathered into the code planes c0 / c1, then
+//   rank bit 0 = ~c0 | c1 (dna5: T = 5) or ~c0 (dna4), bit 1 = c0 ^ c1,
+//   bit 2 = c0 & c1, and N = 100.
+__device__ __forceinline__ uint32_t evenBits(uint64_t x) {
+    x &= 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    return (uint32_t)(x | (x >> 16));
+}
+__device__ __forceinline__ uint32_t spreadNibbles(uint32_t x) {  // bit j of 8 -> bit 4j
+    x &= 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    return (x | (x << 3)) & 0x11111111u;
+}
+__global__ void kPackFrom2(const uint8_t* __restrict__ src, const uint32_t* __restrict__ exc, uint32_t nExc,
+                           uint64_t r0, uint64_t p0, uint64_t p1, uint32_t m, uint32_t rc, uint32_t dna5,
+                           uint32_t patWords, uint32_t patBlocks, uint32_t* __restrict__ pats,
+                           uint4* __restrict__ pats3) {
+    const uint64_t total = (p1 - p0) * patBlocks;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = p0 + i / patBlocks;
+        const uint32_t b = (uint32_t)(i % patBlocks);
+        const uint64_t r = rc ? p >> 1 : p;
+        const bool rev = rc && (p & 1u);
+        const uint32_t nsym = min(32u, m - 32u * b);
+        const uint64_t start = (r - r0) * m + (rev ? m - 32u * b - nsym : 32u * b);  // source symbols [start, start + nsym)
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(src + (start >> 4) * 4);
+        const uint32_t sh = (uint32_t)(start & 15u) * 2u;
+        uint64_t v = ((uint64_t)w[1] << 32) | w[0];
+        if (sh) v = (v >> sh) | ((uint64_t)w[2] << (64u - sh));
+        uint32_t c0 = evenBits(v), c1 = evenBits(v >> 1);
+        const uint32_t valid = nsym >= 32u ? 0xFFFFFFFFu : (1u << nsym) - 1u;
+        uint32_t nm = 0;
+        if (nExc) {
+            uint32_t lo = 0, hi = nExc;  // first listed N at or after start
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (exc[mid] < start) lo = mid + 1; else hi = mid;
+            }
+            for (; lo < nExc && exc[lo] < start + nsym; ++lo) nm |= 1u << (uint32_t)(exc[lo] - start);
+        }
+        if (rev) {  // symbol q = complement of source symbol nsym - 1 - q
+            c0 = ~__builtin_bitreverse32(c0) >> (32u - nsym);
+            c1 = ~__builtin_bitreverse32(c1) >> (32u - nsym);
+            nm = __builtin_bitreverse32(nm) >> (32u - nsym);
+        }
+        const uint32_t P0 = ((dna5 ? (~c0 | c1) : ~c0) & ~nm) & valid;
+        const uint32_t P1 = ((c0 ^ c1) & ~nm) & valid;
+        const uint32_t P2 = ((c0 & c1) | nm) & valid;
+        pats3[p * patBlocks + b] = make_uint4(P0, P1, P2, 0u);
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t wi = 4u * b + t;
+            if (wi < patWords)
+                pats[p * patWords + wi] = spreadNibbles(P0 >> (8 * t)) | (spreadNibbles(P1 >> (8 * t)) << 1) |
+                                          (spreadNibbles(P2 >> (8 * t)) << 2);
+        }
+    }
+}
+
+void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,
+                     uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks, uint32_t* pats,
+                     uint4* pats3, hipStream_t st) {
+    const uint64_t total = (p1 - p0) * patBlocks;
+    if (total == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(kPackFrom2, dim3((unsigned)blocks), dim3(256), 0, st, src, exc, nExc, r0, p0, p1, m,
+                       rc ? 1u : 0u, sigma == 6 ? 1u : 0u, patWords, patBlocks, pats, pats3);
+    SH_HIP(hipGetLastError());
+}
+
 // dst[pos[i]] = rank for the listed positions (the N symbols of a 2-bit chunk)
 __global__ void kPatchRank(const uint32_t* __restrict__ pos, uint64_t n, uint8_t* __restrict__ dst, uint32_t rank) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)

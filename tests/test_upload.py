@@ -71,9 +71,14 @@ def _inputs(with_n, m=60, n_reads=2000):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bits", ["2", "4", "8"])
+@pytest.mark.parametrize("bits", ["2", "2b", "4", "8"])
 @pytest.mark.parametrize("with_n", [False, True])
 def test_streamed_upload_encodings(gpu_device, monkeypatch, bits, with_n):
+    """2 bits: straight into the pattern forms (kPackFrom2), or through bytes
+    (2b: SAHARA_UPLOAD_BYTES=1, kUnpack2 + kPatchRank); 4: nibbles; 8: bytes."""
+    if bits == "2b":
+        monkeypatch.setenv("SAHARA_UPLOAD_BYTES", "1")
+        bits = "2"
     monkeypatch.setenv("SAHARA_UPLOAD_BITS", bits)
     monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "64")
     monkeypatch.setenv("SAHARA_BATCH", "997")
@@ -111,13 +116,14 @@ def test_2bit_upload_refuses_bad_rank(gpu_device, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"SAHARA_FULL_DOWNLOAD": "1"}, {"SAHARA_HITCAP": "300", "SAHARA_TASKCAP": "200"},
-                                 {"SAHARA_PIN_MIN": "0"}])
+                                 {"SAHARA_PIN_MIN": "0"}, {"SAHARA_PIN_MIN": "0", "SAHARA_COMPACT_DOWNLOAD": "1"}])
 def test_hit_download_forms(gpu_device, monkeypatch, env):
-    """Hits leave the device as 8-B records per batch and are expanded into
-    the caller's buffer by host threads (capi.cpp Expander; more batches than
-    staging slots), or whole into a pinned sink (SAHARA_FULL_DOWNLOAD=1);
-    also through an overflow re-run and with every sink pinned. Same hits,
-    first call (pageable sink) and steady state (pooled sink) alike."""
+    """Hits leave the device whole into a pinned sink, or as 8-B records per
+    batch that host threads expand into a pageable one (capi.cpp Expander;
+    more batches than staging slots); also through an overflow re-run, with
+    every sink pinned (SAHARA_PIN_MIN=0), compact into a pinned sink, and with
+    no sink at all (SAHARA_FULL_DOWNLOAD=1 with pageable buffers: copied
+    after the pass). Same hits, first call and steady state alike."""
     monkeypatch.setenv("SAHARA_BATCH", "211")
     monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "100")
     for k, v in env.items():
@@ -128,3 +134,25 @@ def test_hit_download_forms(gpu_device, monkeypatch, env):
     for _ in range(3):
         assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
     assert np.array_equal(hits_as_rows(sa.search(gpu, pats[:777], sch)), want[want[:, 0] < 777])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [17, 32, 33, 250])
+def test_2bit_pattern_forms_any_length(gpu_device, monkeypatch, m):
+    """kPackFrom2 at lengths with one partial block, exactly one block, one
+    symbol more, and C5's 250 (8 blocks): same hits as the byte upload, N
+    included, reads and reverse complements alike."""
+    monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "50")
+    flat, lens = sa.synth_reference([200_000, 100_000], sigma=6, seed=31)
+    reads = sa.synth_reads(flat, lens, 600, m, 2, sigma=6, seed=37)
+    reads[np.random.default_rng(m).random(reads.shape) < 0.02] = 4
+    sch = sa.search_scheme("h2-k2", 0, 2, m)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    monkeypatch.setenv("SAHARA_UPLOAD_BITS", "8")
+    want = hits_as_rows(sa.search_reads(gpu, reads, sch))
+    monkeypatch.setenv("SAHARA_UPLOAD_BITS", "2")
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+    assert gpu.stats()["upload_chunks"][0] > 0
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
+    assert np.array_equal(want, hits_as_rows(ref.search(sa.interleave_rc(reads, 6), sch, nthreads=8)[0]))
