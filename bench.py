@@ -43,6 +43,9 @@ CONFIGS = {
     "c2": (100_000_000, 1, 1_000_000, 100, 1, False, "h2-k2"),
     "c3": (3_000_000_000, 24, 10_000_000, 100, 2, True, "h2-k2"),
     "c5": (3_000_000_000, 24, 1_000_000, 250, 3, True, "h2-k2"),
+    # beyond BASELINE: a 6 Gbp text (two GRCh38-shaped haplotypes) exceeds
+    # 32-bit rows and is indexed in two parts
+    "c6": (6_000_000_000, 48, 10_000_000, 100, 2, True, "h2-k2"),
 }
 
 METRIC = "reads/s at k=2 edit, 10M×100bp vs 3Gbp index; achieved HBM GB/s"
@@ -59,7 +62,7 @@ def log(*a):
 def record_lengths(total, n):
     if n == 1:
         return np.array([total], np.uint64)
-    w = np.array(GRCH38[:n], np.float64)
+    w = np.resize(np.array(GRCH38, np.float64), n)
     lens = np.floor(w / w.sum() * total).astype(np.uint64)
     lens[0] += np.uint64(total - int(lens.sum()))
     return lens
@@ -437,6 +440,33 @@ def origin_recall(h, origin, k):
 
 
 def verify_index(idx, flat, lens, torch, dev, W=21):
+    """verify_index_part for every part of the index (one part unless the
+    text exceeds 32-bit rows), each against its own records' text."""
+    nparts = idx.info()["n_parts"]
+    out, r0, off = None, 0, 0
+    lens = np.asarray(lens, np.uint64)
+    for p in range(nparts):
+        idx.select_part(p)
+        nr = idx.part_info(p)["n_records"]
+        plen = lens[r0:r0 + nr]
+        span = int(plen.sum())
+        res = verify_index_part(idx, flat[off:off + span], plen, torch, dev, W)
+        if out is None:
+            out = res
+        else:
+            out["sa_probe_ok"] = out["sa_probe_ok"] and res["sa_probe_ok"]
+            out["index_checks"] = {k: out["index_checks"][k] and v for k, v in res["index_checks"].items()}
+            out["index_check_rows"] += res["index_check_rows"]
+            out["index_check_s"] = round(out["index_check_s"] + res["index_check_s"], 1)
+            out["index_check_max_lcp_blocks"] = max(out["index_check_max_lcp_blocks"], res["index_check_max_lcp_blocks"])
+        r0 += nr
+        off += span
+    idx.select_part(0)
+    out["index_parts"] = nparts
+    return out
+
+
+def verify_index_part(idx, flat, lens, torch, dev, W=21):
     """Checks the GPU-built forward index of the bench text row by row,
     independently of the code that built it (torch ops on the device):
 
@@ -452,7 +482,7 @@ def verify_index(idx, flat, lens, torch, dev, W=21):
       round trip of LocateLinear;
     - C[] and the symbol counts of the reverse BWT match the text's."""
     t0 = time.time()
-    inf = idx.info()
+    inf = idx.part_info()
     n, rate = int(inf["n"]), int(inf["sampling_rate"])
     ex = idx.export()
     sa_h = idx.export_sa()
@@ -635,35 +665,53 @@ def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):
     import oracle as O
 
     t = time.time()
-    ex = idx.export()
-    ref = O.Index.from_parts(ex["sigma"], ex["n"], ex["rec_lens"], ex["rate"], ex["bwt_f"], ex["bwt_r"],
-                             ex["sampled"], ex["samples"])
-    del ex
-    log(f"cpu baseline: oracle index loaded ({time.time()-t:.1f}s)")
+    # one oracle index per part of the GPU index (a multi-part index: the
+    # sample is searched in every part, seq_ids offset by the part's first
+    # record, as capi.cpp run merges them)
+    refs, rec0 = [], 0
+    for p in range(idx.info()["n_parts"]):
+        idx.select_part(p)
+        ex = idx.export()
+        refs.append((O.Index.from_parts(ex["sigma"], ex["n"], ex["rec_lens"], ex["rate"], ex["bwt_f"], ex["bwt_r"],
+                                        ex["sampled"], ex["samples"]), rec0))
+        rec0 += len(ex["rec_lens"])
+        del ex
+    idx.select_part(0)
+    log(f"cpu baseline: oracle index loaded, {len(refs)} part(s) ({time.time()-t:.1f}s)")
     threads = host_threads()
+
+    def cpu_search(q, nthreads):
+        out = []
+        for ref, r0 in refs:
+            h, _ = ref.search(q, scheme, edit=edit, nthreads=nthreads)
+            h = np.asarray(h, np.uint64).reshape(-1, 4)
+            h[:, 1] += np.uint64(r0)
+            out.append(h)
+        return np.concatenate(out)
+
     # calibrate: grow the sample until it runs >= 1 s, then scale to ~target_s
     n = min(1000, nreads)
     while True:
         t = time.perf_counter()
-        ref.search(pats[: 2 * n], scheme, edit=edit, nthreads=threads)
+        cpu_search(pats[: 2 * n], threads)
         dt = time.perf_counter() - t
         if dt >= 1.0 or n >= nreads:
             break
         n = min(nreads, n * 4)
     n2 = int(min(nreads, max(n, n * target_s / max(dt, 1e-3))))
     t = time.perf_counter()
-    hits, _ = ref.search(pats[: 2 * n2], scheme, edit=edit, nthreads=threads)
+    hits = cpu_search(pats[: 2 * n2], threads)
     dt = time.perf_counter() - t
     rate = n2 / dt
     # single-thread figure (the reference's execution model, search.cpp:221-241)
     n1 = max(20, min(n2, int(n2 / threads / 4)))
     t = time.perf_counter()
-    ref.search(pats[: 2 * n1], scheme, edit=edit, nthreads=1)
+    cpu_search(pats[: 2 * n1], 1)
     rate1 = n1 / (time.perf_counter() - t)
     # parity on the sample
     gpu_hits = sa.search(idx, pats[: 2 * n2], scheme, edit=edit)
     from_gpu = np.stack([gpu_hits["qid"], gpu_hits["seq_id"], gpu_hits["pos"], gpu_hits["err"]], 1).astype(np.uint64)
-    h = np.asarray(hits, np.uint64)
+    h = hits
     order = np.lexsort((h[:, 3], h[:, 2], h[:, 1], h[:, 0]))
     parity = bool(len(h) == len(from_gpu) and np.array_equal(h[order], from_gpu))
     log(f"cpu baseline: {n2} reads in {dt:.1f}s on {threads} threads = {rate:.0f} reads/s "
@@ -671,7 +719,7 @@ def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):
     return {"value": round(rate, 1), "unit": "reads/s", "cores": threads, "kind": "port",
             "sample": f"first {n2} reads (+RC) of the same workload, {dt:.1f}s; "
                       f"1-thread rate {rate1:.1f} reads/s on {n1} reads; host CPU: {cpu_model()}",
-            "single_thread_value": round(rate1, 1), "parity_on_sample": parity}
+            "single_thread_value": round(rate1, 1), "parity_on_sample": parity, "index_parts": len(refs)}
 
 
 if __name__ == "__main__":

@@ -54,6 +54,8 @@ typedef struct sahara_index_info {
     uint64_t n_records;
     uint64_t n_samples;
     uint64_t device_bytes;   /* HBM held by the resident index */
+    uint32_t n_parts;        /* 1, or the parts of a text of >= 2^32 - 2 symbols (split at record boundaries) */
+    uint32_t kmer_depth;     /* k-mer table depth (0: none) */
 } sahara_index_info;
 
 /* Per-run statistics of the last sahara_gpu_search / sahara_gpu_run call. */
@@ -117,6 +119,11 @@ int  sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* samp
  * device: built with the index or densified from the .idx samples (test hooks). */
 int  sahara_gpu_export_sa(void* ctx, uint32_t* sa);
 int  sahara_gpu_export_text(void* ctx, uint8_t* text);
+/* Multi-part index (n_parts > 1): the part the export hooks above read
+ * (default 0). Its records are the part's own, numbered from 0. */
+int  sahara_gpu_select_part(void* ctx, uint32_t part);
+/* sahara_gpu_index_info of one part (sahara_gpu_index_info: totals). */
+int  sahara_gpu_part_info(void* ctx, uint32_t part, sahara_index_info* info);
 /* Execution mode of the search (default verify = 1, locate_sa = 1):
  *   verify    1: once a DFS node's interval is a single row (SAHARA_SPLIT rows),
  *             resolve its text position through the resident SA and continue

@@ -45,7 +45,8 @@ class SaharaError(RuntimeError):
 
 class IndexInfo(C.Structure):
     _fields_ = [("sigma", C.c_uint32), ("sampling_rate", C.c_uint32), ("n", C.c_uint64),
-                ("n_records", C.c_uint64), ("n_samples", C.c_uint64), ("device_bytes", C.c_uint64)]
+                ("n_records", C.c_uint64), ("n_samples", C.c_uint64), ("device_bytes", C.c_uint64),
+                ("n_parts", C.c_uint32), ("kmer_depth", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -82,6 +83,8 @@ EXPORTED = {
     "sahara_gpu_export_sa": (C.c_int, [C.c_void_p, u32p]),
     "sahara_gpu_export_text": (C.c_int, [C.c_void_p, u8p]),
     "sahara_gpu_set_mode": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "sahara_gpu_select_part": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sahara_gpu_part_info": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "sahara_gpu_search": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                     C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
                                     C.POINTER(C.c_uint64)]),
@@ -214,7 +217,7 @@ class BiFMIndex:
         return self.info()["sigma"]
 
     def export(self):
-        inf = self.info()
+        inf = self.part_info()
         n = inf["n"]
         bf = np.zeros(n, np.uint8)
         br = np.zeros(n, np.uint8)
@@ -229,16 +232,26 @@ class BiFMIndex:
                     sigma=inf["sigma"], rate=inf["sampling_rate"])
 
     def export_sa(self):
-        n = self.info()["n"]
+        n = self.part_info()["n"]
         sa = np.zeros(n, np.uint32)
         _check(lib().sahara_gpu_export_sa(self._h, _p(sa, u32p)))
         return sa
 
     def export_text(self):
-        n = self.info()["n"]
+        n = self.part_info()["n"]
         t = np.zeros(n, np.uint8)
         _check(lib().sahara_gpu_export_text(self._h, _p(t, u8p)))
         return t
+
+    def select_part(self, part):
+        """Multi-part index: which part export() / export_sa() / export_text() read."""
+        _check(lib().sahara_gpu_select_part(self._h, part))
+        self._part = part
+
+    def part_info(self, part=None):
+        i = IndexInfo()
+        _check(lib().sahara_gpu_part_info(self._h, getattr(self, "_part", 0) if part is None else part, C.byref(i)))
+        return {n: getattr(i, n) for n, _ in i._fields_}
 
     def set_mode(self, verify=True, locate_sa=True):
         """verify: continue singleton intervals against the resident text;

@@ -218,6 +218,15 @@ struct Ctx {
     hipStream_t st = nullptr;
     int numCU = 0;
     DeviceIndex I;
+    // A text of 2^32 - 2 symbols or more is indexed in parts (splitRecords):
+    // part 0 is I, parts 1.. are `more`; a search runs over each part in turn
+    // (swapped into I) and merges the hits (run). partRec0[p] = the global id
+    // of part p's first record. exportPart selects the part the export test
+    // hooks read (sahara_gpu_select_part).
+    std::vector<DeviceIndex> more;
+    std::vector<uint64_t> partRec0{0};
+    uint32_t exportPart = 0;
+    DevBuf<sahara_hit> outAll;            // multi-part: hits of the parts so far
 
     // staged inputs
     DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern (FM phase)
@@ -1030,7 +1039,85 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
 // stream with grown buffers (`serial`), re-running a batch until it fits.
 void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
 
+void runOne(Ctx* c, bool count);
+
+DeviceIndex& partOf(Ctx* c, uint32_t p) { return p == 0 ? c->I : c->more.at(p - 1); }
+
+// Search over a multi-part index: the pass runs over every part in turn (the
+// staged patterns and scheme are shared; every part has the same k-mer
+// depth), its hits get the part's record offset, and one stable sort by qid
+// restores the canonical (qid, seq_id, pos, err) order, since part p's
+// records all follow part p - 1's. Exact under P-strict: a DFS node exists in
+// the whole index iff its interval is non-empty in some part, and its rows
+// are the union of its rows over the parts. Hits reach the
+// host after the last part (no per-batch sink).
 void run(Ctx* c, bool count) {
+    if (c->more.empty()) return runOne(c, count);
+    sahara_hit* sink = c->sink;
+    c->sink = nullptr;
+    sahara_stats T{};
+    uint64_t total = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        for (uint32_t p = 0; p <= c->more.size(); ++p) {
+            if (p) std::swap(c->I, c->more[p - 1]);
+            try {
+                runOne(c, count);
+            } catch (...) {
+                if (p) std::swap(c->I, c->more[p - 1]);
+                throw;
+            }
+            if (p) std::swap(c->I, c->more[p - 1]);
+            if (c->outAll.cap < total + c->nout) {  // grow, keeping the parts so far
+                DevBuf<sahara_hit> grown;
+                grown.reserve(std::max<uint64_t>((total + c->nout) + (total + c->nout) / 4, 1024));
+                if (total)
+                    SH_HIP(hipMemcpyAsync(grown.ptr, c->outAll.ptr, total * sizeof(sahara_hit), hipMemcpyDeviceToDevice,
+                                          c->st));
+                SH_HIP(hipStreamSynchronize(c->st));
+                c->outAll = std::move(grown);
+            }
+            launchOffsetSeq(c->out.ptr, c->nout, c->partRec0[p], c->outAll.ptr + total, c->st);
+            total += c->nout;
+            const sahara_stats& S = c->stats;  // the parts' work adds up
+            T.patterns = S.patterns;
+            T.search_grid = S.search_grid;
+            T.text_grid = S.text_grid;
+            T.pipelined = S.pipelined;
+            for (uint64_t sahara_stats::*f :
+                 {&sahara_stats::batches, &sahara_stats::cursors, &sahara_stats::nodes, &sahara_stats::rank_nodes,
+                  &sahara_stats::ext_lines, &sahara_stats::lf_steps, &sahara_stats::text_nodes,
+                  &sahara_stats::conversions, &sahara_stats::fm_iterations, &sahara_stats::text_iterations,
+                  &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
+                  &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
+                  &sahara_stats::text_steps, &sahara_stats::text_launches})
+                T.*f += S.*f;
+            for (double sahara_stats::*f : {&sahara_stats::search_ms, &sahara_stats::locate_ms, &sahara_stats::sort_ms,
+                                            &sahara_stats::text_ms, &sahara_stats::seed_ms})
+                T.*f += S.*f;
+            T.search_launches += S.search_launches;
+        }
+        if (c->out.cap < total) {
+            c->out.release();
+            c->out.reserve(std::max<uint64_t>(total, 1024));
+        }
+        sortHitsByQid(c->outAll.ptr, total, c->out.ptr, c->tmp, c->st);
+        SH_HIP(hipStreamSynchronize(c->st));
+    } catch (...) {
+        c->sink = sink;
+        throw;
+    }
+    c->sink = sink;
+    c->sinkDone = 0;
+    c->nout = total;
+    T.hits = total;
+    T.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    T.stage_ms = c->stageMs;
+    for (int b = 0; b < 3; ++b) T.upload_chunks[b] = c->stats.upload_chunks[b];
+    c->stats = T;
+}
+
+void runOne(Ctx* c, bool count) {
     if (!c->staged) throw Error("sahara_gpu_run: nothing staged");
     auto t0 = std::chrono::steady_clock::now();
     if (const char* e = std::getenv("SAHARA_PIPELINE")) c->pipeline = std::atol(e) != 0;
@@ -1609,29 +1696,59 @@ int sahara_gpu_build(int device, const uint8_t* ranks, const uint64_t* rec_lens,
                      uint32_t sampling_rate, void** ctx) {
     return guarded([&] {
         std::unique_ptr<Ctx> c(newCtx(device));
-        buildFromText(c->I, ranks, rec_lens, n_records, sigma, sampling_rate, c->st);
+        const std::vector<uint64_t> first = splitRecords(rec_lens, n_records);
+        if (first.size() == 2) {
+            buildFromText(c->I, ranks, rec_lens, n_records, sigma, sampling_rate, c->st);
+        } else {  // parts at record boundaries, then their k-mer tables at one common depth
+            uint64_t off = 0, nmax = 0;
+            for (size_t p = 0; p + 1 < first.size(); ++p) {
+                uint64_t syms = 0, n = 0;
+                for (uint64_t r = first[p]; r < first[p + 1]; ++r) syms += rec_lens[r];
+                n = syms + (first[p + 1] - first[p]);
+                nmax = std::max(nmax, n);
+                if (p) c->more.emplace_back();
+                buildFromText(partOf(c.get(), (uint32_t)p), ranks + off, rec_lens + first[p], first[p + 1] - first[p],
+                              sigma, sampling_rate, c->st, false);
+                off += syms;
+            }
+            c->partRec0.assign(first.begin(), first.end() - 1);
+            const uint32_t K = kmerDepth(nmax, (uint32_t)first.size() - 1);
+            for (uint32_t p = 0; p + 1 < first.size(); ++p) buildKmerTable(partOf(c.get(), p), K, c->st);
+        }
         *ctx = c.release();
     });
 }
 
+// an .idx image (one part or several) -> a context holding every part
+Ctx* openImage(int device, const uint8_t* buf, size_t bytes) {
+    const std::vector<IdxParts> parts = parseIdxAll(buf, bytes);
+    std::unique_ptr<Ctx> c(newCtx(device));
+    uint64_t rec0 = 0, nmax = 0;
+    c->partRec0.clear();
+    for (size_t p = 0; p < parts.size(); ++p) {
+        const IdxParts& P = parts[p];
+        if (p) c->more.emplace_back();
+        buildFromParts(partOf(c.get(), (uint32_t)p), P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF,
+                       P.bwtR, P.sampled, P.samples, P.nsamples, c->st, parts.size() == 1);
+        c->partRec0.push_back(rec0);
+        rec0 += P.recLens.size();
+        nmax = std::max(nmax, P.n);
+    }
+    if (parts.size() > 1) {
+        const uint32_t K = kmerDepth(nmax, (uint32_t)parts.size());
+        for (uint32_t p = 0; p < parts.size(); ++p) buildKmerTable(partOf(c.get(), p), K, c->st);
+    }
+    return c.release();
+}
+
 int sahara_gpu_open(int device, const void* idx_image, size_t idx_bytes, void** ctx) {
-    return guarded([&] {
-        IdxParts P = parseIdx(static_cast<const uint8_t*>(idx_image), idx_bytes);
-        std::unique_ptr<Ctx> c(newCtx(device));
-        buildFromParts(c->I, P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF, P.bwtR, P.sampled,
-                       P.samples, P.nsamples, c->st);
-        *ctx = c.release();
-    });
+    return guarded([&] { *ctx = openImage(device, static_cast<const uint8_t*>(idx_image), idx_bytes); });
 }
 
 int sahara_gpu_open_file(int device, const char* path, void** ctx) {
     return guarded([&] {
         std::vector<uint8_t> buf = readFile(path);
-        IdxParts P = parseIdx(buf.data(), buf.size());
-        std::unique_ptr<Ctx> c(newCtx(device));
-        buildFromParts(c->I, P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF, P.bwtR, P.sampled,
-                       P.samples, P.nsamples, c->st);
-        *ctx = c.release();
+        *ctx = openImage(device, buf.data(), buf.size());
     });
 }
 
@@ -1640,10 +1757,16 @@ int sahara_gpu_index_info(void* ctx, sahara_index_info* info) {
         Ctx* c = ctxOf(ctx);
         info->sigma = c->I.sigma;
         info->sampling_rate = c->I.rate;
-        info->n = c->I.n;
-        info->n_records = c->I.recLens.size();
-        info->n_samples = c->I.nsamples;
-        info->device_bytes = c->I.deviceBytes();
+        info->n = info->n_records = info->n_samples = info->device_bytes = 0;
+        for (uint32_t p = 0; p <= c->more.size(); ++p) {  // totals over the parts
+            const DeviceIndex& D = partOf(c, p);
+            info->n += D.n;
+            info->n_records += D.recLens.size();
+            info->n_samples += D.nsamples;
+            info->device_bytes += D.deviceBytes();
+        }
+        info->n_parts = (uint32_t)c->more.size() + 1;
+        info->kmer_depth = c->I.kmerK;
     });
 }
 
@@ -1651,29 +1774,54 @@ int sahara_gpu_export(void* ctx, uint8_t* bwt_f, uint8_t* bwt_r, uint64_t* sampl
                       uint64_t* C, uint64_t* rec_lens) {
     return guarded([&] {
         Ctx* c = ctxOf(ctx);
-        exportParts(c->I, bwt_f, bwt_r, sampled_bits, samples, c->st);
-        if (C) std::memcpy(C, c->I.C, (c->I.sigma + 1) * 8);
-        if (rec_lens) std::memcpy(rec_lens, c->I.recLens.data(), c->I.recLens.size() * 8);
+        DeviceIndex& D = partOf(c, c->exportPart);
+        exportParts(D, bwt_f, bwt_r, sampled_bits, samples, c->st);
+        if (C) std::memcpy(C, D.C, (D.sigma + 1) * 8);
+        if (rec_lens) std::memcpy(rec_lens, D.recLens.data(), D.recLens.size() * 8);
     });
 }
 
 int sahara_gpu_export_sa(void* ctx, uint32_t* sa) {
     return guarded([&] {
-        Ctx* c = ctxOf(ctx);
-        SH_HIP(hipMemcpy(sa, c->I.saFull.ptr, c->I.n * 4, hipMemcpyDeviceToHost));
+        const DeviceIndex& D = partOf(ctxOf(ctx), ctxOf(ctx)->exportPart);
+        SH_HIP(hipMemcpy(sa, D.saFull.ptr, D.n * 4, hipMemcpyDeviceToHost));
     });
 }
 
 int sahara_gpu_export_text(void* ctx, uint8_t* text) {
     return guarded([&] {
-        Ctx* c = ctxOf(ctx);
-        std::vector<uint32_t> t3(((c->I.n + 31) / 32) * 4);
-        SH_HIP(hipMemcpy(t3.data(), c->I.text3.ptr, t3.size() * 4, hipMemcpyDeviceToHost));
-        for (uint64_t i = 0; i < c->I.n; ++i) {
+        const DeviceIndex& D = partOf(ctxOf(ctx), ctxOf(ctx)->exportPart);
+        std::vector<uint32_t> t3(((D.n + 31) / 32) * 4);
+        SH_HIP(hipMemcpy(t3.data(), D.text3.ptr, t3.size() * 4, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < D.n; ++i) {
             const uint32_t* b = &t3[(i / 32) * 4];
             const uint32_t j = (uint32_t)(i & 31);
             text[i] = (uint8_t)(((b[0] >> j) & 1u) | (((b[1] >> j) & 1u) << 1) | (((b[2] >> j) & 1u) << 2));
         }
+    });
+}
+
+int sahara_gpu_part_info(void* ctx, uint32_t part, sahara_index_info* info) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (part > c->more.size()) throw Error("no index part " + std::to_string(part));
+        const DeviceIndex& D = partOf(c, part);
+        info->sigma = D.sigma;
+        info->sampling_rate = D.rate;
+        info->n = D.n;
+        info->n_records = D.recLens.size();
+        info->n_samples = D.nsamples;
+        info->device_bytes = D.deviceBytes();
+        info->n_parts = (uint32_t)c->more.size() + 1;
+        info->kmer_depth = D.kmerK;
+    });
+}
+
+int sahara_gpu_select_part(void* ctx, uint32_t part) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (part > c->more.size()) throw Error("no index part " + std::to_string(part));
+        c->exportPart = part;
     });
 }
 
@@ -1688,23 +1836,32 @@ int sahara_gpu_set_mode(void* ctx, int verify, int locate_sa) {
 int sahara_gpu_save(void* ctx, const char* path) {
     return guarded([&] {
         Ctx* c = ctxOf(ctx);
-        const uint64_t n = c->I.n;
-        std::vector<uint8_t> bf(n), br(n);
-        std::vector<uint64_t> sb(n / 64 + 1);
-        std::vector<uint32_t> smp(c->I.nsamples);
-        exportParts(c->I, bf.data(), br.data(), sb.data(), smp.data(), c->st);
-        IdxParts P;
-        P.sigma = c->I.sigma;
-        P.n = n;
-        P.rate = c->I.rate;
-        std::copy(c->I.C, c->I.C + 8, P.C);
-        P.recLens = c->I.recLens;
-        P.bwtF = bf.data();
-        P.bwtR = br.data();
-        P.sampled = sb.data();
-        P.samples = smp.data();
-        P.nsamples = smp.size();
-        writeIdx(path, P);
+        const size_t np = c->more.size() + 1;
+        std::vector<std::vector<uint8_t>> bf(np), br(np);
+        std::vector<std::vector<uint64_t>> sb(np);
+        std::vector<std::vector<uint32_t>> smp(np);
+        std::vector<IdxParts> parts(np);
+        for (uint32_t p = 0; p < np; ++p) {
+            const DeviceIndex& D = partOf(c, p);
+            const uint64_t n = D.n;
+            bf[p].resize(n);
+            br[p].resize(n);
+            sb[p].resize(n / 64 + 1);
+            smp[p].resize(D.nsamples);
+            exportParts(D, bf[p].data(), br[p].data(), sb[p].data(), smp[p].data(), c->st);
+            IdxParts& P = parts[p];
+            P.sigma = D.sigma;
+            P.n = n;
+            P.rate = D.rate;
+            std::copy(D.C, D.C + 8, P.C);
+            P.recLens = D.recLens;
+            P.bwtF = bf[p].data();
+            P.bwtR = br[p].data();
+            P.sampled = sb[p].data();
+            P.samples = smp[p].data();
+            P.nsamples = smp[p].size();
+        }
+        writeIdxAll(path, parts);
     });
 }
 

@@ -42,6 +42,17 @@ struct DevBuf {  // minimal owning device buffer that only ever grows
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), cap(o.cap) { o.ptr = nullptr; o.cap = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            ptr = o.ptr;
+            cap = o.cap;
+            o.ptr = nullptr;
+            o.cap = 0;
+        }
+        return *this;
+    }
 };
 
 // Text (and patterns) for the text phase as 3-bit-plane blocks: block i holds
@@ -79,16 +90,24 @@ struct DeviceIndex {
 };
 
 // index_build.hip
+// withKmer = false leaves the k-mer table out (a multi-part index builds the
+// tables of all its parts at one depth afterwards)
 void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec,
-                   uint32_t sigma, uint32_t rate, hipStream_t st);
+                   uint32_t sigma, uint32_t rate, hipStream_t st, bool withKmer = true);
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec,
                     uint32_t rate, const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits,
-                    const uint32_t* samples, uint64_t nsamples, hipStream_t st);
+                    const uint32_t* samples, uint64_t nsamples, hipStream_t st, bool withKmer = true);
 // depth of the k-mer table for a text of n symbols: floor(log4 n) + 1, at
 // most 16 (a 68.7 GB table at 3 Gbp, where the mean 16-mer occurs 0.7 times:
 // most exact first parts of a search then start as a text task), and at most
-// what fits in half of the free HBM; SAHARA_KMER overrides (0 = no table)
-uint32_t kmerDepth(uint64_t n);
+// what fits in half of the free HBM (`tables` tables of that depth: the parts
+// of a multi-part index); SAHARA_KMER overrides (0 = no table)
+uint32_t kmerDepth(uint64_t n, uint32_t tables = 1);
+// Texts of 2^32 - 2 symbols or more are split into parts at record
+// boundaries (rows, SA entries and cursors are 32-bit): first record of each
+// part, then nrec. At most SAHARA_PART_SYMBOLS symbols (with delimiters) per
+// part when set (tests). A record that alone needs 2^32 - 2 rows is refused.
+std::vector<uint64_t> splitRecords(const uint64_t* recLens, uint64_t nrec);
 void buildKmerTable(DeviceIndex& I, uint32_t K, hipStream_t st);
 void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits,
                  uint32_t* samples, hipStream_t st);

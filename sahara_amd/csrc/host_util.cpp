@@ -66,9 +66,60 @@ IdxParts parseIdx(const uint8_t* buf, size_t bytes) {
     return P;
 }
 
+std::vector<IdxParts> parseIdxAll(const uint8_t* buf, size_t bytes) {
+    Reader r{buf, buf + bytes};
+    const uint64_t sigma = r.get<uint64_t>();
+    if (sigma != 5 && sigma != 6) throw Error("unknown index with " + std::to_string(sigma) + " letters");
+    const uint64_t magic = r.get<uint64_t>();
+    if (magic == kIdxMagic) return {parseIdx(buf, bytes)};
+    if (magic != kIdxPartsMagic) throw Error("not a sahara-amd .idx file (payload magic mismatch)");
+    const uint64_t np = r.get<uint64_t>();
+    if (np == 0 || np > 4096) throw Error("implausible number of index parts: " + std::to_string(np));
+    std::vector<IdxParts> out;
+    for (uint64_t i = 0; i < np; ++i) {
+        const uint64_t len = r.get<uint64_t>();
+        if (len > (uint64_t)(r.end - r.p)) throw Error("truncated .idx file");
+        out.push_back(parseIdx(r.p, len));
+        if (out.back().sigma != sigma) throw Error("index parts disagree on sigma");
+        r.p += len;
+    }
+    if (r.p != r.end) throw Error("trailing bytes after the index parts");
+    return out;
+}
+
+namespace {
+uint64_t idxBytes(const IdxParts& P) {
+    // sigma, magic, n, C[], recLens (count + entries), rate; both BWTs, sampled bits, samples (count + data)
+    return 8 * (3 + (P.sigma + 1) + 1 + P.recLens.size() + 1) + 2 * (8 + P.n) + 8 + 8 * (P.n / 64 + 1) + 8 +
+           4 * P.nsamples;
+}
+void writeIdxTo(std::ostream& o, const IdxParts& P);
+}  // namespace
+
+void writeIdxAll(const std::string& path, const std::vector<IdxParts>& parts) {
+    if (parts.size() == 1) return writeIdx(path, parts[0]);
+    std::ofstream o(path, std::ios::binary);
+    if (!o) throw Error("cannot write " + path);
+    auto put = [&](uint64_t v) { o.write(reinterpret_cast<const char*>(&v), 8); };
+    put(parts.at(0).sigma);
+    put(kIdxPartsMagic);
+    put(parts.size());
+    for (const IdxParts& P : parts) {
+        put(idxBytes(P));
+        writeIdxTo(o, P);
+    }
+    if (!o) throw Error("write failed: " + path);
+}
+
 void writeIdx(const std::string& path, const IdxParts& P) {
     std::ofstream o(path, std::ios::binary);
     if (!o) throw Error("cannot write " + path);
+    writeIdxTo(o, P);
+    if (!o) throw Error("write failed: " + path);
+}
+
+namespace {
+void writeIdxTo(std::ostream& o, const IdxParts& P) {
     auto put = [&](uint64_t v) { o.write(reinterpret_cast<const char*>(&v), 8); };
     put(P.sigma);
     put(kIdxMagic);
@@ -85,8 +136,8 @@ void writeIdx(const std::string& path, const IdxParts& P) {
     o.write(reinterpret_cast<const char*>(P.sampled), (std::streamsize)((P.n / 64 + 1) * 8));
     put(P.nsamples);
     o.write(reinterpret_cast<const char*>(P.samples), (std::streamsize)(P.nsamples * 4));
-    if (!o) throw Error("write failed: " + path);
 }
+}  // namespace
 
 uint64_t readIdxSigma(const std::string& path) {
     std::ifstream f(path, std::ios::binary);

@@ -22,6 +22,14 @@
 namespace sahara {
 
 constexpr uint64_t kIdxMagic = 0x3178646961726173ull;
+// A text of 2^32 - 2 symbols or more is indexed in parts (records split at
+// record boundaries, device_index.h splitRecords), each a complete index:
+//
+//   u64 sigma | u64 partsMagic | u64 nparts | nparts x (u64 bytes | the part
+//   as a single-part image above, its own leading sigma included)
+//
+// A text that fits one part keeps the single-part layout byte for byte.
+constexpr uint64_t kIdxPartsMagic = 0x7374726170616873ull;
 
 struct IdxParts {
     uint32_t sigma = 0;
@@ -38,7 +46,10 @@ struct IdxParts {
 
 std::vector<uint8_t> readFile(const std::string& path);
 IdxParts parseIdx(const uint8_t* buf, size_t bytes);   // pointers alias buf
+// single- or multi-part image -> its parts in record order (pointers alias buf)
+std::vector<IdxParts> parseIdxAll(const uint8_t* buf, size_t bytes);
 void writeIdx(const std::string& path, const IdxParts& p);
+void writeIdxAll(const std::string& path, const std::vector<IdxParts>& parts);  // one part: writeIdx
 uint64_t readIdxSigma(const std::string& path);         // search.cpp:278-283
 
 void synthReads(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma, uint64_t nreads,

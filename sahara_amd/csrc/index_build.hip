@@ -427,8 +427,26 @@ __global__ void kKmerLevel(const OccLine* __restrict__ occR, Cvec C, uint32_t si
     }
 }
 
+std::vector<uint64_t> splitRecords(const uint64_t* recLens, uint64_t nrec) {
+    uint64_t limit = 0xFFFFFFFDull;  // n < 2^32 - 2 symbols per part, delimiters included
+    if (const char* e = std::getenv("SAHARA_PART_SYMBOLS")) limit = std::max<uint64_t>(2, std::min<uint64_t>(limit, std::atoll(e)));
+    std::vector<uint64_t> first{0};
+    uint64_t n = 0;
+    for (uint64_t r = 0; r < nrec; ++r) {
+        if (recLens[r] + 1 > 0xFFFFFFFDull)
+            throw Error("record " + std::to_string(r) + " alone exceeds 2^32 - 2 symbols (32-bit rows per part)");
+        if (n && n + recLens[r] + 1 > limit) {
+            first.push_back(r);
+            n = 0;
+        }
+        n += recLens[r] + 1;
+    }
+    first.push_back(nrec);
+    return first;
+}
+
 void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* recLens, uint64_t nrec, uint32_t sigma,
-                   uint32_t rate, hipStream_t st) {
+                   uint32_t rate, hipStream_t st, bool withKmer) {
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
     if (nrec == 0) throw Error("reference is empty");
     if (rate == 0) throw Error("sampling rate must be > 0");
@@ -493,12 +511,12 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
     for (int c = 0; c < 5; ++c)
         if (totalsR[c] != totals[c]) throw Error("forward/reverse symbol counts differ");
     SH_HIP(hipStreamSynchronize(st));
-    buildKmerTable(I, kmerDepth(N), st);
+    if (withKmer) buildKmerTable(I, kmerDepth(N), st);
 }
 
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec, uint32_t rate,
                     const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits, const uint32_t* samples,
-                    uint64_t nsamples, hipStream_t st) {
+                    uint64_t nsamples, hipStream_t st, bool withKmer) {
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
     if (n >= 0xFFFFFFFEull) throw Error("text too long for 32-bit rows");
     setCommon(I, sigma, n, recLens, nrec, rate, st);
@@ -540,20 +558,27 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     SH_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, st));
     SH_HIP(hipStreamSynchronize(st));
     if (herr) throw Error("SA densification walk exceeded its bound (inconsistent .idx samples)");
-    buildKmerTable(I, kmerDepth(n), st);
+    if (withKmer) buildKmerTable(I, kmerDepth(n), st);
 }
 
-uint32_t kmerDepth(uint64_t n) {
+uint32_t kmerDepth(uint64_t n, uint32_t tables) {
     uint32_t lg = 0;
     while (lg < 31 && (1ull << (2 * (lg + 1))) <= n) ++lg;  // floor(log4 n)
     int k = (int)lg + 1;
     if (const char* e = std::getenv("SAHARA_KMER")) k = std::atoi(e);
     k = std::max(0, std::min(k, 16));
-    // the table (16 B x 4^K) and its build levels (2 x 16 B x 4^(K-1)) take at
-    // most half of the free HBM
+    // the tables (16 B x 4^K each) and the build levels of one (2 x 16 B x
+    // 4^(K-1)) take at most half of the free HBM, or, for the parts of a
+    // multi-part index (built after all parts), three quarters of it less 16 GB
+    // for the search's buffers (6 Gbp in two parts: two depth-16 tables, 137 GB)
     size_t freeB = 0, totalB = 0;
-    if (hipMemGetInfo(&freeB, &totalB) == hipSuccess)
-        while (k > 0 && (16ull << (2 * k)) + (32ull << (2 * (k - 1))) > freeB / 2) --k;
+    const uint64_t budget = [&]() -> uint64_t {
+        if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) return UINT64_MAX;
+        if (tables <= 1) return freeB / 2;
+        const uint64_t q = (uint64_t)freeB / 4 * 3;
+        return q > (16ull << 30) ? q - (16ull << 30) : 0;
+    }();
+    while (k > 0 && tables * (16ull << (2 * k)) + (32ull << (2 * (k - 1))) > budget) --k;
     return (uint32_t)k;
 }
 

@@ -1528,6 +1528,61 @@ void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream
     SH_HIP(hipGetLastError());
 }
 
+// Multi-part index (capi.cpp run): a part's hits with its first global
+// record id added to seq_id, appended to the hits of the parts before it.
+__global__ void kOffsetSeq(const sahara_hit* __restrict__ in, uint64_t n, uint32_t rec0, sahara_hit* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        sahara_hit h = in[i];
+        h.seq_id += rec0;
+        out[i] = h;
+    }
+}
+
+void launchOffsetSeq(const sahara_hit* in, uint64_t n, uint64_t rec0, sahara_hit* out, hipStream_t st) {
+    if (n == 0) return;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(kOffsetSeq, dim3((unsigned)blocks), dim3(256), 0, st, in, n, (uint32_t)rec0, out);
+    SH_HIP(hipGetLastError());
+}
+
+__global__ void kQidKeys(const sahara_hit* __restrict__ h, uint64_t n, uint64_t* __restrict__ key,
+                         uint32_t* __restrict__ idx) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        key[i] = h[i].qid;
+        idx[i] = (uint32_t)i;
+    }
+}
+
+__global__ void kGatherHits(const sahara_hit* __restrict__ in, const uint32_t* __restrict__ idx, uint64_t n,
+                            sahara_hit* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = in[idx[i]];
+}
+
+// Stable sort of hit records by qid (rocPRIM's LSD radix sort is stable):
+// the parts' hits, each part in canonical order and every part's records
+// after the previous part's, come out in canonical (qid, seq_id, pos, err) order.
+void sortHitsByQid(const sahara_hit* in, uint64_t n, sahara_hit* out, DevBuf<char>& tmp, hipStream_t st) {
+    if (n == 0) return;
+    if (n >= (1ull << 32)) throw Error("more than 2^32 hits to merge across index parts");
+    DevBuf<uint64_t> k0, k1;
+    DevBuf<uint32_t> v0, v1;
+    k0.reserve(n);
+    k1.reserve(n);
+    v0.reserve(n);
+    v1.reserve(n);
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(kQidKeys, dim3((unsigned)blocks), dim3(256), 0, st, in, n, k0.ptr, v0.ptr);
+    SH_HIP(hipGetLastError());
+    size_t bytes = 0;
+    SH_HIP(rocprim::radix_sort_pairs(nullptr, bytes, k0.ptr, k1.ptr, v0.ptr, v1.ptr, (size_t)n, 0, 64, st));
+    tmp.reserve(bytes + 256);
+    SH_HIP(rocprim::radix_sort_pairs(tmp.ptr, bytes, k0.ptr, k1.ptr, v0.ptr, v1.ptr, (size_t)n, 0, 64, st));
+    hipLaunchKernelGGL(kGatherHits, dim3((unsigned)blocks), dim3(256), 0, st, in, v1.ptr, n, out);
+    SH_HIP(hipGetLastError());
+    SH_HIP(hipStreamSynchronize(st));
+}
+
 // sahara_gpu_search's download form of a batch's hits, 8 B instead of 24:
 // (qid - qidBase) << 36 | text position << 4 | e (batches < 2^28 queries,
 // texts < 2^32, e < 16), expanded back on the host (capi.cpp expandHits).

@@ -22,24 +22,36 @@ import bench  # noqa: E402
 
 
 class _OracleIdx:
-    """The three BiFMIndex calls verify_index makes, served from the oracle."""
+    """The BiFMIndex calls verify_index makes, served from the oracle: one
+    index, or (refs a list) the parts of a multi-part index, each over its
+    own records; corrupt(ex) plants an error in part `bad_part`."""
 
-    def __init__(self, ref, lens, sigma=6, rate=16, corrupt=None):
-        self.ex = ref.export()
-        self.lens, self.sigma, self.rate = lens, sigma, rate
+    def __init__(self, ref, lens, sigma=6, rate=16, corrupt=None, bad_part=0):
+        refs = ref if isinstance(ref, list) else [ref]
+        self.exs = [r.export() for r in refs]
+        self.lens, self.sigma, self.rate, self.part = lens, sigma, rate, 0
         if corrupt:
-            corrupt(self.ex)
+            corrupt(self.exs[bad_part])
 
     def info(self):
-        return {"n": len(self.ex["bwt_f"]), "sampling_rate": self.rate, "sigma": self.sigma}
+        return {"n": sum(len(e["bwt_f"]) for e in self.exs), "sampling_rate": self.rate, "sigma": self.sigma,
+                "n_parts": len(self.exs)}
+
+    def select_part(self, p):
+        self.part = p
+
+    def part_info(self, p=None):
+        e = self.exs[self.part if p is None else p]
+        return {"n": len(e["bwt_f"]), "sampling_rate": self.rate, "sigma": self.sigma, "n_parts": len(self.exs),
+                "n_records": len(e["rec_lens"]) if "rec_lens" in e else int((e["bwt_f"] == 0).sum())}
 
     def export(self):
-        e = dict(self.ex)
+        e = dict(self.exs[self.part])
         e["C"] = e["C"][: self.sigma + 1]
         return e
 
     def export_sa(self):
-        return self.ex["sa"].copy()
+        return self.exs[self.part]["sa"].copy()
 
 
 def _text(seed=3, lengths=(3000, 17, 900, 2500)):
@@ -92,6 +104,20 @@ def test_verify_index_catches_corruption(corrupt, key):
     ref = O.Index.build(recs, 6, 16)
     out = bench.verify_index(_OracleIdx(ref, lens, corrupt=corrupt), flat, lens, torch, "cpu", W=5)
     assert not out["sa_probe_ok"] and not out["index_checks"][key], out
+
+
+@pytest.mark.parametrize("corrupt,key", [(None, None), (_swap_sa, "sa_sorted"), (_sample, "samples")])
+def test_verify_index_over_parts(corrupt, key):
+    """A multi-part index (texts beyond 32-bit rows): every part is checked
+    against its own records' text; an error in the second part is caught."""
+    flat, lens, recs = _text(lengths=(3000, 17, 900, 2500, 1200))
+    refs = [O.Index.build(recs[:2], 6, 16), O.Index.build(recs[2:], 6, 16)]
+    out = bench.verify_index(_OracleIdx(refs, lens, corrupt=corrupt, bad_part=1), flat, lens, torch, "cpu", W=5)
+    assert out["index_parts"] == 2 and out["index_check_rows"] == len(flat) + len(lens)
+    if corrupt is None:
+        assert out["sa_probe_ok"], out
+    else:
+        assert not out["sa_probe_ok"] and not out["index_checks"][key], out
 
 
 def test_origin_recall():
