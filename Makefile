@@ -11,7 +11,8 @@ LIB      := $(LIBDIR)/libsahara_hip.so
 CLI      := bin/sahara
 HDRS     := $(wildcard $(CSRC)/*.h) include/sahara_hip.h
 
-OBJS := $(OBJDIR)/index_build.o $(OBJDIR)/search.o $(OBJDIR)/capi.o $(OBJDIR)/host_util.o $(OBJDIR)/scheme.o
+OBJS := $(OBJDIR)/index_build.o $(OBJDIR)/search.o $(OBJDIR)/capi.o $(OBJDIR)/staging.o $(OBJDIR)/pass.o \
+        $(OBJDIR)/host_util.o $(OBJDIR)/scheme.o
 
 all: $(LIB) oracle $(if $(wildcard sahara_amd/cli/*.cpp),$(CLI),) tools/gather_bench
 
@@ -19,15 +20,7 @@ $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/capi.o: $(CSRC)/capi.cpp $(HDRS)
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-
-$(OBJDIR)/scheme.o: $(CSRC)/scheme.cpp $(HDRS)
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-
-$(OBJDIR)/host_util.o: $(CSRC)/host_util.cpp $(HDRS)
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -51,7 +44,8 @@ oracle:
 # test suite against them.
 ASAN_HOST := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
 ASANDIR   := build/asan
-ASAN_OBJS := $(ASANDIR)/index_build.o $(ASANDIR)/search.o $(ASANDIR)/capi.o $(ASANDIR)/host_util.o $(ASANDIR)/scheme.o
+ASAN_OBJS := $(ASANDIR)/index_build.o $(ASANDIR)/search.o $(ASANDIR)/capi.o $(ASANDIR)/staging.o $(ASANDIR)/pass.o \
+             $(ASANDIR)/host_util.o $(ASANDIR)/scheme.o
 
 $(ASANDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(ASANDIR)

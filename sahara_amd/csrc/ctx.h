@@ -1,0 +1,404 @@
+// ctx.h — the per-device context of libsahara_hip.so and what the C ABI
+// (capi.cpp), the query staging (staging.cpp) and the batch pipeline
+// (pass.cpp) share.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sahara_hip.h"
+#include "device_index.h"
+#include "search.h"
+
+namespace sahara {
+
+extern thread_local std::string g_err;  // sahara_gpu_last_error
+
+// Host worker threads of a context (pattern packing for the upload), started
+// once: a streamed upload packs several chunks per call, and fresh threads per
+// chunk measured slower than the link.
+class HostPool {
+public:
+    explicit HostPool(unsigned workers) {
+        for (unsigned i = 1; i <= workers; ++i) ts_.emplace_back([this, i] { loop(i); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : ts_) t.join();
+    }
+    unsigned size() const { return (unsigned)ts_.size() + 1; }
+    // f(t) for every t in [0, size()), t = 0 on the calling thread; f must not throw
+    void run(const std::function<void(unsigned)>& f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &f;
+            pending_ = (unsigned)ts_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(id);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> ts_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    unsigned pending_ = 0;
+    bool stop_ = false;
+};
+
+// Host side of sahara_gpu_search's compact hit download: batch by batch, the
+// 8-B records (search.hip kCompactHits) land in pinned staging memory on
+// stream stF, and this thread expands them into the caller's sahara_hit
+// buffer (record id by binary search over the record starts) on a few worker
+// threads while later batches still search. Cuts the PCIe download to a third
+// (8 of 24 B per hit).
+class Expander {
+public:
+    struct Job {
+        hipEvent_t ev;           // the batch's download is done
+        const uint64_t* src;     // compact records (pinned staging)
+        sahara_hit* dst;
+        uint64_t n, q0;          // records; the batch's first qid
+    };
+    Expander(int device, unsigned workers) : device_(device), pool_(workers) {
+        th_ = std::thread([this] { loop(); });
+    }
+    ~Expander() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void setStarts(const std::vector<uint64_t>* starts) { starts_ = starts; }
+    std::function<void(const char*, uint64_t)> mark;  // SAHARA_TIMING=2 trace
+    void submit(const Job& j) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(j);
+            ++submitted_;
+        }
+        cv_.notify_all();
+    }
+    // waits until the first n jobs submitted since reset() are expanded
+    void waitFor(uint64_t n) {
+        std::unique_lock<std::mutex> lk(mu_);
+        idle_.wait(lk, [&] { return done_ >= n || err_; });
+    }
+    void reset() {
+        drain();
+        std::lock_guard<std::mutex> g(mu_);
+        submitted_ = done_ = 0;
+    }
+    // waits until every submitted batch is expanded; rethrows the first failure
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu_);
+        idle_.wait(lk, [&] { return q_.empty() && !busy_; });
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            std::rethrow_exception(e);
+        }
+    }
+
+private:
+    void loop() {
+        (void)hipSetDevice(device_);
+        for (;;) {
+            Job j{};
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                j = q_.front();
+                q_.erase(q_.begin());
+                busy_ = true;
+            }
+            try {
+                SH_HIP(hipEventSynchronize(j.ev));
+                if (mark) mark("expand", done_);
+                expand(j);
+                if (mark) mark("expanded", done_);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!err_) err_ = std::current_exception();
+            }
+            std::lock_guard<std::mutex> g(mu_);
+            busy_ = false;
+            ++done_;
+            idle_.notify_all();
+        }
+    }
+    void expand(const Job& j) {
+        const std::vector<uint64_t>& S = *starts_;
+        const unsigned nt = pool_.size();
+        const uint64_t per = (j.n + nt - 1) / nt;
+        pool_.run([&](unsigned t) {
+            const uint64_t b = std::min(j.n, (uint64_t)t * per), e = std::min(j.n, b + per);
+            uint32_t seq = 0;
+            uint64_t lo = 1, hi = 0;  // the current record's [start, next start): empty
+            for (uint64_t i = b; i < e; ++i) {
+                const uint64_t v = j.src[i], g = (v >> 4) & 0xFFFFFFFFull;
+                if (g < lo || g >= hi) {  // hits come sorted by (qid, seq_id, pos): mostly the same record
+                    seq = (uint32_t)(std::upper_bound(S.begin(), S.end(), g) - S.begin() - 1);
+                    lo = S[seq];
+                    hi = seq + 1 < S.size() ? S[seq + 1] : UINT64_MAX;
+                }
+                sahara_hit& h = j.dst[i];
+                h.qid = j.q0 + (v >> 36);
+                h.seq_id = seq;
+                h.err = (uint32_t)(v & 15u);
+                h.pos = g - lo;
+            }
+        });
+    }
+    int device_;
+    HostPool pool_;
+    const std::vector<uint64_t>* starts_ = nullptr;
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_, idle_;
+    std::vector<Job> q_;
+    bool stop_ = false, busy_ = false;
+    uint64_t submitted_ = 0, done_ = 0;
+    std::exception_ptr err_;
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t st = nullptr;
+    int numCU = 0;
+    DeviceIndex I;
+    // A text of 2^32 - 2 symbols or more is indexed in parts (splitRecords):
+    // part 0 is I, parts 1.. are `more`; a search runs over each part in turn
+    // (swapped into I) and merges the hits (run). partRec0[p] = the global id
+    // of part p's first record. exportPart selects the part the export test
+    // hooks read (sahara_gpu_select_part).
+    std::vector<DeviceIndex> more;
+    std::vector<uint64_t> partRec0{0};
+    uint32_t exportPart = 0;
+    DevBuf<sahara_hit> outAll;            // multi-part: hits of the parts so far
+
+    // staged inputs
+    DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern (FM phase)
+    DevBuf<uint4> pats3;                  // 3-bit-plane blocks, patBlocks per pattern (text phase)
+    uint64_t npat = 0;
+    uint32_t m = 0, patWords = 0, patBlocks = 0;
+    DevBuf<uint32_t> scheme, cover, kmerStart;        // FM scheme table; text table (textTable)
+    uint32_t nsearch = 0;
+    uint32_t maxErr = 0;
+    bool edit = true;
+    bool staged = false;
+    bool verify = true;
+    bool locateSA = true;
+    uint32_t split = 1;                   // text-phase threshold (rows per interval)
+    uint32_t textSteps = 4;               // text-phase micro-steps per lane per wave iteration
+    uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
+
+    // work buffers. Batches rotate over three slots so that the FM phase runs
+    // up to two batches ahead (stream `st`) of the text phase (stream `stB`),
+    // while batch i-1 runs its locate and sort (stream `stC`).
+    static constexpr int kSlots = 5;
+    struct Slot {
+        DevBuf<uint4> hits, tasks, seeds;  // seeds: starting cursors (kSeedItems -> kSearchFM)
+        DevBuf<uint32_t> seedItem;
+        DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
+        DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512), [512, 768)
+        hipEvent_t fmStart = nullptr, seedDone = nullptr, fmDone = nullptr, textStart = nullptr, textDone = nullptr,
+                   free = nullptr;
+    } slot[kSlots];
+    hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
+    uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
+    // two pinned staging chunks for handing hits to pageable host memory: the
+    // DMA of one chunk overlaps the host copy out of the other (copyOut)
+    static constexpr size_t kOutChunk = 32u << 20;
+    void* outStage[2] = {nullptr, nullptr};
+    size_t pinnedCap = 0;
+    bool pipeline = true;
+    DevBuf<uint4> stack;                  // FM spill stack (stream st only)
+    DevBuf<uint8_t> rawPats;              // staged pattern bytes before packing
+    DevBuf<uint8_t> nibPats;              // the same, two symbols per byte as uploaded (stageIn)
+    bool nibbleUpload = true;             // SAHARA_NIBBLE_UPLOAD=0: pattern bytes go up as given
+    uint8_t* nibHost = nullptr;           // pinned: the packed patterns on their way up (stage)
+    size_t nibHostCap = 0;
+    DevBuf<uint32_t> small;               // scratch counters for single-stream helpers
+    DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
+    DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
+    DevBuf<uint64_t> partial;             // tile sums of the segment scan
+    DevBuf<uint32_t> qcnt, big;           // per-query row counts (zero between batches); long segments
+    DevBuf<char> tmp;
+    DevBuf<sahara_hit> out;
+    uint64_t nout = 0;
+    double stageMs = 0;                   // wall time of the last stage(): H2D, pack, validation
+    uint32_t hitCap = 0, taskCap = 0;
+    sahara_stats stats{};
+    hipEvent_t ev[8] = {};
+
+    // Streamed query upload (sahara_gpu_search, sahara_gpu_search_reads): the
+    // source rows go up in chunks, each packed on the host (two symbols per
+    // byte, ranks checked) into a slot of a pinned ring and copied on stream
+    // stE when the first batch that needs it is issued, so that the upload of
+    // later batches overlaps the search of earlier ones. ringEv[s] fires once
+    // slot s's last DMA is done: the device-side unpacking waits for it, and
+    // the host waits for it before packing into the slot again. The ring is
+    // pinned once per context, in the background while the index loads.
+    struct Upload {
+        const uint8_t* src = nullptr;  // host symbols: the patterns, or the reads (rc)
+        bool rc = false;               // reads: reverse complements interleaved on the device
+        uint32_t bits = 4;             // 2: ACGT codes + N list, 4: nibbles, 8: bytes as given
+        uint64_t rows = 0;             // source rows
+        uint64_t chunk = 0;            // source rows per chunk (even: chunks start at even symbols)
+        uint64_t done = 0;             // source rows enqueued
+        bool bad = false;              // a chunk held a byte that is no rank of this index
+        double hostMs = 0;             // host time spent packing and enqueueing
+        uint64_t chunks[3] = {0, 0, 0};  // chunks sent at 2 / 4 / 8 bits per symbol
+    } up;
+    std::vector<std::vector<uint32_t>> excParts;  // per packing thread: N positions of a 2-bit chunk
+    bool streaming = false;
+    hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
+    static constexpr size_t kRingSlots = 8, kRingSlot = 32u << 20;  // 256 MB pinned
+    uint8_t* ring = nullptr;
+    hipEvent_t ringEv[kRingSlots] = {};
+    std::thread ringInit;                 // pins the ring (started by newCtx)
+    bool ringFailed = false;
+    DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
+    DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
+    std::unique_ptr<HostPool> pool;
+    // host sink of sahara_gpu_search: each batch's sorted hits go to host
+    // memory (pinned) on stF while later batches search
+    sahara_hit* sink = nullptr;
+    uint64_t sinkCap = 0, sinkDone = 0;
+    bool sinkOk = false;
+    uint64_t lastHits = 0;                // hits of the previous sahara_gpu_search (sink size estimate)
+    // compact download into the sink (Expander): device records of the
+    // pass, their pinned host staging, one event per batch's download
+    // (batch b's records land in slot b % kDownSlots of a pinned ring,
+    // pinned with the upload ring; the slot is reused once batch b is expanded)
+    bool compactSink = false, sinkPinned = false;
+    DevBuf<uint64_t> outC;
+    static constexpr size_t kDownSlots = 3, kDownSlot = 64u << 20;  // 8M records per batch
+    uint64_t* downRing = nullptr;
+    uint64_t downJobs = 0;                // batches handed to the expander this call
+    std::vector<hipEvent_t> downEv;
+    std::unique_ptr<Expander> expander;
+    // SAHARA_TIMING=2: host-side marks of one call (ms since its start, what)
+    bool traceOn = false;
+    std::chrono::steady_clock::time_point traceT0;
+    std::mutex traceMu;
+    std::vector<std::pair<double, std::string>> trace;
+    void mark(const char* what, uint64_t i) {
+        if (!traceOn) return;
+        const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - traceT0).count();
+        std::lock_guard<std::mutex> g(traceMu);
+        trace.emplace_back(t, std::string(what) + " " + std::to_string(i));
+    }
+
+    ~Ctx() {
+        expander.reset();
+        for (hipEvent_t e : downEv) (void)hipEventDestroy(e);
+        if (downRing) (void)hipHostFree(downRing);
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (ringInit.joinable()) ringInit.join();
+        for (auto& e : ringEv)
+            if (e) (void)hipEventDestroy(e);
+        if (ring) (void)hipHostFree(ring);
+        if (stE) (void)hipStreamDestroy(stE);
+        if (stF) (void)hipStreamDestroy(stF);
+        for (auto& sl : slot)
+            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmDone, sl.textStart, sl.textDone, sl.free})
+                if (e) (void)hipEventDestroy(e);
+        if (pinned) (void)hipHostFree(pinned);
+        if (nibHost) (void)hipHostFree(nibHost);
+        for (void* p : outStage)
+            if (p) (void)hipHostFree(p);
+        if (stB) (void)hipStreamDestroy(stB);
+        if (stC) (void)hipStreamDestroy(stC);
+        if (stD) (void)hipStreamDestroy(stD);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+    } catch (...) {
+        g_err = "unknown error";
+    }
+    return -1;
+}
+
+bool hitLess(const sahara_hit& a, const sahara_hit& b);
+void limitHits(std::vector<sahara_hit>& v, uint32_t n);
+void handOver(const std::vector<sahara_hit>& v, sahara_hit** hits, uint64_t* n_hits);
+Ctx* newCtx(int device);
+Ctx* ctxOf(void* p);
+HostPool& hostPool(Ctx* c);
+
+// staging.cpp: scheme tables, the query packers, the streamed upload
+void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
+                     std::vector<uint32_t>& out, uint32_t& maxErr);
+void textTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
+               const std::vector<uint32_t>& packed, std::vector<uint32_t>& out);
+bool hostHasAvx2();
+uint64_t pack2Scalar(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
+                     std::vector<uint32_t>& exc);
+uint64_t pack2Avx2(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
+                   std::vector<uint32_t>& exc);
+void uploadChunk(Ctx* c, hipStream_t kst);
+void ensureUploaded(Ctx* c, uint64_t patEnd, hipStream_t kst);
+void stageScheme(Ctx* c, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                 uint32_t ns, int edit);
+void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t m,
+                   const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit);
+void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l,
+           const uint32_t* u, uint32_t ns, int edit);
+
+// pass.cpp: one pass over the staged patterns (every part of the index)
+DeviceIndex& partOf(Ctx* c, uint32_t p);
+void run(Ctx* c, bool count);
+void runOne(Ctx* c, bool count);
+void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
+void growCap(uint32_t& cap, uint32_t seen);
+
+}  // namespace sahara

@@ -1,0 +1,668 @@
+// pass.cpp — one pass of the search over the staged patterns: batches
+// through seeds, FM phase, text phase, locate, sort and decode on the
+// context's streams, and the pass over every part of a
+// multi-part index.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+
+#include "ctx.h"
+
+namespace sahara {
+
+// One pass over the staged patterns in batches of <= 4M. Per batch:
+//   stream st : kSeedItems, kSearchFM        -> hits, tasks of its slot
+//   stream stB: kResolveTasks, kSearchText   -> hits of its slot
+//   stream stC: row offsets, locate, sort, decode
+// Three slots rotate, so the FM phase of batches i+1, i+2 (memory-latency
+// bound) overlaps the text phase of batch i (ALU bound), and both phases run
+// back to back while locate and sort of batch i-1 fill the gaps on stream
+// stC. Host order: finish(i-3), FM(i), text(i) — FM(i) reuses the slot that
+// locate(i-3) frees. Buffer overflow is detected
+// after the fact from each batch's flags; the whole pass is then redone on one
+// stream with grown buffers (`serial`), re-running a batch until it fits.
+void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
+
+void runOne(Ctx* c, bool count);
+
+DeviceIndex& partOf(Ctx* c, uint32_t p) { return p == 0 ? c->I : c->more.at(p - 1); }
+
+// Search over a multi-part index: the pass runs over every part in turn (the
+// staged patterns and scheme are shared; every part has the same k-mer
+// depth), its hits get the part's record offset, and one stable sort by qid
+// restores the canonical (qid, seq_id, pos, err) order, since part p's
+// records all follow part p - 1's. Exact under P-strict: a DFS node exists in
+// the whole index iff its interval is non-empty in some part, and its rows
+// are the union of its rows over the parts. Hits reach the
+// host after the last part (no per-batch sink).
+void run(Ctx* c, bool count) {
+    if (c->more.empty()) return runOne(c, count);
+    sahara_hit* sink = c->sink;
+    c->sink = nullptr;
+    sahara_stats T{};
+    uint64_t total = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        for (uint32_t p = 0; p <= c->more.size(); ++p) {
+            if (p) std::swap(c->I, c->more[p - 1]);
+            try {
+                runOne(c, count);
+            } catch (...) {
+                if (p) std::swap(c->I, c->more[p - 1]);
+                throw;
+            }
+            if (p) std::swap(c->I, c->more[p - 1]);
+            if (c->outAll.cap < total + c->nout) {  // grow, keeping the parts so far
+                DevBuf<sahara_hit> grown;
+                grown.reserve(std::max<uint64_t>((total + c->nout) + (total + c->nout) / 4, 1024));
+                if (total)
+                    SH_HIP(hipMemcpyAsync(grown.ptr, c->outAll.ptr, total * sizeof(sahara_hit), hipMemcpyDeviceToDevice,
+                                          c->st));
+                SH_HIP(hipStreamSynchronize(c->st));
+                c->outAll = std::move(grown);
+            }
+            launchOffsetSeq(c->out.ptr, c->nout, c->partRec0[p], c->outAll.ptr + total, c->st);
+            total += c->nout;
+            const sahara_stats& S = c->stats;  // the parts' work adds up
+            T.patterns = S.patterns;
+            T.search_grid = S.search_grid;
+            T.text_grid = S.text_grid;
+            T.pipelined = S.pipelined;
+            for (uint64_t sahara_stats::*f :
+                 {&sahara_stats::batches, &sahara_stats::cursors, &sahara_stats::nodes, &sahara_stats::rank_nodes,
+                  &sahara_stats::ext_lines, &sahara_stats::lf_steps, &sahara_stats::text_nodes,
+                  &sahara_stats::conversions, &sahara_stats::fm_iterations, &sahara_stats::text_iterations,
+                  &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
+                  &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
+                  &sahara_stats::text_steps, &sahara_stats::text_launches})
+                T.*f += S.*f;
+            for (double sahara_stats::*f : {&sahara_stats::search_ms, &sahara_stats::locate_ms, &sahara_stats::sort_ms,
+                                            &sahara_stats::text_ms, &sahara_stats::seed_ms})
+                T.*f += S.*f;
+            T.search_launches += S.search_launches;
+        }
+        if (c->out.cap < total) {
+            c->out.release();
+            c->out.reserve(std::max<uint64_t>(total, 1024));
+        }
+        sortHitsByQid(c->outAll.ptr, total, c->out.ptr, c->tmp, c->st);
+        SH_HIP(hipStreamSynchronize(c->st));
+    } catch (...) {
+        c->sink = sink;
+        throw;
+    }
+    c->sink = sink;
+    c->sinkDone = 0;
+    c->nout = total;
+    T.hits = total;
+    T.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    T.stage_ms = c->stageMs;
+    for (int b = 0; b < 3; ++b) T.upload_chunks[b] = c->stats.upload_chunks[b];
+    c->stats = T;
+}
+
+void runOne(Ctx* c, bool count) {
+    if (!c->staged) throw Error("sahara_gpu_run: nothing staged");
+    auto t0 = std::chrono::steady_clock::now();
+    if (const char* e = std::getenv("SAHARA_PIPELINE")) c->pipeline = std::atol(e) != 0;
+    sahara_stats S{};
+    bool overflow = false;
+    runPass(c, count, !c->pipeline, S, overflow);
+    if (overflow) {
+        S = sahara_stats{};
+        runPass(c, count, true, S, overflow);
+    }
+    S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    S.stage_ms = c->stageMs;
+    c->stats = S;
+}
+
+void growCap(uint32_t& cap, uint32_t seen) {
+    const uint64_t want = (uint64_t)seen + seen / 4 + 1024;
+    if (want >= (1ull << 32) - 2) throw Error("a work buffer would exceed 2^32 entries in one batch");
+    cap = std::max<uint32_t>(cap, (uint32_t)want);
+}
+
+void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
+    overflow = false;
+    S.patterns = c->npat;
+    const uint32_t sigma = c->I.sigma;
+    // FM LDS: the scheme table, then the bottom fmLdsDepth DFS levels (16 B
+    // per lane each; SAHARA_FM_LDS_DEPTH). None by default: with a depth-16
+    // k-mer table the FM phase is light, its stack lives in L2, and its 1.2 KB
+    // fit beside four text workgroups per CU (measured: depth 0 846M, 1 845M,
+    // 4 817M reads/s at C3)
+    // In the reference execution (verify off) every node is ranked from the
+    // root, the DFS runs ~100x deeper trees and nothing else needs the LDS:
+    // the bottom four levels there took C3 from 44.4M to 53.3M reads/s
+    // (2: 49.9M, 8: 53.1M; profiles/r02_v1_sweep_ref_fm_lds_depth.txt).
+    uint32_t fmLdsDepth = c->verify ? 0u : 4u;
+    if (const char* e = std::getenv("SAHARA_FM_LDS_DEPTH")) fmLdsDepth = (uint32_t)std::max(0, std::min(8, std::atoi(e)));
+    const size_t lds = (size_t)((c->nsearch * c->m + 3u) & ~3u) * 4 + (size_t)fmLdsDepth * 256 * 16;
+    const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
+    int bpc = fullBpc;
+    // Overlapped with the text phase of the previous batch, the FM phase
+    // (memory-latency bound) runs two workgroups per CU beside three text
+    // workgroups; alone it takes all that fit. (Measured at C3 with pruned
+    // text steps: text 3 + FM 2 846-873M reads/s, text 4 + FM 1 845-847M.)
+    // patterns per batch: 4M, fewer for schemes with many searches (work
+    // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
+    uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
+    if (const char* e = std::getenv("SAHARA_BATCH"))
+        maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
+    const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
+    if (!serial && batchesHere > 1 && c->verify) bpc = 2;
+    if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
+    const uint32_t blocks = (uint32_t)(c->numCU * bpc);
+    // the first batch's FM phase has nothing to overlap with: full occupancy
+    const uint32_t firstBlocks = std::getenv("SAHARA_FM_BPC") ? blocks : (uint32_t)(c->numCU * fullBpc);
+    const uint64_t T = (uint64_t)std::max(blocks, firstBlocks) * 256;
+    const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
+    c->stack.reserve((size_t)std::max<uint32_t>(stackCap, 5) * T);  // levels beyond the LDS part
+    S.search_grid = blocks;
+
+    // text phase geometry (LDS per lane: window | pattern | stack)
+    // window: |t| + what both sides can still consume <= m + 2k symbols, plus
+    // the block alignment of its start (31 symbols); 3 words per block
+    // (exact start: m + 2k symbols in whole blocks, copied funnel-shifted from
+    // one block more; SAHARA_EXACT_WINDOW=0: the block-aligned start below it)
+    const char* exactEnv = std::getenv("SAHARA_EXACT_WINDOW");
+    const uint32_t exactBlocks = (c->m + 2 * c->maxErr + 31) / 32;
+    const bool exactWindow = (!exactEnv || std::atoi(exactEnv) != 0) && exactBlocks + 1 <= 8 && c->patBlocks <= 8;
+    const uint32_t winBlocks = exactWindow ? exactBlocks : (c->m + 2 * c->maxErr + 31 + 31) / 32;
+    const uint32_t textStack = 2 * c->maxErr + 2;
+    // one-word stack entries where a node fits 30 bits (search.hip packNode)
+    // (SAHARA_PACKED_STACK; off by default: at m = 100 it buys a fourth text
+    // workgroup per CU, but costs a pack / unpack per micro-step, and three
+    // workgroups leave LDS for an FM workgroup beside them)
+    const bool packedStack = c->m <= 127 && winBlocks <= 7 && c->maxErr <= 7 && std::getenv("SAHARA_PACKED_STACK") &&
+                             std::atoi(std::getenv("SAHARA_PACKED_STACK")) != 0;
+    const uint32_t tableWords = std::max<uint32_t>(2 * c->nsearch * c->m, kTextTableMin);
+    const size_t textLds = (size_t)tableWords * 4 +
+                           (size_t)256 * (3 * (winBlocks + c->patBlocks) + (packedStack ? 1 : 2) * textStack) * 4;
+    if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
+    if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
+    int tbpc = 0;
+    // the text phase addresses text and a batch's patterns with 32-bit buffer offsets
+    const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
+                          maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
+    if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
+        tbpc = textBlocksPerCU(sigma, c->edit, packedStack, textLds);
+    // overlapped with the FM phase, three text workgroups per CU leave room
+    // for two FM workgroups beside them (the FM chain of seeds and FM launches
+    // is the other critical path once the text phase prunes dead children)
+    if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, packedStack, textLds), std::atoi(e)));
+    const uint32_t split = tbpc > 0 ? c->split : 0u;
+    // where a task's SA row becomes its text position: 2 = inside the text
+    // kernel, a chunk of task records ahead (default: no pass between the FM
+    // and text phases); 1 = kResolveTasks after the FM phase on its stream;
+    // 0 = kResolveTasks before the text phase (SAHARA_RESOLVE)
+    uint32_t fmPrio = 0;
+    if (const char* e = std::getenv("SAHARA_FM_PRIO")) fmPrio = (uint32_t)std::max(0, std::min(3, std::atoi(e)));
+    int resolveMode = 2;
+    if (const char* e = std::getenv("SAHARA_RESOLVE")) resolveMode = std::max(0, std::min(2, std::atoi(e)));
+    // (pipelined, in-kernel task resolve) the first batch's text phase starts
+    // on its seed tasks while its FM phase runs (SAHARA_EARLY_TEXT=0: after it)
+    const char* earlyEnv = std::getenv("SAHARA_EARLY_TEXT");
+    // (only with several batches: a lone batch's FM phase runs at full
+    // occupancy, and its text phase split in two measured 45M against 68M
+    // reads/s at C5)
+    const bool early = !serial && split && resolveMode == 2 && batchesHere > 1 &&
+                       (!earlyEnv || std::atoi(earlyEnv) != 0);
+    const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
+    S.text_grid = split ? textBlocks : 0u;
+    S.pipelined = serial ? 0u : 1u;
+
+    if (c->hitCap == 0) {
+        c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (const char* e = std::getenv("SAHARA_HITCAP")) c->hitCap = (uint32_t)std::max(1L, std::atol(e));
+    }
+    if (c->taskCap == 0) {
+        c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
+    }
+    // batch boundaries. SAHARA_RAMP (pipelined only): 1 makes the first two
+    // batches smaller (1/4, 1/2 of the others) so that the FM phase of the
+    // first, which overlaps nothing, is short; 2 also the last two
+    std::vector<uint64_t> bstart{0};
+    {
+        const int rampMode = std::getenv("SAHARA_RAMP") ? std::atoi(std::getenv("SAHARA_RAMP")) : 0;
+        const bool up = !serial && rampMode >= 1 && c->npat > 3 * maxBatch;
+        const bool down = up && rampMode >= 2;
+        const uint64_t edge[2] = {std::max<uint64_t>(maxBatch / 4, 1), std::max<uint64_t>(maxBatch / 2, 1)};
+        const uint64_t mid = c->npat - (up ? edge[0] + edge[1] : 0) - (down ? edge[0] + edge[1] : 0);
+        if (up) {
+            bstart.push_back(edge[0]);
+            bstart.push_back(edge[0] + edge[1]);
+        }
+        const uint64_t nmid = (mid + maxBatch - 1) / maxBatch, q0 = bstart.back();
+        for (uint64_t i = 1; i <= nmid; ++i) bstart.push_back(q0 + mid * i / nmid);
+        if (down) {
+            bstart.push_back(bstart.back() + edge[1]);
+            bstart.push_back(bstart.back() + edge[0]);
+        }
+    }
+    const uint64_t nbatch = bstart.size() - 1;
+    if (c->pinnedCap < nbatch * 8) {
+        if (c->pinned) SH_HIP(hipHostFree(c->pinned));
+        c->pinned = nullptr;
+        SH_HIP(hipHostMalloc(&c->pinned, nbatch * 8 * sizeof(uint32_t)));
+        c->pinnedCap = nbatch * 8;
+    }
+    if (c->qcnt.cap < maxBatch + 1) {
+        c->qcnt.reserve(maxBatch + 1);
+        c->qoff.reserve(maxBatch + 1);
+        c->big.reserve(maxBatch);
+    }
+    SH_HIP(hipMemsetAsync(c->qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
+    hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
+    SH_HIP(hipStreamSynchronize(c->st));
+    SH_HIP(hipStreamSynchronize(c->stB));
+    SH_HIP(hipStreamSynchronize(c->stC));
+    SH_HIP(hipStreamSynchronize(c->stD));
+    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
+    c->nout = 0;
+    c->sinkDone = 0;
+    c->sinkOk = c->sink != nullptr;
+    // a slot's counters and queues are zero when its `free` event fires:
+    // here for the first use, after its locate (finish) for the next
+    auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
+        SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), s));
+        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 768 * sizeof(uint32_t), s));
+        SH_HIP(hipEventRecord(sl.free, s));
+    };
+    for (auto& sl : c->slot) resetSlot(sl, sA);
+
+    auto issueFM = [&](uint64_t b) {
+        Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
+        const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
+        sl.hits.reserve((size_t)c->hitCap + 1);
+        sl.tasks.reserve((size_t)c->taskCap);
+        SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
+        SearchArgs a{};
+        a.occF = c->I.occF.ptr;
+        a.occR = c->I.occR.ptr;
+        for (int i = 0; i < 8; ++i) a.C[i] = (uint32_t)c->I.C[i];
+        a.n = (uint32_t)c->I.n;
+        a.pats = c->pats.ptr + q0 * c->patWords;
+        a.patWords = c->patWords;
+        a.m = c->m;
+        a.nsearch = c->nsearch;
+        a.nitems = (uint32_t)(nb * c->nsearch);
+        a.scheme = c->scheme.ptr;
+        a.work = sl.queues.ptr;
+        a.hitCount = sl.small.ptr + 1;
+        a.flags = sl.small.ptr + 2;
+        a.filled = sl.small.ptr + 3;
+        a.taskCount = sl.small.ptr + 4;
+        a.stack = c->stack.ptr;
+        a.stackCap = stackCap;
+        a.hits = sl.hits.ptr;
+        a.hitCap = c->hitCap;
+        a.counters = c->counters.ptr;
+        a.tasks = sl.tasks.ptr;
+        a.taskCap = c->taskCap;
+        a.split = split;
+        a.ldsDepth = fmLdsDepth;
+        a.prio = serial ? 0u : fmPrio;
+        // starting cursors; reference execution (verify off) ranks every node
+        // from the root, so it does not use the k-mer table
+        SeedArgs sd{};
+        sd.pats = a.pats;
+        sd.patWords = c->patWords;
+        sd.nsearch = c->nsearch;
+        sd.nitems = a.nitems;
+        sd.n = a.n;
+        sd.kmer = c->verify && c->I.kmerK ? c->I.kmer.ptr : nullptr;
+        sd.kmerK = c->I.kmerK;
+        sd.kmerStart = c->kmerStart.ptr;
+        sl.seeds.reserve(a.nitems);
+        sl.seedItem.reserve(a.nitems);
+        sd.seeds = sl.seeds.ptr;
+        sd.seedItem = sl.seedItem.ptr;
+        sd.seedCount = sl.small.ptr + 6;
+        sd.m = c->m;
+        const char* seedTasks = std::getenv("SAHARA_SEED_TASKS");  // 0: every seed goes through the FM kernel
+        sd.toText = split >= 1 && (!seedTasks || std::atoi(seedTasks) != 0) ? 1u : 0u;
+        sd.tasks = sl.tasks.ptr;
+        sd.taskCap = c->taskCap;
+        sd.taskCount = sl.small.ptr + 4;
+        sd.flags = sl.small.ptr + 2;
+        sd.counters = count ? c->counters.ptr : nullptr;
+        a.seeds = sl.seeds.ptr;
+        a.seedItem = sl.seedItem.ptr;
+        a.seedCount = sl.small.ptr + 6;
+        // seeds on their own stream (sD), so that they run ahead of the FM
+        // phase of the batch before (both are HBM-latency bound and light)
+        SH_HIP(hipStreamWaitEvent(sD, sl.free, 0));
+        // streamed upload: the batch's patterns (packed here on the host while
+        // the batches before it search; unpacked on sD ahead of its seeds)
+        ensureUploaded(c, bstart[b + 1], sD);
+        SH_HIP(hipEventRecord(sl.fmStart, sD));
+        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sD);
+        if (early && b == 0)  // the seed tasks end here: the text phase may start on them
+            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+        SH_HIP(hipEventRecord(sl.seedDone, sD));
+        SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
+        launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
+        if (split && resolveMode == 1)
+            launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sA);
+        SH_HIP(hipEventRecord(sl.fmDone, sA));
+        ++S.search_launches;
+    };
+    auto issueText = [&](uint64_t b) {
+        Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
+        const uint64_t q0 = bstart[b];
+        const bool split0 = early && b == 0;
+        SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone : sl.fmDone, 0));
+        SH_HIP(hipEventRecord(sl.textStart, sB));
+        if (split) {
+            TextArgs t{};
+            t.sa = c->I.saFull.ptr;
+            t.text3 = c->I.text3.ptr;
+            t.pats3 = c->pats3.ptr + q0 * c->patBlocks;
+            t.patBlocks = c->patBlocks;
+            t.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
+            t.pats3Bytes = (uint32_t)std::min<uint64_t>((c->npat - q0) * c->patBlocks * 16, 0xFFFFFF00ull);
+            t.m = c->m;
+            t.nsearch = c->nsearch;
+            t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
+            t.tasks = sl.tasks.ptr;
+            t.taskCount = sl.small.ptr + 4;
+            t.taskCap = c->taskCap;
+            t.work = sl.queues.ptr + 256;
+            t.hits = sl.hits.ptr;
+            t.hitCap = c->hitCap;
+            t.hitCount = sl.small.ptr + 1;
+            t.filled = sl.small.ptr + 3;
+            t.flags = sl.small.ptr + 2;
+            t.counters = c->counters.ptr;
+            t.winBlocks = winBlocks;
+            t.exactWindow = exactWindow ? 1u : 0u;
+            // (SAHARA_PRUNE=0 turns it off; C3: 43 -> 28 micro-steps per read,
+            // C5: 439 -> 303 and 68M -> 82M reads/s)
+            const char* pruneEnv = std::getenv("SAHARA_PRUNE");
+            t.prune = !pruneEnv || std::atoi(pruneEnv) != 0 ? 1u : 0u;
+            t.stackCap = textStack;
+            t.packedStack = packedStack ? 1u : 0u;
+            t.tableWords = tableWords;
+            t.resolveRows = resolveMode == 2 ? 1u : 0u;
+            t.steps = c->textSteps;
+            t.refillAt = c->refillAt;
+            if (resolveMode == 0)
+                launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
+            if (split0) {
+                // the first batch's seed tasks while its FM phase runs, then the
+                // tasks the FM phase appended after them
+                t.taskCount = sl.small.ptr + 5;
+                launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+                SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+                t.taskBegin = sl.small.ptr + 5;
+                t.taskCount = sl.small.ptr + 4;
+                t.work = sl.queues.ptr + 512;
+                ++S.text_launches;
+            }
+            launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+            ++S.text_launches;
+        }
+        SH_HIP(hipEventRecord(sl.textDone, sB));
+    };
+    // locate: row offsets (exclusive scan of len), SA / LF locate, canonical
+    // sort, decode into the device-resident output, on stream sC. Needs the
+    // batch's counts (host waits for its text phase). Returns false on
+    // overflow; `finishCheck` then reads the locate flags and timings.
+    uint32_t seenTask = 0, seenHit = 0;  // pipelined overflow: the caps the re-run needs
+    auto finish = [&](uint64_t b) {
+        Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
+        const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
+        c->mark("finish", b);
+        // the batch's counters, copied on sC (a copy on sB would wait for CU
+        // slots between two text phases)
+        SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 8, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipEventRecord(c->ev[6], sC));
+        SH_HIP(hipEventSynchronize(c->ev[6]));
+        c->mark("text done", b);
+        const uint32_t* hs = c->pinned + b * 8;
+        float ms = 0;
+        SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
+        S.seed_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, sl.seedDone, sl.fmDone));
+        S.search_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+        S.text_ms += ms;
+        if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
+        if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
+        if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
+            // (pipelined: issueFM may be reading the caps on the other host
+            // thread; they grow after the pass, before the serial re-run)
+            if (hs[2] & 8u) growCap(serial ? c->taskCap : seenTask, hs[4]);
+            if (hs[2] & 2u) growCap(serial ? c->hitCap : seenHit, hs[1]);
+            overflow = true;
+            resetSlot(sl, sC);
+            return false;
+        }
+        // reserved slots incl. len-0 holes; a wave's last range may reach past
+        // the capacity without having written there (no overflow flag)
+        const uint64_t nh = std::min<uint64_t>(hs[1], c->hitCap);
+        S.cursors += hs[3];
+        SH_HIP(hipEventRecord(c->ev[2], sC));
+        SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
+        c->partial.reserve(scanTiles((uint32_t)nb));
+        querySegments(sl.hits.ptr, nh, c->qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr,
+                      c->small.ptr + 4, sC);
+        uint64_t rows = 0;
+        uint32_t nbig = 0;
+        SH_HIP(hipMemcpyAsync(&rows, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipMemcpyAsync(&nbig, c->small.ptr + 4, 4, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipStreamSynchronize(sC));
+        c->mark("rows", b);
+        if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
+        c->k0.reserve(std::max<uint64_t>(rows, 1));
+        if (nbig) c->k1.reserve(std::max<uint64_t>(rows, 1));
+        LocateArgs la{};
+        la.hits = sl.hits.ptr;
+        la.nhits = nh;
+        la.qoff = c->qoff.ptr;
+        la.qcnt = c->qcnt.ptr;
+        la.occF = c->I.occF.ptr;
+        for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
+        la.samples = c->I.samples.ptr;
+        la.rate = c->I.rate;
+        la.keys = c->k0.ptr;
+        la.flags = c->small.ptr + 2;
+        la.counters = c->counters.ptr + 3;
+        la.sa = c->I.saFull.ptr;
+        la.useSA = c->locateSA ? 1u : 0u;
+        launchLocate(la, count, sC);
+        SH_HIP(hipEventRecord(c->ev[3], sC));
+        resetSlot(sl, sC);  // the slot's hits are consumed
+        if (nbig) c->tmp.reserve(bigSortTempBytes(rows, nbig) + 256);
+        if (c->nout + rows > c->out.cap) {  // grow the device-resident output
+            const size_t want = std::max<size_t>((c->nout + rows) + (c->nout + rows) / 2, 1024);
+            sahara_hit* np = nullptr;
+            SH_HIP(hipMalloc(&np, want * sizeof(sahara_hit)));
+            if (c->nout) SH_HIP(hipMemcpyAsync(np, c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToDevice, sC));
+            SH_HIP(hipStreamSynchronize(sC));
+            SH_HIP(hipStreamSynchronize(c->stF));  // sink copies may still read the old buffer
+            c->out.release();
+            c->out.ptr = np;
+            c->out.cap = want;
+        }
+        sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, q0, c->I.dRecStarts.ptr,
+                   (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, c->tmp.ptr, c->tmp.cap, sC);
+        SH_HIP(hipEventRecord(c->ev[4], sC));
+        // sahara_gpu_search's host sink: the batch's hits go to host memory
+        // on stF while later batches search (while they fit the sink)
+        if (c->sinkOk && c->nout + rows <= c->sinkCap) {
+            const bool compact = c->compactSink && rows * sizeof(uint64_t) <= Ctx::kDownSlot && nb < (1ull << 28);
+            if (rows && compact) {  // 8-B records, expanded on the host (Expander)
+                const uint64_t j = c->downJobs++;
+                const size_t slot = (size_t)(j % Ctx::kDownSlots);
+                if (j >= Ctx::kDownSlots) c->expander->waitFor(j + 1 - Ctx::kDownSlots);  // the slot is read
+                if (c->downEv.size() <= slot) {
+                    const size_t had = c->downEv.size();
+                    c->downEv.resize(Ctx::kDownSlots);
+                    for (size_t i = had; i < Ctx::kDownSlots; ++i)
+                        SH_HIP(hipEventCreateWithFlags(&c->downEv[i], hipEventDisableTiming));
+                }
+                uint64_t* stage = c->downRing + slot * (Ctx::kDownSlot / sizeof(uint64_t));
+                c->outC.reserve(Ctx::kDownSlots * (Ctx::kDownSlot / sizeof(uint64_t)));
+                uint64_t* dev = c->outC.ptr + slot * (Ctx::kDownSlot / sizeof(uint64_t));
+                launchCompactHits(c->out.ptr + c->nout, rows, q0, c->I.dRecStarts.ptr, dev, sC);
+                SH_HIP(hipEventRecord(c->ev[7], sC));
+                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[7], 0));
+                SH_HIP(hipMemcpyAsync(stage, dev, rows * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stF));
+                SH_HIP(hipEventRecord(c->downEv[slot], c->stF));
+                c->expander->submit({c->downEv[slot], stage, c->sink + c->nout, rows, q0});
+            } else if (rows && c->sinkPinned) {
+                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[4], 0));
+                SH_HIP(hipMemcpyAsync(c->sink + c->nout, c->out.ptr + c->nout, rows * sizeof(sahara_hit),
+                                      hipMemcpyDeviceToHost, c->stF));
+            } else if (rows) {  // neither fits: the rest goes after the pass
+                c->sinkOk = false;
+            }
+            if (c->sinkOk) c->sinkDone = c->nout + rows;
+        } else {
+            c->sinkOk = false;
+        }
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 8 + 7, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipEventRecord(c->ev[5], sC));
+        c->nout += rows;
+        S.hits += rows;
+        return true;
+    };
+    auto finishCheck = [&](uint64_t b) {
+        SH_HIP(hipEventSynchronize(c->ev[5]));
+        if (c->pinned[b * 8 + 7] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
+        float ms = 0;
+        SH_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+        S.locate_ms += ms;
+        SH_HIP(hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
+        S.sort_ms += ms;
+    };
+
+    if (!serial) {
+        // Two host threads. This one packs the queries of a streamed upload
+        // and issues seeds, FM(b) and text(b) as soon as batch b's slot is
+        // free; a finisher thread waits for each batch's text phase and
+        // issues its locate, sort and hit download, so that batch b's hits
+        // leave while later batches are still being packed and searched.
+        // FM(b) reuses the slot that finish(b - kSlots) released.
+        std::mutex mu;
+        std::condition_variable cv;
+        uint64_t issued = 0, released = 0;  // batches issued; batches whose slot is released
+        bool stop = false;
+        std::exception_ptr finErr;
+        std::thread finisher([&] {
+            try {
+                SH_HIP(hipSetDevice(c->device));
+                bool pending = false;  // finishCheck owed for batch `owed`
+                uint64_t owed = 0;
+                for (uint64_t f = 0; f < nbatch; ++f) {
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return issued > f || stop; });
+                        if (issued <= f) break;
+                    }
+                    if (pending) finishCheck(owed);
+                    pending = finish(f);
+                    owed = f;
+                    {
+                        std::lock_guard<std::mutex> g(mu);
+                        released = f + 1;
+                        if (overflow) stop = true;  // the caller redoes the pass serially
+                    }
+                    cv.notify_all();
+                    if (overflow) break;
+                }
+                if (pending) finishCheck(owed);
+            } catch (...) {
+                finErr = std::current_exception();
+            }
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            cv.notify_all();
+        });
+        std::exception_ptr issueErr;
+        try {
+            for (uint64_t b = 0; b < nbatch; ++b) {
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return b < released + Ctx::kSlots || stop; });
+                    if (stop) break;
+                }
+                c->mark("issue", b);
+                issueFM(b);
+                issueText(b);
+                c->mark("issued", b);
+                ++S.batches;
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    issued = b + 1;
+                }
+                cv.notify_all();
+            }
+        } catch (...) {
+            issueErr = std::current_exception();
+        }
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (issueErr) stop = true;
+        }
+        cv.notify_all();
+        finisher.join();
+        if (issueErr) std::rethrow_exception(issueErr);
+        if (finErr) std::rethrow_exception(finErr);
+        if (overflow) {
+            c->taskCap = std::max(c->taskCap, seenTask);
+            c->hitCap = std::max(c->hitCap, seenHit);
+        }
+        SH_HIP(hipStreamSynchronize(sA));
+        SH_HIP(hipStreamSynchronize(sB));
+        SH_HIP(hipStreamSynchronize(sC));
+        SH_HIP(hipStreamSynchronize(sD));
+        SH_HIP(hipStreamSynchronize(c->stF));
+        if (overflow) return;  // the caller redoes the pass serially with the grown buffers
+    } else {
+        for (uint64_t b = 0; b < nbatch; ++b) {
+            ++S.batches;
+            for (;;) {  // re-run the batch until its buffers suffice
+                overflow = false;
+                issueFM(b);
+                issueText(b);
+                if (finish(b)) {
+                    finishCheck(b);
+                    break;
+                }
+            }
+        }
+        overflow = false;
+        SH_HIP(hipStreamSynchronize(c->stF));
+    }
+    if (count) {
+        unsigned long long h[16];
+        SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipStreamSynchronize(sC));
+        S.nodes = h[0];
+        S.rank_nodes = h[1];
+        S.ext_lines = h[2];
+        S.lf_steps = h[3];
+        S.text_nodes = h[5];
+        S.conversions = h[6];  // text tasks
+        S.fm_iterations = h[7];
+        S.text_iterations = h[8];
+        S.text_active = h[9];
+        S.text_refills = h[10];
+        S.text_cycles_refill = h[11];
+        S.text_cycles_step = h[12];
+        S.text_cycles_emit = h[13];
+        S.text_compare_steps = h[14];
+        S.text_steps = h[15];
+    }
+}
+
+}  // namespace sahara
