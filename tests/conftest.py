@@ -15,6 +15,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gpu_device():
+    # torch's HIP state first: some GPU tests hand device buffers to the
+    # library, and torch initialised after the library's own HIP calls
+    # reported no device when a run started with those tests
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     import sahara_amd as sa
     n = sa.lib().sahara_gpu_device_count()
     if n < 1:
