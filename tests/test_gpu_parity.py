@@ -395,3 +395,25 @@ def test_pinned_hit_sink_grows_and_is_recycled(gpu_device, monkeypatch):
         assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
     assert np.array_equal(hits_as_rows(kept), want)  # a held buffer is never handed out again
     del small, kept
+
+
+@pytest.mark.parametrize("m,k,gen", [(400, 2, "h2-k2"), (1000, 2, "h2-k2"), (700, 3, "pigeon")])
+def test_long_reads(gpu_device, m, k, gen):
+    """Reads far beyond the bench's 100 / 250 bp: windows of more than eight
+    blocks copied in rounds (m = 400: one text workgroup per CU), and reads
+    whose window and pattern no longer fit the text phase's LDS (m = 700,
+    1000), which stay in the FM phase to the end. Same hits as the oracle;
+    every read found at its origin."""
+    flat, lens = sa.synth_reference([400_000, 250_000], sigma=6, seed=m)
+    reads, origin = sa.synth_reads(flat, lens, 300, m, k, sigma=6, seed=k, with_origin=True)
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme(gen, 0, k, m)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    got = hits_as_rows(sa.search_reads(gpu, reads, sch))
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
+    assert np.array_equal(got, hits_as_rows(ref.search(pats, sch, nthreads=8)[0]))
+    fwd = got[got[:, 0] % 2 == 0]
+    hit = {(int(q) // 2, int(s), int(p)) for q, s, p, e in fwd}
+    assert all(any((i, int(origin[i, 0]), int(origin[i, 1]) + d) in hit for d in range(-k, k + 1))
+               for i in range(len(reads)))
