@@ -156,3 +156,27 @@ def test_2bit_pattern_forms_any_length(gpu_device, monkeypatch, m):
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
     assert np.array_equal(want, hits_as_rows(ref.search(sa.interleave_rc(reads, 6), sch, nthreads=8)[0]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", ["2", "4"])
+def test_streamed_upload_dna4(gpu_device, monkeypatch, bits):
+    """A dna4 index (sigma 5, A C G T = 1..4): the 2-bit codes unpack through
+    the dna4 table, no N exists, and an N (rank 5 here) is out of range."""
+    monkeypatch.setenv("SAHARA_UPLOAD_BITS", bits)
+    monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "128")
+    flat, lens = sa.synth_reference([200_000, 150_000], sigma=5, seed=41)
+    reads = sa.synth_reads(flat, lens, 1500, 64, 2, sigma=5, seed=43)
+    pats = sa.interleave_rc(reads, 5)
+    sch = sa.search_scheme("h2-k2", 0, 2, 64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 5, 16)
+    want = hits_as_rows(ref.search(pats, sch, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=5, device=gpu_device)
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want)
+    assert gpu.stats()["upload_chunks"][0 if bits == "2" else 1] > 0
+    bad = reads.copy()
+    bad[700, 9] = 5
+    with pytest.raises(sa.SaharaError, match="out of range"):
+        sa.search_reads(gpu, bad, sch)
