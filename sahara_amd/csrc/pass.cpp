@@ -452,8 +452,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(c->ev[2], sC));
         SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
         c->partial.reserve(scanTiles((uint32_t)nb));
-        querySegments(sl.hits.ptr, nh, c->qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr,
-                      c->small.ptr + 4, sC);
+        c->hrank.reserve(std::max<uint64_t>(nh, 1));
+        querySegments(sl.hits.ptr, nh, c->qcnt.ptr, c->hrank.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr,
+                      c->big.ptr, c->small.ptr + 4, sC);
         uint64_t rows = 0;
         uint32_t nbig = 0;
         SH_HIP(hipMemcpyAsync(&rows, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
@@ -467,7 +468,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         la.hits = sl.hits.ptr;
         la.nhits = nh;
         la.qoff = c->qoff.ptr;
-        la.qcnt = c->qcnt.ptr;
+        la.rank = c->hrank.ptr;
         la.occF = c->I.occF.ptr;
         for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
         la.samples = c->I.samples.ptr;

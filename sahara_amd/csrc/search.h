@@ -104,7 +104,7 @@ struct LocateArgs {
     const uint4* hits;
     uint64_t nhits;
     const uint64_t* qoff;          // per-query row segments (querySegments)
-    uint32_t* qcnt;                // per-query row counts, counted back to 0
+    const uint32_t* rank;          // per cursor: slot of its first row in the segment (querySegments)
     const OccLine* occF;
     uint32_t C[8];
     const uint32_t* samples;
@@ -146,8 +146,9 @@ void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, ui
 // the host), launchLocate (keys into the segments), sortDecode (short
 // segments in registers, medium across a wave, long by segmented radix sort).
 uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
-void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
-                   uint32_t* big, uint32_t* nbig, hipStream_t st);
+// qcnt: all zero on entry and on return; rank: one slot per hit
+void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* rank, uint32_t nq, uint64_t* qoff,
+                   uint64_t* partial, uint32_t* big, uint32_t* nbig, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
 size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
 void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff, uint32_t nq, const uint32_t* big,

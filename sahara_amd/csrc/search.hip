@@ -1106,13 +1106,18 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
 
 // ================================================================ locate ====
 
-// Rows per query: qcnt[qid] += len for every reported cursor. qcnt is all
-// zero between batches (kLocate counts it back down).
-__global__ void kCountRows(const uint4* __restrict__ hits, uint64_t nhits, uint32_t* __restrict__ qcnt) {
+// Rows per query: qcnt[qid] += len for every reported cursor, and the count
+// before the add is the cursor's first slot in its query's segment (rank), so
+// that kLocate places its rows without atomics of its own. The adds execute
+// at the memory side (one 64-B request per lane for scattered qids); this is
+// the only atomic pass of the locate chain. qcnt is all zero between batches
+// (kScanTiles clears what it read).
+__global__ void kCountRows(const uint4* __restrict__ hits, uint64_t nhits, uint32_t* __restrict__ qcnt,
+                           uint32_t* __restrict__ rank) {
     for (uint64_t h = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; h < nhits;
          h += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 hit = hits[h];
-        if (hit.z) atomicAdd(qcnt + hit.x, hit.z);
+        if (hit.z) rank[h] = atomicAdd(qcnt + hit.x, hit.z);
     }
 }
 
@@ -1177,7 +1182,7 @@ __global__ __launch_bounds__(256) void kScanPartials(uint64_t* __restrict__ part
     }
 }
 
-__global__ __launch_bounds__(256) void kScanTiles(const uint32_t* __restrict__ cnt, uint32_t n,
+__global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, uint32_t n,
                                                  const uint64_t* __restrict__ partial, uint64_t* __restrict__ off,
                                                  uint32_t* __restrict__ list, uint32_t* __restrict__ nlist) {
     __shared__ uint64_t wsum[4];
@@ -1190,6 +1195,7 @@ __global__ __launch_bounds__(256) void kScanTiles(const uint32_t* __restrict__ c
     for (uint32_t c = 0; c < kScanTile; c += 256) {  // uniform trip count: block scans inside
         const uint32_t i = base + c + threadIdx.x;
         const uint32_t v = i < n ? cnt[i] : 0u;
+        if (v) cnt[i] = 0u;  // zero again for the next batch
         uint64_t tot;
         const uint64_t ex = blockExclusiveScan(v, tot, wsum);
         if (i < n) off[i] = carry + ex;
@@ -1211,8 +1217,7 @@ __global__ __launch_bounds__(256) void kScanTiles(const uint32_t* __restrict__ c
 
 // One lane per reported cursor: locate every row of [lb, lb+len) into the
 // query's segment [qoff[qid], qoff[qid+1]) of the key array (key = text
-// position << 4 | e); the slot within the segment comes from counting
-// qcnt[qid] back down, which leaves qcnt zero for the next batch.
+// position << 4 | e), from the slot kCountRows ranked it at.
 template <bool COUNT>
 __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
     uint64_t steps = 0;
@@ -1220,7 +1225,7 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
          h += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 hit = a.hits[h];
         if (hit.z == 0) continue;  // reserved hole
-        const uint64_t out = a.qoff[hit.x] + (atomicSub(a.qcnt + hit.x, hit.z) - hit.z);
+        const uint64_t out = a.qoff[hit.x] + a.rank[h];
         const uint64_t e = hit.w & 0xFu;
         if (hit.w & kPosKnown) {  // resolved by the text phase
             a.keys[out] = ((uint64_t)hit.y << 4) | e;
@@ -1285,24 +1290,116 @@ __device__ __forceinline__ void cswap(uint64_t& a, uint64_t& b) {
     b = hi;
 }
 
-// Sort + decode of the short and medium segments, one lane per query: a
-// segment of <= kSmallSeg rows is sorted in the lane's registers
-// (odd-even transposition, padded with ~0); the wave then takes its medium
-// segments one by one, one key per lane, bitonic-sorted over shuffles.
-// Long segments are left to the segmented radix sort.
+// Sort + decode, one workgroup per 256 consecutive queries. Their segments
+// are one contiguous key range; when it fits kTileKeys (the common case: ~1.3
+// rows per query) it is staged in LDS by coalesced loads, every segment is
+// sorted there, and the decoded hits leave as one coalesced run of 24-B
+// records. Per segment: <= kSmallSeg rows sorted in the lane's registers
+// (odd-even transposition, padded with ~0); medium ones by the wave, one key
+// per lane, bitonic over shuffles; long ones are left to the segmented radix
+// sort (kDecodeBig). Record starts sit in LDS for texts of <= kLdsStarts
+// records, so a decode's binary search waits on no global loads. A range
+// larger than the tile takes the same tiers straight from global memory.
+constexpr uint32_t kTileKeys = 1024;
+constexpr uint32_t kLdsStarts = 256;
+constexpr uint16_t kSkipRow = 0xFFFFu;
+
 __global__ __launch_bounds__(256) void kSortDecode(const uint64_t* __restrict__ keys,
                                                   const uint64_t* __restrict__ qoff, uint32_t nq, uint64_t qidBase,
                                                   const uint64_t* __restrict__ starts, uint32_t nrec,
                                                   sahara_hit* __restrict__ out) {
-    const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t q0 = blockIdx.x * blockDim.x; q0 < nq; q0 += gridDim.x * blockDim.x) {
-        const uint32_t q = q0 + threadIdx.x;
-        uint64_t b = 0;
-        uint32_t n = 0;
-        if (q < nq) {
-            b = qoff[q];
-            n = (uint32_t)(qoff[q + 1] - b);
+    __shared__ uint64_t sk[kTileKeys];
+    __shared__ uint64_t soff[257];
+    __shared__ uint64_t sst[kLdsStarts];
+    __shared__ uint16_t sq[kTileKeys];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const bool ldsStarts = nrec <= kLdsStarts;
+    if (ldsStarts)
+        for (uint32_t i = t; i < nrec; i += 256) sst[i] = starts[i];
+    auto decode = [&](uint64_t k, uint64_t qid) {
+        const uint64_t gpos = k >> 4;
+        uint32_t lo = 0, hi = nrec;
+        uint64_t s0 = 0;
+        if (ldsStarts) {
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (sst[mid] <= gpos) lo = mid; else hi = mid;
+            }
+            s0 = sst[lo];
+        } else {
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (starts[mid] <= gpos) lo = mid; else hi = mid;
+            }
+            s0 = starts[lo];
         }
+        sahara_hit h;
+        h.qid = qid;
+        h.seq_id = lo;
+        h.err = (uint32_t)(k & 15u);
+        h.pos = gpos - s0;
+        return h;
+    };
+    for (uint32_t q0 = blockIdx.x * 256u; q0 < nq; q0 += gridDim.x * 256u) {
+        const uint32_t q = q0 + t;
+        soff[t] = qoff[q < nq ? q : nq];
+        if (t == 0) soff[256] = qoff[q0 + 256u < nq ? q0 + 256u : nq];
+        __syncthreads();
+        const uint64_t base = soff[0], R = soff[256] - base;
+        const uint64_t b = soff[t];
+        const uint32_t n = q < nq ? (uint32_t)(soff[t + 1] - b) : 0u;
+        if (R <= kTileKeys) {  // block-uniform
+            for (uint32_t i = t; i < (uint32_t)R; i += 256) sk[i] = keys[base + i];
+            __syncthreads();
+            const uint32_t lb = (uint32_t)(b - base);
+            if (n && n <= kSmallSeg) {
+                uint64_t v[kSmallSeg];
+#pragma unroll
+                for (uint32_t i = 0; i < kSmallSeg; ++i) v[i] = i < n ? sk[lb + i] : ~0ull;
+#pragma unroll
+                for (uint32_t r = 0; r < kSmallSeg; ++r) {
+                    if (r >= n) break;
+#pragma unroll
+                    for (uint32_t i = r & 1u; i + 1 < kSmallSeg; i += 2) cswap(v[i], v[i + 1]);
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < kSmallSeg; ++i)
+                    if (i < n) {
+                        sk[lb + i] = v[i];
+                        sq[lb + i] = (uint16_t)t;
+                    }
+            } else if (n > kMediumSeg) {
+                for (uint32_t i = 0; i < n; ++i) sq[lb + i] = kSkipRow;  // the radix path decodes it
+            }
+            uint64_t med = __ballot(n > kSmallSeg && n <= kMediumSeg);
+            while (med) {
+                const int src = __ffsll((long long)med) - 1;
+                med &= med - 1;
+                const uint32_t sn = (uint32_t)__shfl((int)n, src), slb = (uint32_t)__shfl((int)lb, src);
+                uint64_t v = lane < sn ? sk[slb + lane] : ~0ull;
+#pragma unroll
+                for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                        const uint64_t o = __shfl_xor(v, j);
+                        const bool keepMin = ((lane & j) == 0) == ((lane & k) == 0);
+                        v = keepMin ? (v < o ? v : o) : (v < o ? o : v);
+                    }
+                }
+                if (lane < sn) {
+                    sk[slb + lane] = v;
+                    sq[slb + lane] = (uint16_t)((t & ~63u) + (uint32_t)src);
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = t; i < (uint32_t)R; i += 256) {
+                const uint32_t lq = sq[i];
+                if (lq != kSkipRow) out[base + i] = decode(sk[i], qidBase + q0 + lq);
+            }
+            __syncthreads();  // soff, sk, sq are reused by the next range
+            continue;
+        }
+        __syncthreads();  // soff is reused by the next range
         if (n && n <= kSmallSeg) {
             uint64_t v[kSmallSeg];
 #pragma unroll
@@ -1316,13 +1413,13 @@ __global__ __launch_bounds__(256) void kSortDecode(const uint64_t* __restrict__ 
             }
 #pragma unroll
             for (uint32_t i = 0; i < kSmallSeg; ++i)
-                if (i < n) out[b + i] = decodeKey(v[i], qidBase + q, starts, nrec);
+                if (i < n) out[b + i] = decode(v[i], qidBase + q);
         }
         uint64_t med = __ballot(n > kSmallSeg && n <= kMediumSeg);
         while (med) {
             const int src = __ffsll((long long)med) - 1;
             med &= med - 1;
-            const uint32_t sq = (uint32_t)__shfl((int)q, src), sn = (uint32_t)__shfl((int)n, src);
+            const uint32_t sqid = (uint32_t)__shfl((int)q, src), sn = (uint32_t)__shfl((int)n, src);
             const uint64_t sb = __shfl(b, src);
             uint64_t v = lane < sn ? keys[sb + lane] : ~0ull;
 #pragma unroll
@@ -1334,7 +1431,7 @@ __global__ __launch_bounds__(256) void kSortDecode(const uint64_t* __restrict__ 
                     v = keepMin ? (v < o ? v : o) : (v < o ? o : v);
                 }
             }
-            if (lane < sn) out[sb + lane] = decodeKey(v, qidBase + sq, starts, nrec);
+            if (lane < sn) out[sb + lane] = decode(v, qidBase + sqid);
         }
     }
 }
@@ -1803,12 +1900,12 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
     SH_HIP(hipGetLastError());
 }
 
-void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
-                   uint32_t* big, uint32_t* nbig, hipStream_t st) {
+void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* rank, uint32_t nq, uint64_t* qoff,
+                   uint64_t* partial, uint32_t* big, uint32_t* nbig, hipStream_t st) {
     // qcnt[nq] stays 0, so qoff[nq] = total rows
     if (nhits) {
         const uint64_t blocks = std::min<uint64_t>((nhits + 255) / 256, 65536);
-        hipLaunchKernelGGL(kCountRows, dim3((unsigned)blocks), dim3(256), 0, st, hits, nhits, qcnt);
+        hipLaunchKernelGGL(kCountRows, dim3((unsigned)blocks), dim3(256), 0, st, hits, nhits, qcnt, rank);
         SH_HIP(hipGetLastError());
     }
     const uint32_t n = nq + 1, tiles = (n + kScanTile - 1) / kScanTile;
