@@ -238,16 +238,7 @@ def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch, wide)
             assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (k, verify, locate_sa)
 
 
-@pytest.mark.parametrize("batch,resolve", [("97", "2"), ("97", "1"), ("97", "0"), ("1000000", "2")])
-def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch, resolve):
-    """Per-query segments of every length: reads from a 40-fold repeated unit
-    have > 8 located rows (segmented radix sort), unique reads 1-2 (register
-    sort), random reads none. SAHARA_BATCH=97 runs many batches through the
-    three-stream pipeline, with the per-query counters reused between them.
-    SAHARA_RESOLVE: text tasks' SA rows resolved inside the text kernel (2) or
-    by kResolveTasks on the FM stream (1) / the text stream (0)."""
-    monkeypatch.setenv("SAHARA_BATCH", batch)
-    monkeypatch.setenv("SAHARA_RESOLVE", resolve)
+def _repeat_case():
     rng = np.random.default_rng(5)
     unit = random_records(rng, [400], 6)[0]
     parts = []
@@ -262,6 +253,42 @@ def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch, r
     pats = sa.interleave_rc(reads, 6)
     sch = sa.search_scheme("h2-k2", 0, k, m)
     want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch, nthreads=8)[0])
+    return recs, pats, sch, want
+
+
+def test_sort_decode_tile_holds_every_tier(gpu_device):
+    """kSortDecode (search.hip) stages the rows of 256 consecutive queries in
+    LDS when they fit its 1024-key tile. Here one such range mixes queries
+    without hits with register-sorted (<= 8 rows), wave-sorted (9-64) and
+    radix-sorted (> 64) segments, in shuffled order; the range before it holds
+    > 1024 rows and takes the global-memory path."""
+    recs, pats, sch, want = _repeat_case()
+    per_q = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
+    rng = np.random.default_rng(9)
+    pick = [np.flatnonzero(sel)[:n] for sel, n in (((per_q >= 1) & (per_q <= 8), 40), ((per_q > 8) & (per_q <= 64), 4),
+                                                   ((per_q > 64) & (per_q <= 300), 1), (per_q == 0, 60))]
+    assert all(len(p) for p in pick)
+    tile = rng.permutation(np.concatenate(pick))
+    assert per_q[tile].sum() <= 1024 and per_q[:256].sum() > 1024
+    pats2 = np.vstack([pats[:256], pats[tile]])
+    want2 = hits_as_rows(O.Index.build(recs, 6, 16).search(pats2, sch, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    for verify, locate_sa in MODES:
+        gpu.set_mode(verify, locate_sa)
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats2, sch)), want2), (verify, locate_sa)
+
+
+@pytest.mark.parametrize("batch,resolve", [("97", "2"), ("97", "1"), ("97", "0"), ("1000000", "2")])
+def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch, resolve):
+    """Per-query segments of every length: reads from a 40-fold repeated unit
+    have > 8 located rows (segmented radix sort), unique reads 1-2 (register
+    sort), random reads none. SAHARA_BATCH=97 runs many batches through the
+    three-stream pipeline, with the per-query counters reused between them.
+    SAHARA_RESOLVE: text tasks' SA rows resolved inside the text kernel (2) or
+    by kResolveTasks on the FM stream (1) / the text stream (0)."""
+    monkeypatch.setenv("SAHARA_BATCH", batch)
+    monkeypatch.setenv("SAHARA_RESOLVE", resolve)
+    recs, pats, sch, want = _repeat_case()
     per_q = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
     assert per_q.max() > 8 and ((per_q >= 1) & (per_q <= 8)).any() and (per_q == 0).any()
     gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)

@@ -11,6 +11,6 @@ for i in $(seq 1 "$N"); do
   for cfg in "${CFGS[@]}"; do
     env $cfg timeout -k 10 300 python3 "$R/bench.py" --no-cpu --no-count --no-e2e --no-verify --no-ref-path "$@" \
         > "$R/gpurun_out/ab.json" 2> "$R/gpurun_out/ab.log" || { echo "FAIL $cfg"; tail -3 "$R/gpurun_out/ab.log"; exit 1; }
-    python3 -c "import json,sys; d=json.load(open('$R/gpurun_out/ab.json')); print(repr(sys.argv[1]), round(d['value']/1e6,1), d['ms_per_step'])" "$cfg"
+    python3 -c "import json,sys; d=json.load(open('$R/gpurun_out/ab.json')); c=d['config']; print(repr(sys.argv[1]), round(d['value']/1e6,1), d['ms_per_step'], {k: c.get(k) for k in ('text_ms','search_ms','seed_ms','locate_ms','sort_ms')})" "$cfg"
   done
 done
