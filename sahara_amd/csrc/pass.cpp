@@ -143,16 +143,20 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const int fullBpc = searchBlocksPerCU(sigma, c->edit, lds);
     int bpc = fullBpc;
     // Overlapped with the text phase of the previous batch, the FM phase
-    // (memory-latency bound) runs two workgroups per CU beside three text
+    // (memory-latency bound) runs one workgroup per CU beside three text
     // workgroups; alone it takes all that fit. (Measured at C3 with pruned
-    // text steps: text 3 + FM 2 846-873M reads/s, text 4 + FM 1 845-847M.)
+    // text steps: text 3 + FM 2 846-873M reads/s, text 4 + FM 1 845-847M;
+    // after the atomic-free locate chain, text 3 + FM 1 917-957M against
+    // text 3 + FM 2 883-905M and FM 3 847-890M, alternating runs on one box:
+    // 115-131 VGPRs per FM wave leave the SIMDs' registers to the text waves
+    // and the locate chain.)
     // patterns per batch: 4M, fewer for schemes with many searches (work
     // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (const char* e = std::getenv("SAHARA_BATCH"))
         maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
     const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
-    if (!serial && batchesHere > 1 && c->verify) bpc = 2;
+    if (!serial && batchesHere > 1 && c->verify) bpc = 1;
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
     const uint32_t blocks = (uint32_t)(c->numCU * bpc);
     // the first batch's FM phase has nothing to overlap with: full occupancy
