@@ -346,7 +346,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // the batches before it search; unpacked on sD ahead of its seeds)
         ensureUploaded(c, bstart[b + 1], sD);
         SH_HIP(hipEventRecord(sl.fmStart, sD));
-        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sD);
+        // (SAHARA_SEED_BPC: workgroups per CU of the seeds after the first batch's)
+        uint32_t seedBpc = 8;
+        if (const char* e = std::getenv("SAHARA_SEED_BPC"); e && b > 0) seedBpc = (uint32_t)std::max(1, std::min(8, std::atoi(e)));
+        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * seedBpc), sD);
         if (early && b == 0)  // the seed tasks end here: the text phase may start on them
             SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
         SH_HIP(hipEventRecord(sl.seedDone, sD));
