@@ -231,9 +231,9 @@ struct Ctx {
     uint32_t textSteps = 4;               // text-phase micro-steps per lane per wave iteration
     uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
 
-    // work buffers. Batches rotate over three slots so that the FM phase runs
-    // up to two batches ahead (stream `st`) of the text phase (stream `stB`),
-    // while batch i-1 runs its locate and sort (stream `stC`).
+    // work buffers. Batches rotate over kSlots slots so that seeds and the FM
+    // phase run batches ahead (streams `stD`, `st`) of the text phase (stream
+    // `stB`), while earlier batches run their locate and sort (stream `stC`).
     static constexpr int kSlots = 5;
     struct Slot {
         DevBuf<uint4> hits, tasks, seeds;  // seeds: starting cursors (kSeedItems -> kSearchFM)

@@ -12,16 +12,19 @@
 namespace sahara {
 
 // One pass over the staged patterns in batches of <= 4M. Per batch:
-//   stream st : kSeedItems, kSearchFM        -> hits, tasks of its slot
-//   stream stB: kResolveTasks, kSearchText   -> hits of its slot
-//   stream stC: row offsets, locate, sort, decode
-// Three slots rotate, so the FM phase of batches i+1, i+2 (memory-latency
-// bound) overlaps the text phase of batch i (ALU bound), and both phases run
-// back to back while locate and sort of batch i-1 fill the gaps on stream
-// stC. Host order: finish(i-3), FM(i), text(i) — FM(i) reuses the slot that
-// locate(i-3) frees. Buffer overflow is detected
-// after the fact from each batch's flags; the whole pass is then redone on one
-// stream with grown buffers (`serial`), re-running a batch until it fits.
+//   stream stD: chunk unpack (streamed upload), kSeedItems
+//   stream st : kSearchFM                    -> hits, tasks of its slot
+//   stream stB: kSearchText                  -> hits of its slot
+//   stream stC: row counts + ranks, scan, locate, sort, decode
+//   stream stF: the batch's hits to the host sink (streamed calls)
+// Ctx::kSlots slots rotate, so the seeds and FM phase of later batches
+// (memory-latency bound) overlap the text phase of batch i (ALU bound), the
+// text phases run back to back, and locate and sort of batch i-1 fill the
+// gaps on stream stC. The issuing thread runs seeds, FM(i), text(i) as soon as
+// slot i % kSlots is free; the finisher thread runs finish(i) (locate, sort,
+// download), which frees it. Buffer overflow is detected after the fact from
+// each batch's flags; the whole pass is then redone on one stream with grown
+// buffers (`serial`), re-running a batch until it fits.
 void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
 
 void runOne(Ctx* c, bool count);

@@ -209,6 +209,26 @@ def test_medium_scale_parity(gpu_device, k, m, nreads, ref_len):
     assert found.all()
 
 
+@pytest.mark.parametrize("nrec", [256, 257, 700])
+def test_decode_over_many_records(gpu_device, nrec):
+    """Hits decoded to (seq_id, pos) over texts of many short records: the
+    record starts sit in LDS for <= 256 records (kSortDecode) and are searched
+    in global memory above that."""
+    rng = np.random.default_rng(nrec)
+    recs = random_records(rng, list(rng.integers(30, 160, size=nrec)), 6)
+    m, k = 30, 2
+    reads = mutate_reads(rng, recs, 3000, m, k)
+    pats = sa.interleave_rc(reads, 6)
+    sch = sa.search_scheme("h2-k2", 0, k, m)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch, nthreads=8)[0])
+    assert len(np.unique(want[:, 1])) > nrec // 2
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    assert gpu.info()["n_records"] == nrec
+    for verify, locate_sa in MODES:
+        gpu.set_mode(verify, locate_sa)
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
+
+
 @pytest.mark.parametrize("wide", [False, True])
 def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch, wide):
     """Occurrences that touch position 0, the last symbol of the text and
