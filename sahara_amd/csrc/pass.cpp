@@ -197,9 +197,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
         tbpc = textBlocksPerCU(sigma, c->edit, packedStack, textLds);
-    // overlapped with the FM phase, three text workgroups per CU leave room
-    // for two FM workgroups beside them (the FM chain of seeds and FM launches
-    // is the other critical path once the text phase prunes dead children)
+    // overlapped with the FM phase, three text workgroups per CU beside its one
+    // (four would fit: r2 v8 measured text 4 against 3 in alternating pairs,
+    // C3 914-943M vs 880-952M on one box and 873-914M vs 953-956M on another,
+    // C2 950-1013M vs 956-1026M: the sign flips with the box)
     if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
     if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, packedStack, textLds), std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
