@@ -237,7 +237,9 @@ def main():
         # algorithmic bytes per step: FM = 64-B Occ lines touched
         # + pattern bytes; text = per task its window, packed pattern, task
         # record and SA entry; locate = one SA read per FM-located row
-        search_bytes = 64.0 * cnt["ext_lines"] + pats.size
+        # (the FM kernel reads each pattern as 4-bit words: patWords u32 per
+        # pattern, capi staging, not one byte per symbol)
+        search_bytes = 64.0 * cnt["ext_lines"] + pats.shape[0] * ((rlen + 7) // 8) * 4.0
         # per text task: its window and pattern as 16-B blocks of 32 symbols
         # (3 bit planes; capi.cpp winBlocks / patBlocks), the task record, the SA entry
         win_blocks = (rlen + 2 * k + 62) // 32
@@ -341,11 +343,13 @@ def main():
         # (sahara_gpu_search_reads: what `sahara search` calls)
         extra["pcie_inclusive"] = pcie_inclusive(
             lambda: sa.search_reads(idx, reads, scheme, edit=edit), idx, nreads, args.steps, w2, world, barrier, nh,
+            digest,
             "sahara_gpu_search_reads from host reads: streamed upload (four symbols per byte, N listed) + device RC interleave, "
             "search, locate, sort, hits D2H batch by batch into pinned host memory recycled through sahara_gpu_free")
         # the interleaved patterns cross PCIe (the reference's queries vector, sahara_gpu_search)
         extra["pcie_inclusive_patterns"] = pcie_inclusive(
             lambda: sa.search(idx, pats, scheme, edit=edit), idx, nreads, args.steps, w2, world, barrier, nh,
+            digest,
             "sahara_gpu_search from host patterns (reads + RC interleaved on the host): streamed upload, search, "
             "locate, sort, hits D2H batch by batch into pinned host memory")
     # the reference's execution model timed on the same reads (north_star's
@@ -570,10 +574,35 @@ def verify_index_part(idx, flat, lens, torch, dev, W=21):
     return out
 
 
-def pcie_inclusive(search, idx, nreads, steps, warmup, world, barrier, local_hits, path):
+def hits_digest(h):
+    """Host restatement of search.hip kDigest (order-independent sum of a
+    64-bit mix per record) over a HIT_DTYPE array."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+    def mix64(x):
+        x = x ^ (x >> np.uint64(30))
+        x = x * np.uint64(0xbf58476d1ce4e5b9)
+        x = x ^ (x >> np.uint64(27))
+        x = x * np.uint64(0x94d049bb133111eb)
+        return x ^ (x >> np.uint64(31))
+
+    acc = 0
+    with np.errstate(over="ignore"):
+        for s in range(0, len(h), 1 << 24):
+            b = h[s:s + (1 << 24)]
+            inner = mix64((b["seq_id"].astype(np.uint64) << np.uint64(40)) ^ (b["pos"] << np.uint64(4)) ^
+                          b["err"].astype(np.uint64))
+            v = mix64((b["qid"] * np.uint64(0x9E3779B97F4A7C15)) ^ inner)
+            acc = (acc + int(v.sum(dtype=np.uint64))) & int(M)
+    return acc
+
+
+def pcie_inclusive(search, idx, nreads, steps, warmup, world, barrier, local_hits, local_digest, path):
     """`search()` from host ranks to located hits in host memory (SURVEY §8(d)'s
     search wall time), timed over `steps` calls after `warmup` calls. Each
-    call's hit buffer is released (sahara_gpu_free) before the next."""
+    call's hit buffer is released (sahara_gpu_free) before the next, except
+    the last one's, whose content is checked (after the timing) against the
+    device-resident pass's digest."""
     n = 0
     for _ in range(warmup):
         h = search()
@@ -582,20 +611,24 @@ def pcie_inclusive(search, idx, nreads, steps, warmup, world, barrier, local_hit
     barrier()
     t0 = time.perf_counter()
     acc = {"stage_ms": 0.0, "total_ms": 0.0, "output_ms": 0.0}
+    h = None
     for _ in range(steps):
+        h = None
         h = search()
         st = idx.stats()
         for kk in acc:
             acc[kk] += st[kk]
         n = len(h)
-        del h
     barrier()
     el = time.perf_counter() - t0
+    same_digest = hits_digest(h) == local_digest
+    del h
     if world > 1:
         from sahara_amd.dist import max_over_ranks
         el = max_over_ranks(el, device="cuda")
     return {"reads_per_s": round(nreads * world * steps / el, 1), "ms_per_step": round(el * 1e3 / steps, 2),
-            "steps": steps, "warmup": warmup, "hits": int(n), "same_hits": int(n) == int(local_hits),
+            "steps": steps, "warmup": warmup, "hits": int(n),
+            "same_hits": int(n) == int(local_hits) and same_digest,
             "stage_ms": round(acc["stage_ms"] / steps, 2), "search_ms": round(acc["total_ms"] / steps, 2),
             "output_ms": round(acc["output_ms"] / steps, 2),
             "upload_chunks_2_4_8_bits": list(idx.stats()["upload_chunks"]), "path": path}

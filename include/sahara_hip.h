@@ -181,6 +181,12 @@ int  sahara_gpu_copy_hits(void* ctx, void* dst_device, uint64_t capacity, uint64
  * each record) computed on the device. */
 int  sahara_gpu_digest(void* ctx, uint64_t* digest);
 int  sahara_gpu_stats(void* ctx, sahara_stats* stats);
+/* Where a context runs: the HIP device it opened (SAHARA_DEVICE_MAP may remap
+ * the device argument of sahara_gpu_open / _build, a test hook), the NUMA node
+ * of that device (-1 unknown) and the number of host CPUs of that node the
+ * context's own threads (packing pool, finisher, hit expander) are bound to
+ * (0: not bound; SAHARA_NUMA=0 turns binding off). Any pointer may be NULL. */
+int  sahara_gpu_placement(void* ctx, int* device, int* numa_node, int* n_cpus);
 
 /* Releases a hit buffer returned by sahara_gpu_search / sahara_gpu_search_best.
  * Large buffers (>= 64 MB) are page-locked host memory; freeing one hands it

@@ -101,6 +101,7 @@ EXPORTED = {
     "sahara_gpu_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "sahara_gpu_copy_hits": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "sahara_gpu_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "sahara_gpu_placement": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "sahara_gpu_free": (None, [C.c_void_p]),
     "sahara_gpu_close": (None, [C.c_void_p]),
     "sahara_scheme_generators": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int]),
@@ -289,6 +290,12 @@ class BiFMIndex:
         d = C.c_uint64()
         _check(lib().sahara_gpu_digest(self._h, C.byref(d)))
         return d.value
+
+    def placement(self):
+        """(HIP device, NUMA node or -1, CPUs the context's threads are bound to)."""
+        d, node, ncpu = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().sahara_gpu_placement(self._h, C.byref(d), C.byref(node), C.byref(ncpu)))
+        return {"device": d.value, "numa_node": node.value, "n_cpus": ncpu.value}
 
     def stats(self):
         s = Stats()

@@ -427,7 +427,7 @@ int cmdSearch(int argc, char** argv) {
 
     std::vector<Scheme> schemes;  // all: [0..k]; besthits: one per exact error count j
     // --dynamic_generator: part sizes by weighted node count (search.cpp:192-195, 202-205)
-    auto build = [&](int minK, int maxK, bool hamming) {
+    auto build = [&](int minK, int maxK, bool hamming, bool printPartition) {
         if (!dyn.given) return makeScheme(gen.value, minK, maxK, len, hamming);
         Scheme s;
         const int n = sahara_scheme_dynamic(gen.value.c_str(), minK, maxK, len, 0, edit ? 1 : 0, (int)sigma,
@@ -441,14 +441,17 @@ int cmdSearch(int argc, char** argv) {
         if (sahara_scheme_dynamic(gen.value.c_str(), minK, maxK, len, hamming ? 1 : 0, edit ? 1 : 0, (int)sigma,
                                   (double)info.n, sizes.data(), 64, s.pi.data(), s.l.data(), s.u.data(), n) != n)
             throw CliError("cannot expand search scheme " + gen.value + " to length " + std::to_string(len));
-        int P = 0;
-        sahara_scheme_parts(gen.value.c_str(), minK, maxK, &P, nullptr, nullptr, nullptr, 0);
-        std::string part = "[";
-        for (int t = 0; t < P; ++t) part += (t ? ", " : "") + std::to_string(sizes[t]);
-        std::printf("partition: %s]\n", part.c_str());
+        if (printPartition) {
+            int P = 0;
+            sahara_scheme_parts(gen.value.c_str(), minK, maxK, &P, nullptr, nullptr, nullptr, 0);
+            std::string part = "[";
+            for (int t = 0; t < P; ++t) part += (t ? ", " : "") + std::to_string(sizes[t]);
+            std::printf("partition: %s]\n", part.c_str());
+        }
         return s;
     };
-    // each scheme's node counts right after it, as loadSearchScheme prints them (search.cpp:186-212)
+    // each scheme's node counts right after it, as loadSearchScheme prints them
+    // (search.cpp:186-212): on the expanded scheme, before limitToHamming
     auto add = [&](Scheme sch) {
         double nc = 0, wnc = 0;
         sahara_scheme_counts(sch.l.data(), sch.u.data(), sch.n, len, edit ? 1 : 0, (int)sigma, (double)info.n, &nc,
@@ -457,9 +460,13 @@ int cmdSearch(int argc, char** argv) {
         std::printf("weighted node count: %s\n", shortest(wnc).c_str());
         schemes.push_back(std::move(sch));
     };
-    if (!besthits) add(build(0, k, !edit));
-    else
-        for (int j = 0; j <= k; ++j) add(build(j, j, false));
+    if (!besthits) {
+        add(build(0, k, false, true));
+        // -d ham: the search runs on limitToHamming of that scheme (search.cpp:226)
+        if (!edit) schemes.back() = build(0, k, true, false);
+    } else {
+        for (int j = 0; j <= k; ++j) add(build(j, j, false, true));
+    }
     timing.emplace_back("searchScheme", sw.reset());
 
     // search + locate (search.cpp:218-250), reads sharded over the devices

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -76,16 +77,93 @@ void handOver(const std::vector<sahara_hit>& v, sahara_hit** hits, uint64_t* n_h
     *n_hits = v.size();
 }
 
+// SAHARA_DEVICE_MAP=a,b,c (test hook): context device d opens HIP device
+// list[d], so that `sahara search --gpus N` and concurrent contexts run their
+// multi-device code path on one GPU (tests/test_multi_device.py)
+static int mapDevice(int device) {
+    const char* e = std::getenv("SAHARA_DEVICE_MAP");
+    if (!e || !*e) return device;
+    std::vector<int> map;
+    for (const char* p = e; *p;) {
+        char* end = nullptr;
+        const long v = std::strtol(p, &end, 10);
+        if (end == p) throw Error(std::string("SAHARA_DEVICE_MAP: not a list of device numbers: ") + e);
+        map.push_back((int)v);
+        p = *end == ',' ? end + 1 : end;
+        if (*end && *end != ',') throw Error(std::string("SAHARA_DEVICE_MAP: not a list of device numbers: ") + e);
+    }
+    if (device < 0 || (size_t)device >= map.size())
+        throw Error("SAHARA_DEVICE_MAP has no entry for device " + std::to_string(device));
+    return map[(size_t)device];
+}
+
+// The CPUs of the device's NUMA node that this process may run on (Placement).
+static void placeNear(Ctx* c) {
+    const char* e = std::getenv("SAHARA_NUMA");
+    if (e && std::atoi(e) == 0) return;
+    char bdf[64] = {0};
+    if (hipDeviceGetPCIBusId(bdf, sizeof(bdf), c->device) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    std::string id(bdf);
+    for (char& ch : id) ch = (char)std::tolower((unsigned char)ch);
+    int node = -1;
+    if (std::FILE* f = std::fopen(("/sys/bus/pci/devices/" + id + "/numa_node").c_str(), "r")) {
+        if (std::fscanf(f, "%d", &node) != 1) node = -1;
+        std::fclose(f);
+    }
+    c->place.node = node;
+    if (node < 0) return;
+    std::FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+    if (!f) return;
+    char buf[8192] = {0};
+    const size_t got = std::fread(buf, 1, sizeof(buf) - 1, f);
+    std::fclose(f);
+    buf[got] = 0;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (const char* p = buf; *p && *p != '\n';) {  // "0-15,64-79"
+        char* end = nullptr;
+        const long a = std::strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        if (*end == '-') b = std::strtol(end + 1, &end, 10);
+        for (long i = a; i <= b && i < CPU_SETSIZE; ++i)
+            if (CPU_ISSET(i, &allowed)) CPU_SET(i, &set);
+        p = *end == ',' ? end + 1 : end;
+    }
+    c->place.cpus = set;
+    c->place.ncpus = CPU_COUNT(&set);
+}
+
+// host threads a context uses for one job: its node's allowed CPUs (or the
+// process's), at most cap
+unsigned hostThreads(const Ctx* c, unsigned cap) {
+    unsigned n = (unsigned)c->place.ncpus;
+    if (n == 0) {
+        cpu_set_t s;
+        CPU_ZERO(&s);
+        n = sched_getaffinity(0, sizeof(s), &s) == 0 ? (unsigned)CPU_COUNT(&s) : std::thread::hardware_concurrency();
+    }
+    return std::max(1u, std::min(cap, n));
+}
+
 Ctx* newCtx(int device) {
     int n = 0;
     SH_HIP(hipGetDeviceCount(&n));
-    if (device < 0 || device >= n)
-        throw Error("no HIP device " + std::to_string(device) + " (found " + std::to_string(n) + ")");
-    SH_HIP(hipSetDevice(device));
+    const int hipDev = mapDevice(device);
+    if (hipDev < 0 || hipDev >= n)
+        throw Error("no HIP device " + std::to_string(hipDev) + " (found " + std::to_string(n) + ")");
+    SH_HIP(hipSetDevice(hipDev));
     auto c = std::make_unique<Ctx>();
-    c->device = device;
+    c->device = hipDev;
+    placeNear(c.get());
     hipDeviceProp_t prop;
-    SH_HIP(hipGetDeviceProperties(&prop, device));
+    SH_HIP(hipGetDeviceProperties(&prop, hipDev));
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
@@ -101,6 +179,7 @@ Ctx* newCtx(int device) {
     // loads the index (pinning 256 MB takes ~50 ms)
     Ctx* raw = c.get();
     raw->ringInit = std::thread([raw] {
+        raw->place.bind();  // pinned pages first touched on the device's node
         (void)hipSetDevice(raw->device);
         if (hipHostMalloc(reinterpret_cast<void**>(&raw->ring), Ctx::kRingSlots * Ctx::kRingSlot, hipHostMallocPortable) !=
             hipSuccess) {
@@ -112,7 +191,8 @@ Ctx* newCtx(int device) {
             raw->downRing = nullptr;  // no compact download: hits go to a pinned sink whole
     });
     for (auto& sl : c->slot) {
-        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmDone, &sl.textStart, &sl.textDone, &sl.free})
+        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmBegin, &sl.fmDone, &sl.textStart, &sl.textMid0,
+                              &sl.textMid1, &sl.textDone, &sl.free})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);
         sl.queues.reserve(768);
@@ -198,7 +278,7 @@ int sahara_gpu_open(int device, const void* idx_image, size_t idx_bytes, void** 
 
 int sahara_gpu_open_file(int device, const char* path, void** ctx) {
     return guarded([&] {
-        std::vector<uint8_t> buf = readFile(path);
+        const std::vector<uint8_t> buf = readFile(path);
         *ctx = openImage(device, buf.data(), buf.size());
     });
 }
@@ -358,6 +438,15 @@ int sahara_gpu_digest(void* ctx, uint64_t* digest) {
         SH_HIP(hipMemcpyAsync(&d, c->counters.ptr + 4, 8, hipMemcpyDeviceToHost, c->st));
         SH_HIP(hipStreamSynchronize(c->st));
         *digest = d;
+    });
+}
+
+int sahara_gpu_placement(void* ctx, int* device, int* numa_node, int* n_cpus) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (device) *device = c->device;
+        if (numa_node) *numa_node = c->place.node;
+        if (n_cpus) *n_cpus = c->place.ncpus;
     });
 }
 
@@ -543,7 +632,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         }
         if (c->compactSink) {
             if (!c->expander)
-                c->expander = std::make_unique<Expander>(c->device, std::max(1u, std::min(8u, std::thread::hardware_concurrency())) - 1);
+                c->expander = std::make_unique<Expander>(c->device, hostThreads(c, 8) - 1, &c->place);
             c->expander->setStarts(&c->I.recStarts);
             c->expander->mark = [c](const char* w, uint64_t i) { c->mark(w, i); };
             c->expander->reset();

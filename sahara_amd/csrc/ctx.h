@@ -3,6 +3,8 @@
 // (pass.cpp) share.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <atomic>
 #include <chrono>
@@ -23,13 +25,34 @@ namespace sahara {
 
 extern thread_local std::string g_err;  // sahara_gpu_last_error
 
+// NUMA placement of a context's own host threads (the packing pool, the
+// pass's finisher, the hit expander, the ring pinning): the CPUs of the NUMA
+// node the GPU hangs off (/sys/bus/pci/devices/<bdf>/numa_node), as far as
+// the process may use them. The streamed path is host-memory-bandwidth bound
+// (DESIGN.md §3.6, §5); with 8 GPUs each context's packing must read its
+// reads from, and write its pinned ring in, the node next to its GPU.
+// node = -1 (unknown, or SAHARA_NUMA=0): threads stay where the OS puts them.
+struct Placement {
+    int node = -1;
+    int ncpus = 0;      // CPUs the context's threads are bound to (0: not bound)
+    cpu_set_t cpus;
+    Placement() { CPU_ZERO(&cpus); }
+    void bind() const {
+        if (ncpus > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus), &cpus);
+    }
+};
+
 // Host worker threads of a context (pattern packing for the upload), started
 // once: a streamed upload packs several chunks per call, and fresh threads per
 // chunk measured slower than the link.
 class HostPool {
 public:
-    explicit HostPool(unsigned workers) {
-        for (unsigned i = 1; i <= workers; ++i) ts_.emplace_back([this, i] { loop(i); });
+    explicit HostPool(unsigned workers, const Placement* pl = nullptr) {
+        for (unsigned i = 1; i <= workers; ++i)
+            ts_.emplace_back([this, i, pl] {
+                if (pl) pl->bind();
+                loop(i);
+            });
     }
     ~HostPool() {
         {
@@ -95,8 +118,11 @@ public:
         sahara_hit* dst;
         uint64_t n, q0;          // records; the batch's first qid
     };
-    Expander(int device, unsigned workers) : device_(device), pool_(workers) {
-        th_ = std::thread([this] { loop(); });
+    Expander(int device, unsigned workers, const Placement* pl) : device_(device), pool_(workers, pl) {
+        th_ = std::thread([this, pl] {
+            if (pl) pl->bind();
+            loop();
+        });
     }
     ~Expander() {
         {
@@ -202,6 +228,7 @@ private:
 
 struct Ctx {
     int device = 0;
+    Placement place;                      // NUMA node of the device; the context's threads run there
     hipStream_t st = nullptr;
     int numCU = 0;
     DeviceIndex I;
@@ -214,6 +241,7 @@ struct Ctx {
     std::vector<uint64_t> partRec0{0};
     uint32_t exportPart = 0;
     DevBuf<sahara_hit> outAll;            // multi-part: hits of the parts so far
+    MergeBufs merge;                      // multi-part: sort keys of the merge by qid
 
     // staged inputs
     DevBuf<uint32_t> pats;                // 4-bit packed patterns, patWords per pattern (FM phase)
@@ -240,8 +268,13 @@ struct Ctx {
         DevBuf<uint32_t> seedItem;
         DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
         DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512), [512, 768)
-        hipEvent_t fmStart = nullptr, seedDone = nullptr, fmDone = nullptr, textStart = nullptr, textDone = nullptr,
-                   free = nullptr;
+        // kernel spans, each recorded on the kernel's own stream right around
+        // its launch(es): seeds fmStart..seedDone (sD), FM fmBegin..fmDone
+        // (sA), text textStart..textDone, or for the first batch's two text
+        // launches textStart..textMid0 and textMid1..textDone (sB)
+        hipEvent_t fmStart = nullptr, seedDone = nullptr, fmBegin = nullptr, fmDone = nullptr, textStart = nullptr,
+                   textMid0 = nullptr, textMid1 = nullptr, textDone = nullptr, free = nullptr;
+        bool twoText = false;
     } slot[kSlots];
     hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
     uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
@@ -331,19 +364,22 @@ struct Ctx {
     }
 
     ~Ctx() {
+        // the pinning thread assigns ring and downRing: it must be done before
+        // either is read (a context closed or failed right after newCtx)
+        if (ringInit.joinable()) ringInit.join();
         expander.reset();
         for (hipEvent_t e : downEv) (void)hipEventDestroy(e);
         if (downRing) (void)hipHostFree(downRing);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
-        if (ringInit.joinable()) ringInit.join();
         for (auto& e : ringEv)
             if (e) (void)hipEventDestroy(e);
         if (ring) (void)hipHostFree(ring);
         if (stE) (void)hipStreamDestroy(stE);
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
-            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmDone, sl.textStart, sl.textDone, sl.free})
+            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
+                                 sl.textMid1, sl.textDone, sl.free})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
         if (nibHost) (void)hipHostFree(nibHost);
@@ -373,6 +409,7 @@ bool hitLess(const sahara_hit& a, const sahara_hit& b);
 void limitHits(std::vector<sahara_hit>& v, uint32_t n);
 void handOver(const std::vector<sahara_hit>& v, sahara_hit** hits, uint64_t* n_hits);
 Ctx* newCtx(int device);
+unsigned hostThreads(const Ctx* c, unsigned cap);
 Ctx* ctxOf(void* p);
 HostPool& hostPool(Ctx* c);
 

@@ -55,8 +55,10 @@ IdxParts parseIdx(const uint8_t* buf, size_t bytes) {
     P.rate = (uint32_t)r.get<uint64_t>();
     P.bwtF = r.vec<uint8_t>(nf);
     P.bwtR = r.vec<uint8_t>(nr);
-    // the u64/u32 vectors are 8/4-aligned only if the preceding byte vectors
-    // keep alignment; copy-free access requires it, so check
+    // the u64/u32 vectors follow the n-byte BWTs, so they are in general NOT
+    // 8/4-aligned in the image (nor is a part of a multi-part file): treat
+    // sampled / samples as raw bytes — they are only ever memcpy'd / copied to
+    // the device (buildFromParts, cpuParts), never dereferenced as typed
     P.sampled = r.vec<uint64_t>(ns);
     P.samples = r.vec<uint32_t>(P.nsamples);
     if (nf != P.n || nr != P.n || ns != P.n / 64 + 1) throw Error("inconsistent .idx payload sizes");

@@ -89,7 +89,7 @@ void run(Ctx* c, bool count) {
             c->out.release();
             c->out.reserve(std::max<uint64_t>(total, 1024));
         }
-        sortHitsByQid(c->outAll.ptr, total, c->out.ptr, c->tmp, c->st);
+        sortHitsByQid(c->outAll.ptr, total, c->npat, c->out.ptr, c->merge, c->tmp, c->st);
         SH_HIP(hipStreamSynchronize(c->st));
     } catch (...) {
         c->sink = sink;
@@ -358,6 +358,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
         SH_HIP(hipEventRecord(sl.seedDone, sD));
         SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
+        SH_HIP(hipEventRecord(sl.fmBegin, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
         if (split && resolveMode == 1)
             launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sA);
@@ -370,6 +371,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         const bool split0 = early && b == 0;
         SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone : sl.fmDone, 0));
         SH_HIP(hipEventRecord(sl.textStart, sB));
+        sl.twoText = split && split0;
         if (split) {
             TextArgs t{};
             t.sa = c->I.saFull.ptr;
@@ -410,7 +412,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                 // tasks the FM phase appended after them
                 t.taskCount = sl.small.ptr + 5;
                 launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+                SH_HIP(hipEventRecord(sl.textMid0, sB));
                 SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+                SH_HIP(hipEventRecord(sl.textMid1, sB));
                 t.taskBegin = sl.small.ptr + 5;
                 t.taskCount = sl.small.ptr + 4;
                 t.work = sl.queues.ptr + 512;
@@ -441,9 +445,15 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         float ms = 0;
         SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
         S.seed_ms += ms;
-        SH_HIP(hipEventElapsedTime(&ms, sl.seedDone, sl.fmDone));
+        SH_HIP(hipEventElapsedTime(&ms, sl.fmBegin, sl.fmDone));
         S.search_ms += ms;
-        SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+        if (sl.twoText) {  // the two launches only, not the wait for the FM phase between them
+            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMid0));
+            S.text_ms += ms;
+            SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textDone));
+        } else {
+            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+        }
         S.text_ms += ms;
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
         if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
@@ -570,6 +580,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         bool stop = false;
         std::exception_ptr finErr;
         std::thread finisher([&] {
+            c->place.bind();
             try {
                 SH_HIP(hipSetDevice(c->device));
                 bool pending = false;  // finishCheck owed for batch `owed`

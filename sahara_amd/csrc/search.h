@@ -128,7 +128,13 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst
 void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream_t st);
 void launchOffsetSeq(const sahara_hit* in, uint64_t n, uint64_t rec0, sahara_hit* out, hipStream_t st);
-void sortHitsByQid(const sahara_hit* in, uint64_t n, sahara_hit* out, DevBuf<char>& tmp, hipStream_t st);
+// key / index buffers of the multi-part merge (kept by the context)
+struct MergeBufs {
+    DevBuf<uint64_t> k0, k1;
+    DevBuf<uint32_t> v0, v1;
+};
+void sortHitsByQid(const sahara_hit* in, uint64_t n, uint64_t nqid, sahara_hit* out, MergeBufs& B, DevBuf<char>& tmp,
+                   hipStream_t st);
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
                        hipStream_t st);
 void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,

@@ -1696,24 +1696,27 @@ __global__ void kGatherHits(const sahara_hit* __restrict__ in, const uint32_t* _
 
 // Stable sort of hit records by qid (rocPRIM's LSD radix sort is stable):
 // the parts' hits, each part in canonical order and every part's records
-// after the previous part's, come out in canonical (qid, seq_id, pos, err) order.
-void sortHitsByQid(const sahara_hit* in, uint64_t n, sahara_hit* out, DevBuf<char>& tmp, hipStream_t st) {
+// after the previous part's, come out in canonical (qid, seq_id, pos, err)
+// order. Only the bits of qids below nqid are sorted; the key / index
+// buffers (B) are the context's, reused across calls.
+void sortHitsByQid(const sahara_hit* in, uint64_t n, uint64_t nqid, sahara_hit* out, MergeBufs& B, DevBuf<char>& tmp,
+                   hipStream_t st) {
     if (n == 0) return;
     if (n >= (1ull << 32)) throw Error("more than 2^32 hits to merge across index parts");
-    DevBuf<uint64_t> k0, k1;
-    DevBuf<uint32_t> v0, v1;
-    k0.reserve(n);
-    k1.reserve(n);
-    v0.reserve(n);
-    v1.reserve(n);
+    B.k0.reserve(n);
+    B.k1.reserve(n);
+    B.v0.reserve(n);
+    B.v1.reserve(n);
+    unsigned endBit = 1;
+    while (endBit < 64 && (nqid > (1ull << endBit))) ++endBit;
     const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(kQidKeys, dim3((unsigned)blocks), dim3(256), 0, st, in, n, k0.ptr, v0.ptr);
+    hipLaunchKernelGGL(kQidKeys, dim3((unsigned)blocks), dim3(256), 0, st, in, n, B.k0.ptr, B.v0.ptr);
     SH_HIP(hipGetLastError());
     size_t bytes = 0;
-    SH_HIP(rocprim::radix_sort_pairs(nullptr, bytes, k0.ptr, k1.ptr, v0.ptr, v1.ptr, (size_t)n, 0, 64, st));
+    SH_HIP(rocprim::radix_sort_pairs(nullptr, bytes, B.k0.ptr, B.k1.ptr, B.v0.ptr, B.v1.ptr, (size_t)n, 0, endBit, st));
     tmp.reserve(bytes + 256);
-    SH_HIP(rocprim::radix_sort_pairs(tmp.ptr, bytes, k0.ptr, k1.ptr, v0.ptr, v1.ptr, (size_t)n, 0, 64, st));
-    hipLaunchKernelGGL(kGatherHits, dim3((unsigned)blocks), dim3(256), 0, st, in, v1.ptr, n, out);
+    SH_HIP(rocprim::radix_sort_pairs(tmp.ptr, bytes, B.k0.ptr, B.k1.ptr, B.v0.ptr, B.v1.ptr, (size_t)n, 0, endBit, st));
+    hipLaunchKernelGGL(kGatherHits, dim3((unsigned)blocks), dim3(256), 0, st, in, B.v1.ptr, n, out);
     SH_HIP(hipGetLastError());
     SH_HIP(hipStreamSynchronize(st));
 }

@@ -97,7 +97,7 @@ static bool stageIn(Ctx* c, uint8_t* dst, const uint8_t* src, size_t n) {
     c->nibPats.reserve(nb + 8);
     SH_HIP(hipStreamSynchronize(c->st));  // the pinned buffer may still feed the last call's DMA
     uint8_t* out = c->nibHost;
-    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned nt = hostThreads(c, 16);
     constexpr size_t kPiece = 4u << 20;
     const size_t pieces = (nb + kPiece - 1) / kPiece;
     std::atomic<uint64_t> orAll{0};
@@ -292,7 +292,7 @@ bool hostHasAvx2() {
 }
 
 HostPool& hostPool(Ctx* c) {
-    if (!c->pool) c->pool = std::make_unique<HostPool>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+    if (!c->pool) c->pool = std::make_unique<HostPool>(hostThreads(c, 16) - 1, &c->place);
     return *c->pool;
 }
 
@@ -493,7 +493,13 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     if (const char* e = std::getenv("SAHARA_UPLOAD_CHUNK")) chunkPats = std::max<uint64_t>(2, std::atoll(e));
     uint64_t chunk = rc ? chunkPats / 2 : chunkPats;
     if (U.bits != 8) chunk = std::min<uint64_t>(chunk, Ctx::kRingSlot * 2 / m);
-    U.chunk = std::max<uint64_t>(2, chunk & ~uint64_t(1));
+    // chunk * m a multiple of 32 symbols: every chunk's region of the staging
+    // buffers (s0 / 2 bytes at 2 or 4 bits, s0 at 8) then starts 16-B aligned
+    // for kPackFrom2's word loads and kUnpack2's 16-B stores (C5: m = 250)
+    uint64_t g = 32;
+    while (m % g) g /= 2;
+    const uint64_t step = std::max<uint64_t>(2, 32 / g);
+    U.chunk = std::max<uint64_t>(step, chunk - chunk % step);
     if (c->ringInit.joinable()) c->ringInit.join();
     if (U.bits != 8 && !c->ring) throw Error("could not pin the upload ring buffer");
     for (hipEvent_t e : c->ringEv) SH_HIP(hipEventSynchronize(e));  // the last call's DMAs

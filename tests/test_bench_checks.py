@@ -134,3 +134,32 @@ def test_origin_recall():
     moved = h.copy()
     moved["pos"][moved["qid"] == 10] += 50
     assert bench.origin_recall(moved, origin, 2) == pytest.approx(399 / 400)
+
+
+def _mix64(x):
+    M = (1 << 64) - 1
+    x ^= x >> 30
+    x = (x * 0xbf58476d1ce4e5b9) & M
+    x ^= x >> 27
+    x = (x * 0x94d049bb133111eb) & M
+    return x ^ (x >> 31)
+
+
+def test_hits_digest_restates_kdigest():
+    """bench.hits_digest (numpy, wrapping u64) against the kDigest formula in
+    plain Python integers (search.hip kDigest), order-independent."""
+    rng = np.random.default_rng(5)
+    h = np.zeros(3000, sa.HIT_DTYPE)
+    h["qid"] = rng.integers(0, 1 << 40, len(h), dtype=np.uint64)
+    h["seq_id"] = rng.integers(0, 1 << 20, len(h), dtype=np.uint32)
+    h["pos"] = rng.integers(0, 1 << 33, len(h), dtype=np.uint64)
+    h["err"] = rng.integers(0, 16, len(h), dtype=np.uint32)
+    M = (1 << 64) - 1
+    want = 0
+    for r in h.tolist():
+        q, s, e, p = r
+        inner = _mix64(((s << 40) ^ (p << 4) ^ e) & M)
+        want = (want + _mix64(((q * 0x9E3779B97F4A7C15) & M) ^ inner)) & M
+    assert bench.hits_digest(h) == want
+    assert bench.hits_digest(h[::-1].copy()) == want
+    assert bench.hits_digest(h[:-1]) != want

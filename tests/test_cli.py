@@ -324,3 +324,32 @@ def test_cli_dynamic_generator(tmp_path, gpu_device):
     assert len(part) == 1 and sum(map(int, part[0][12:-1].split(","))) == 40
     from helpers import pset
     assert pset(hits_as_rows(read_hits(out, 4))) == pset(expected("a_lev_k2"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gen,k", [("backtracking", 2), ("h2-k2", 2), ("pigeon", 1)])
+def test_cli_hamming_node_counts_before_limit(gen, k, tmp_path, gpu_device):
+    """-d ham: search.cpp:207-208 print nodeCount<false> / weightedNodeCount<false>
+    of the expanded scheme, and only then (search.cpp:226) limitToHamming it
+    for the search; the hits are the limited scheme's."""
+    import sahara_amd as sa
+    from test_golden import read_fasta, SIGMA
+    reads = read_fasta(os.path.join(GOLD, "reads_a.fa"), SIGMA["a"])
+    m = len(reads[0])
+    n = sa.BiFMIndex.load(os.path.join(GOLD, IDX["a"]), device=gpu_device).info()["n"]
+    full = sa.search_scheme(gen, 0, k, m, hamming=False)
+    limited = sa.search_scheme(gen, 0, k, m, hamming=True)
+    nc, wnc = sa.scheme_counts(full, False, 6, n)
+    lnc, lwnc = sa.scheme_counts(limited, False, 6, n)
+    out = tmp_path / "h.txt"
+    rc, so, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                      "-e", k, "-g", gen, "-d", "ham", "-o", out)
+    assert rc == 0, err
+    lines = so.splitlines()
+    got_nc = float(next(ln for ln in lines if ln.startswith("node count: ")).split(": ")[1])
+    got_wnc = float(next(ln for ln in lines if ln.startswith("weighted node count: ")).split(": ")[1])
+    assert got_nc == nc and got_wnc == wnc
+    # (this build's count DP visits only reachable (pos, e) states, which the
+    # Hamming limit never removes: the limited scheme counts the same here;
+    # upstream's nodeCount over the raw bounds may not, hence the order)
+    assert (lnc, lwnc) == (nc, wnc)

@@ -152,7 +152,12 @@ def test_2bit_pattern_forms_any_length(gpu_device, monkeypatch, m):
     want = hits_as_rows(sa.search_reads(gpu, reads, sch))
     monkeypatch.setenv("SAHARA_UPLOAD_BITS", "2")
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
-    assert gpu.stats()["upload_chunks"][0] > 0
+    assert gpu.stats()["upload_chunks"][0] > 1
+    # the byte pass (kUnpack2's 16-B stores) over the same chunks: every
+    # chunk's region starts 16-B aligned whatever m (staging.cpp stageStreamed)
+    monkeypatch.setenv("SAHARA_UPLOAD_BYTES", "1")
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+    monkeypatch.delenv("SAHARA_UPLOAD_BYTES")
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
     assert np.array_equal(want, hits_as_rows(ref.search(sa.interleave_rc(reads, 6), sch, nthreads=8)[0]))
