@@ -339,9 +339,19 @@ def main():
         # buffer from its own result, the second pins it into the pool that
         # every later call draws from (capi.cpp allocHits)
         w2 = 2
-        # the reads cross PCIe, reverse complements interleaved on the device
-        # (sahara_gpu_search_reads: what `sahara search` calls)
-        extra["pcie_inclusive"] = pcie_inclusive(
+        # the reads cross PCIe, reverse complements interleaved on the device,
+        # the hits come back as 8-B records (sahara_gpu_search_reads_compact:
+        # what `sahara search` calls; single-part indexes)
+        if idx.info()["n_parts"] == 1:
+            extra["pcie_inclusive"] = pcie_inclusive(
+                lambda: sa.search_reads_compact(idx, reads, scheme, edit=edit), idx, nreads, args.steps, w2, world,
+                barrier, nh, digest,
+                "sahara_gpu_search_reads_compact from host reads: streamed upload (four symbols per byte, N listed) + "
+                "device RC interleave, search, locate, sort, each batch's hits written by the device as 8-B records "
+                "(qid, text position, e; sahara_hit_blocks) into pinned host memory recycled through "
+                "sahara_gpu_free_blocks")
+        # the same with whole 24-B sahara_hit records (sahara_gpu_search_reads)
+        extra["pcie_inclusive_full_records"] = pcie_inclusive(
             lambda: sa.search_reads(idx, reads, scheme, edit=edit), idx, nreads, args.steps, w2, world, barrier, nh,
             digest,
             "sahara_gpu_search_reads from host reads: streamed upload (four symbols per byte, N listed) + device RC interleave, "
@@ -621,7 +631,7 @@ def pcie_inclusive(search, idx, nreads, steps, warmup, world, barrier, local_hit
         n = len(h)
     barrier()
     el = time.perf_counter() - t0
-    same_digest = hits_digest(h) == local_digest
+    same_digest = hits_digest(h.to_hits() if hasattr(h, "to_hits") else h) == local_digest
     del h
     if world > 1:
         from sahara_amd.dist import max_over_ranks

@@ -155,6 +155,34 @@ int  sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uin
 int  sahara_gpu_search_reads(void* ctx, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
                              uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
                              uint32_t n_searches, int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits);
+/* Compact hit records: the same hits in 8 B each instead of 24, for callers
+ * that turn them into text anyway (`sahara search` writes "qid seqId pos"):
+ * a third of the device-to-host bytes, written by the device straight into
+ * page-locked host memory batch by batch while later batches search. Record
+ * i of block b (block_end[b-1] <= i < block_end[b], block_end[-1] = 0):
+ *   qid    = block_qid0[b] + (recs[i] >> 36)
+ *   text   = (recs[i] >> 4) & 0xFFFFFFFF   (position in the concatenated text)
+ *   err    = recs[i] & 15
+ *   seq_id = the r with rec_starts[r] <= text < rec_starts[r + 1]
+ *   pos    = text - rec_starts[seq_id]
+ * in canonical (qid, seq_id, pos, err) order. rec_starts (n_records + 1
+ * entries, the last = the text length) belongs to the context and stays valid
+ * until sahara_gpu_close; the rest is released by sahara_gpu_free_blocks. */
+typedef struct sahara_hit_blocks {
+    uint64_t* recs;
+    uint64_t n_hits;
+    uint64_t* block_qid0;
+    uint64_t* block_end;
+    uint64_t n_blocks;
+    const uint64_t* rec_starts;
+    uint64_t n_records;
+} sahara_hit_blocks;
+/* sahara_gpu_search_reads (max_hits = 0) with the hits as compact records.
+ * Needs a single-part index (text < 2^32 symbols) and at most 15 errors. */
+int  sahara_gpu_search_reads_compact(void* ctx, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
+                                     uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                                     uint32_t n_searches, int edit, sahara_hit_blocks* out);
+void sahara_gpu_free_blocks(sahara_hit_blocks* blocks);
 /* --search_mode besthits (search_ng21::search_best[_n], search.cpp:233-241):
  * n_schemes expanded schemes, scheme j covering exactly j errors, stored one
  * after another in pi/l/u (n_searches[j] rows of len entries each). A pattern's

@@ -20,6 +20,7 @@
 #include "oracle.h"
 
 #include <algorithm>
+#include <initializer_list>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -281,8 +282,90 @@ static PScheme genBox(int P, int minK, int maxK) {
     return s;
 }
 
+// A published table: per search the 1-based part order, lower and upper
+// cumulative bounds as digit strings, for errors in [0, K]; minK lifts the
+// last lower bound.
+struct TableRow { const char *pi, *l, *u; };
+static PScheme fromTable(std::initializer_list<TableRow> rows, int minK) {
+    PScheme out;
+    for (const TableRow& r : rows) {
+        PSearch s;
+        for (const char* c = r.pi; *c; ++c) s.pi.push_back(*c - '1');
+        for (const char* c = r.l; *c; ++c) s.l.push_back(*c - '0');
+        for (const char* c = r.u; *c; ++c) s.u.push_back(*c - '0');
+        s.l.back() = std::max(s.l.back(), minK);
+        out.push_back(s);
+    }
+    return out;
+}
+
 static bool makeScheme(const std::string& name, int minK, int maxK, PScheme& out) {
     if (minK < 0 || maxK < minK) return false;
+    const bool tableFamily = name == "lam" || name == "kucherov-k1" || name == "kucherov-k2";
+    if (tableFamily && maxK > 2) return false;  // tables for k <= 2 only
+    if (tableFamily && maxK == 0) {             // one exact search over the family's parts
+        const int P = name == "kucherov-k2" ? 2 : 1;
+        out = {PSearch{orderFrom(P, 0, true), std::vector<int>(P, 0), std::vector<int>(P, 0)}};
+        return true;
+    }
+    if (name == "lam") {  // Lam et al. 2009 (as Kucherov, Salikhov, Tsur 2016 give it)
+        out = maxK == 1 ? fromTable({{"12", "00", "01"}, {"21", "00", "01"}}, minK)
+                        : fromTable({{"123", "000", "022"}, {"321", "000", "012"}, {"213", "001", "012"}}, minK);
+        return true;
+    }
+    if (name == "kucherov-k1") {
+        out = maxK == 1 ? fromTable({{"12", "00", "01"}, {"21", "01", "01"}}, minK)
+                        : fromTable({{"123", "000", "022"}, {"321", "000", "012"}, {"213", "001", "012"}}, minK);
+        return true;
+    }
+    if (name == "kucherov-k2") {
+        out = maxK == 1 ? fromTable({{"123", "000", "011"}, {"321", "001", "001"}}, minK)
+                        : fromTable({{"1234", "0000", "0122"}, {"4321", "0001", "0122"}, {"2341", "0012", "0012"}},
+                                    minK);
+        return true;
+    }
+    if (name == "pigeon_opt" || name == "suffix") {
+        // both: K + 1 parts, search j = part j, then the parts right of it,
+        // then the parts left of it (nearest first)
+        const int P = maxK + 1;
+        out.clear();
+        for (int j = 0; j < P; ++j) {
+            PSearch s;
+            s.pi = orderFrom(P, j, true);
+            for (int i = 0; i < P; ++i) {
+                const bool rightSweep = i < P - j;          // part j itself and the parts right of it
+                const int r = rightSweep ? 0 : i - (P - j) + 1;  // r-th part of the left sweep
+                if (name == "pigeon_opt") {   // parts left of the lowest error-free part j: >= 1 error each
+                    s.l.push_back(i == 0 ? 0 : r);
+                    s.u.push_back(i == 0 ? 0 : (rightSweep ? maxK - j : maxK - j + r));
+                } else {                      // suffix filter: t + 1 parts of the suffix hold <= t errors
+                    s.l.push_back(0);
+                    s.u.push_back(rightSweep ? i : maxK);
+                }
+            }
+            s.l[P - 1] = std::max(s.l[P - 1], minK);
+            out.push_back(s);
+        }
+        return true;
+    }
+    if (name == "01*0") {  // K + 2 parts; one search per seed 0 1^t 0 (Vroland et al. 2016)
+        const int P = maxK + 2;
+        out.clear();
+        for (int i = 0; i < P; ++i)
+            for (int t = 0; t <= maxK && i + t + 2 <= P; ++t) {
+                PSearch s;
+                s.pi = orderFrom(P, i, true);
+                for (int x = 0; x < P; ++x) {
+                    if (x == 0) { s.l.push_back(0); s.u.push_back(0); }
+                    else if (x <= t) { s.l.push_back(x); s.u.push_back(x); }    // one error per middle part
+                    else if (x == t + 1) { s.l.push_back(t); s.u.push_back(t); } // the closing error-free part
+                    else { s.l.push_back(t); s.u.push_back(maxK); }
+                }
+                s.l[P - 1] = std::max(s.l[P - 1], minK);
+                out.push_back(s);
+            }
+        return true;
+    }
     if (name == "backtracking") {
         out = {PSearch{{0}, {minK}, {maxK}}};
         return true;

@@ -20,7 +20,7 @@ import os
 import numpy as np
 
 __all__ = [
-    "BiFMIndex", "HIT_DTYPE", "search", "search_reads", "search_scheme", "scheme_parts", "scheme_generators",
+    "BiFMIndex", "HIT_DTYPE", "search", "search_reads", "search_reads_compact", "CompactHits", "search_scheme", "scheme_parts", "scheme_generators",
     "scheme_counts", "synth_reference", "synth_reads", "interleave_rc", "load_fasta",
     "library_path", "lib", "SaharaError", "DNA5", "DNA4",
 ]
@@ -41,6 +41,12 @@ u64p = C.POINTER(C.c_uint64)
 
 class SaharaError(RuntimeError):
     pass
+
+
+class HitBlocks(C.Structure):
+    _fields_ = [("recs", C.POINTER(C.c_uint64)), ("n_hits", C.c_uint64), ("block_qid0", C.POINTER(C.c_uint64)),
+                ("block_end", C.POINTER(C.c_uint64)), ("n_blocks", C.c_uint64),
+                ("rec_starts", C.POINTER(C.c_uint64)), ("n_records", C.c_uint64)]
 
 
 class IndexInfo(C.Structure):
@@ -91,6 +97,9 @@ EXPORTED = {
     "sahara_gpu_search_reads": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64, u32p, u32p,
                                           u32p, C.c_uint32, C.c_int, C.c_uint32, C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_uint64)]),
+    "sahara_gpu_search_reads_compact": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64,
+                                                  u32p, u32p, u32p, C.c_uint32, C.c_int, C.POINTER(HitBlocks)]),
+    "sahara_gpu_free_blocks": (None, [C.POINTER(HitBlocks)]),
     "sahara_gpu_search_best": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                          u32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_uint64)]),
@@ -374,6 +383,68 @@ def search_reads(index, reads, scheme, edit=True, reverse=True, limit=0, max_hit
                                          _p(pi, u32p), _p(l, u32p), _p(u, u32p), pi.shape[0], int(edit), max_hits,
                                          C.byref(out), C.byref(n)))
     return _hits_array(out, n.value)
+
+
+class CompactHits:
+    """Hits of sahara_gpu_search_reads_compact (include/sahara_hip.h
+    sahara_hit_blocks): 8-B records in page-locked host memory, one block per
+    batch. `recs` is a zero-copy view; to_hits() expands them to HIT_DTYPE.
+    The library memory goes back with close() or the last reference."""
+
+    def __init__(self, blocks, index):
+        self._b = blocks
+        self._index = index  # rec_starts belongs to the context
+        n = blocks.n_hits
+        self.recs = np.ctypeslib.as_array(blocks.recs, shape=(n,)) if n else np.zeros(0, np.uint64)
+        nb = blocks.n_blocks
+        self.block_qid0 = np.ctypeslib.as_array(blocks.block_qid0, shape=(nb,)).copy() if nb else np.zeros(0, np.uint64)
+        self.block_end = np.ctypeslib.as_array(blocks.block_end, shape=(nb,)).copy() if nb else np.zeros(0, np.uint64)
+        self.rec_starts = np.ctypeslib.as_array(blocks.rec_starts, shape=(blocks.n_records + 1,)).copy()
+
+    def __len__(self):
+        return int(self._b.n_hits) if self._b is not None else 0
+
+    def to_hits(self):
+        n = len(self)
+        out = np.zeros(n, HIT_DTYPE)
+        if n == 0:
+            return out
+        v = self.recs
+        counts = np.diff(np.concatenate([[0], self.block_end])).astype(np.int64)
+        base = np.repeat(self.block_qid0, counts)
+        out["qid"] = base + (v >> np.uint64(36))
+        g = (v >> np.uint64(4)) & np.uint64(0xFFFFFFFF)
+        seq = np.searchsorted(self.rec_starts, g, side="right") - 1
+        out["seq_id"] = seq
+        out["pos"] = g - self.rec_starts[seq]
+        out["err"] = (v & np.uint64(15)).astype(np.uint32)
+        return out
+
+    def close(self):
+        if self._b is not None:
+            self.recs = None
+            lib().sahara_gpu_free_blocks(C.byref(self._b))
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def search_reads_compact(index, reads, scheme, edit=True, reverse=True, limit=0):
+    """search_reads (max_hits = 0) with the hits as compact 8-B records written
+    by the device into pinned host memory (sahara_gpu_search_reads_compact)."""
+    r = np.ascontiguousarray(reads, dtype=np.uint8)
+    if r.ndim != 2 or r.shape[0] == 0:
+        raise SaharaError("reads must be a non-empty (n_reads, len) array")
+    pi, l, u = (np.ascontiguousarray(a, dtype=np.uint32) for a in scheme)
+    b = HitBlocks()
+    _check(lib().sahara_gpu_search_reads_compact(index._h, _p(r, u8p), r.shape[0], r.shape[1], int(reverse),
+                                                 int(limit), _p(pi, u32p), _p(l, u32p), _p(u, u32p), pi.shape[0],
+                                                 int(edit), C.byref(b)))
+    return CompactHits(b, index)
 
 
 def search_best(index, queries, schemes, max_hits=0):

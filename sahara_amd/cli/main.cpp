@@ -196,14 +196,25 @@ int cmdIndex(int argc, char** argv) {
 // --------------------------------------------------------------- search ----
 
 // One device's hits as the library hands them over: qids local to its shard.
+// Either whole records (hits) or compact ones (blocks, sahara_hit_blocks).
 struct HitPart {
     sahara_hit* hits = nullptr;
+    sahara_hit_blocks blocks{};
+    bool compact = false;
     uint64_t n = 0;
     uint64_t qidOffset = 0;
+    void release() {
+        if (compact) sahara_gpu_free_blocks(&blocks);
+        else sahara_gpu_free(hits);
+        hits = nullptr;
+        compact = false;
+    }
 };
 
 // Text output of hits: "qid seqId pos[ e]\n" (search.cpp:254-261). Blocks of
-// hits are formatted on nt threads, then written in order.
+// hits are formatted on nt threads, then written in order. Compact records
+// are decoded right here, in the formatting loop that runs anyway: record id
+// by the record starts (usually the previous hit's record), position, errors.
 void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool emitErrors, unsigned nt) {
     std::FILE* f = std::fopen(path.c_str(), "w");
     if (!f) throw CliError("can not open output file " + path);
@@ -225,18 +236,39 @@ void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool 
             buf.resize((B.hi - B.lo) * 96);
             char* o = buf.data();
             char* e = o + buf.size();
-            for (uint64_t k = B.lo; k < B.hi; ++k) {
-                const sahara_hit& h = B.part->hits[k];
-                o = std::to_chars(o, e, h.qid + B.part->qidOffset).ptr;
+            auto line = [&](uint64_t qid, uint64_t seq, uint64_t pos, uint32_t err) {
+                o = std::to_chars(o, e, qid).ptr;
                 *o++ = ' ';
-                o = std::to_chars(o, e, h.seq_id).ptr;
+                o = std::to_chars(o, e, seq).ptr;
                 *o++ = ' ';
-                o = std::to_chars(o, e, h.pos).ptr;
+                o = std::to_chars(o, e, pos).ptr;
                 if (emitErrors) {
                     *o++ = ' ';
-                    o = std::to_chars(o, e, h.err).ptr;
+                    o = std::to_chars(o, e, err).ptr;
                 }
                 *o++ = '\n';
+            };
+            const HitPart& P = *B.part;
+            if (!P.compact) {
+                for (uint64_t k = B.lo; k < B.hi; ++k) {
+                    const sahara_hit& h = P.hits[k];
+                    line(h.qid + P.qidOffset, h.seq_id, h.pos, h.err);
+                }
+            } else {
+                const sahara_hit_blocks& H = P.blocks;
+                const uint64_t* S = H.rec_starts;
+                uint64_t blk = (uint64_t)(std::upper_bound(H.block_end, H.block_end + H.n_blocks, B.lo) - H.block_end);
+                uint64_t seq = 0, lo = 1, hi = 0;  // the current record's [start, next start): empty
+                for (uint64_t k = B.lo; k < B.hi; ++k) {
+                    while (k >= H.block_end[blk]) ++blk;
+                    const uint64_t v = H.recs[k], g = (v >> 4) & 0xFFFFFFFFull;
+                    if (g < lo || g >= hi) {
+                        seq = (uint64_t)(std::upper_bound(S, S + H.n_records + 1, g) - S) - 1;
+                        lo = S[seq];
+                        hi = S[seq + 1];
+                    }
+                    line(H.block_qid0[blk] + (v >> 36) + P.qidOffset, seq, g - lo, (uint32_t)(v & 15u));
+                }
             }
             buf.resize((size_t)(o - buf.data()));
         });
@@ -408,11 +440,14 @@ int cmdSearch(int argc, char** argv) {
     {
         const char* names[64];
         int ng = sahara_scheme_generators(names, nullptr, 64);
+        // the reference lists generator::all's keys, a map: sorted by name (search.cpp:177-181)
+        std::vector<std::string> sorted(names, names + ng);
+        std::sort(sorted.begin(), sorted.end());
         bool known = false;
         std::string all;
-        for (int i = 0; i < ng; ++i) {
-            known = known || gen.value == names[i];
-            all += (i ? ", " : "") + std::string(names[i]);
+        for (size_t i = 0; i < sorted.size(); ++i) {
+            known = known || gen.value == sorted[i];
+            all += (i ? ", " : "") + sorted[i];
         }
         if (!known)
             throw CliError("unknown search scheme generetaror \"" + gen.value + "\", valid generators are: " + all);
@@ -469,6 +504,10 @@ int cmdSearch(int argc, char** argv) {
     }
     timing.emplace_back("searchScheme", sw.reset());
 
+    // hits as compact records where they apply (all mode without --max_hits,
+    // one index part, <= 15 errors; SAHARA_CLI_FULL_HITS=1: whole records)
+    const char* fullEnv = std::getenv("SAHARA_CLI_FULL_HITS");
+    const bool compactOut = !besthits && mh <= 0 && info.n_parts == 1 && k <= 15 && !(fullEnv && std::atoi(fullEnv));
     // search + locate (search.cpp:218-250), reads sharded over the devices
     // (a read and its reverse complement stay together; qids stay global)
     std::vector<HitPart> parts(ngpu);
@@ -486,7 +525,15 @@ int cmdSearch(int argc, char** argv) {
                 uint64_t nh = 0;
                 int rc;
                 const uint32_t cap = (uint32_t)std::max(0L, mh);
-                if (!besthits) {
+                HitPart part;
+                if (!besthits && compactOut) {  // 8-B records straight into host memory, decoded by writeHits
+                    const Scheme& s = schemes[0];
+                    rc = sahara_gpu_search_reads_compact(ctx[g], reads + r0 * len, r1 - r0, len, noRev.given ? 0 : 1,
+                                                         q1 - q0, s.pi.data(), s.l.data(), s.u.data(), s.n,
+                                                         edit ? 1 : 0, &part.blocks);
+                    part.compact = rc == 0;
+                    nh = part.blocks.n_hits;
+                } else if (!besthits) {
                     const Scheme& s = schemes[0];
                     rc = sahara_gpu_search_reads(ctx[g], reads + r0 * len, r1 - r0, len, noRev.given ? 0 : 1, q1 - q0,
                                                  s.pi.data(), s.l.data(), s.u.data(), s.n, edit ? 1 : 0, cap, &hits,
@@ -520,14 +567,17 @@ int cmdSearch(int argc, char** argv) {
                 sahara_gpu_stats(ctx[g], &st);
                 devLocate[g] = (st.locate_ms + st.sort_ms) / 1e3;
                 devSearch[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                parts[g] = HitPart{hits, nh, q0};  // released after writing
+                part.hits = hits;
+                part.n = nh;
+                part.qidOffset = q0;
+                parts[g] = part;  // released after writing
             });
         }
         for (auto& t : th) t.join();
     }
     for (auto& e : errs)
         if (!e.empty()) {
-            for (auto& hp : parts) sahara_gpu_free(hp.hits);
+            for (auto& hp : parts) hp.release();
             throw CliError("search: " + e);
         }
     double wall = sw.reset();
@@ -538,7 +588,7 @@ int cmdSearch(int argc, char** argv) {
     uint64_t nhits = 0;
     for (auto& hp : parts) nhits += hp.n;
     writeHits(output.value, parts, emitErr.given, nt);
-    for (auto& hp : parts) sahara_gpu_free(hp.hits);
+    for (auto& hp : parts) hp.release();
     timing.emplace_back("result", sw.reset());
     for (void* c : ctx) sahara_gpu_close(c);
 

@@ -471,15 +471,26 @@ static HitPool& hitPool() {
     return *p;
 }
 
-// Host buffer for n hits (released with sahara_gpu_free); *pinned tells
-// whether the device can copy into it directly.
+// Host buffer of `bytes` (released with sahara_gpu_free); *pinned tells
+// whether the device can copy (or write) into it directly; *capBytes its size.
+static void* allocPinned(size_t bytes, bool* pinned, size_t* capBytes, bool mayPin, bool always = false);
+
+// Host buffer for n hits (released with sahara_gpu_free).
 static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr, bool mayPin = true) {
-    const size_t bytes = std::max<uint64_t>(n, 1) * sizeof(sahara_hit);
+    size_t cap = 0;
+    void* p = allocPinned(std::max<uint64_t>(n, 1) * sizeof(sahara_hit), pinned, &cap, mayPin);
+    if (capHits) *capHits = cap / sizeof(sahara_hit);
+    return p;
+}
+
+// always: pinned whatever the size (a sink the device writes into)
+static void* allocPinned(size_t bytes, bool* pinned, size_t* capBytes, bool mayPin, bool always) {
+    bytes = std::max<size_t>(bytes, 1);
     *pinned = false;
-    if (capHits) *capHits = std::max<uint64_t>(n, 1);
+    *capBytes = bytes;
     size_t pinMin = 64u << 20;  // SAHARA_PIN_MIN: smallest pinned buffer in bytes (tests pin every size)
     if (const char* e = std::getenv("SAHARA_PIN_MIN")) pinMin = (size_t)std::atoll(e);
-    if (bytes < pinMin) return std::malloc(bytes);
+    if (bytes < pinMin && !always) return std::malloc(bytes);
     HitPool& P = hitPool();
     std::vector<void*> unpin;
     void* p = nullptr;
@@ -491,7 +502,7 @@ static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr, bo
         if (best != SIZE_MAX) {
             p = P.idle[best].first;
             P.live[p] = P.idle[best].second;
-            if (capHits) *capHits = P.idle[best].second / sizeof(sahara_hit);
+            *capBytes = P.idle[best].second;
             P.idle.erase(P.idle.begin() + (long)best);
         } else {  // none fits: the smaller idle ones will not fit later calls of this size either
             for (auto& e : P.idle) unpin.push_back(e.first);
@@ -509,7 +520,7 @@ static void* allocHits(uint64_t n, bool* pinned, uint64_t* capHits = nullptr, bo
         std::lock_guard<std::mutex> g(P.mu);
         P.live[p] = cap;
         *pinned = true;
-        if (capHits) *capHits = cap / sizeof(sahara_hit);
+        *capBytes = cap;
         return p;
     }
     (void)hipGetLastError();
@@ -744,6 +755,137 @@ int sahara_gpu_search_reads(void* ctx, const uint8_t* reads, uint64_t n_reads, u
         const uint64_t rows = reverse ? (npat + 1) / 2 : npat;
         searchStreamed(c, reads, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit, max_hits, hits, n_hits);
     });
+}
+
+// sahara_gpu_search_reads_compact: the streamed pass with every batch's hits
+// written as 8-B records by the device into a pinned host sink (pass.cpp
+// finish), handed over as blocks (one per batch).
+static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
+                               uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                               uint32_t n_searches, int edit, sahara_hit_blocks* out) {
+    using clk = std::chrono::steady_clock;
+    const auto tA = clk::now();
+    if (c->I.sigma != 5 && c->I.sigma != 6) throw Error("reverse complements need a dna4 or dna5 index");
+    if (!c->more.empty()) throw Error("compact hit records need a single-part index (text < 2^32 symbols)");
+    uint64_t npat = reverse ? 2 * n_reads : n_reads;
+    if (limit && limit < npat) npat = limit;  // --limit_queries (search.cpp:125-127)
+    if (npat == 0) throw Error("no patterns");
+    const uint64_t rows = reverse ? (npat + 1) / 2 : npat;
+    {
+        const char* te = std::getenv("SAHARA_TIMING");
+        c->traceOn = te && std::atoi(te) >= 2;
+        c->traceT0 = tA;
+        c->trace.clear();
+    }
+    stageStreamed(c, reads, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit);
+    if (c->maxErr > 15) throw Error("compact hit records hold at most 15 errors");
+    c->sink = nullptr;
+    c->compactSink = c->sinkPinned = false;
+    // the sink, sized from the last call (else 2 hits per pattern), always
+    // page-locked: the device writes into it
+    const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
+    bool pinned = false;
+    size_t capBytes = 0;
+    void* sinkMem = allocPinned(est * 8, &pinned, &capBytes, true, true);
+    if (!sinkMem) throw Error("out of host memory for hits");
+    if (const char* e = std::getenv("SAHARA_BLOCK_WRITE_WG")) c->blockWriteBlocks = (uint32_t)std::max(1, std::atoi(e));
+    c->blockRecs = pinned ? static_cast<uint64_t*>(sinkMem) : nullptr;
+    c->sinkCap = pinned ? capBytes / 8 : 0;
+    auto* recs = static_cast<uint64_t*>(sinkMem);
+    uint64_t recCap = capBytes / 8;
+    try {
+        run(c, false);
+        uint32_t bad = 0;
+        SH_HIP(hipMemcpy(&bad, c->badFlag.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (bad) throw Error("pattern rank out of range for this index");
+        const auto t0 = clk::now();
+        if (!c->blockRecs || c->sinkDone < c->nout) {
+            // the sink held too few (or is not pinned): the records of every
+            // batch again, from the device-resident hits, into one that fits
+            if (c->nout > recCap) {
+                freeHits(recs);
+                recs = nullptr;
+                recs = static_cast<uint64_t*>(allocPinned(c->nout * 8, &pinned, &capBytes, true, true));
+                if (!recs) throw Error("out of host memory for hits");
+                recCap = capBytes / 8;
+            }
+            uint64_t* dst = recs;
+            if (!pinned) {
+                c->outC.reserve(std::max<uint64_t>(c->nout, 1));
+                dst = c->outC.ptr;
+            }
+            uint64_t b0 = 0;
+            for (size_t b = 0; b < c->batchQ0.size(); ++b) {
+                launchCompactHits(c->out.ptr + b0, c->batchEnd[b] - b0, c->batchQ0[b], c->I.dRecStarts.ptr, dst + b0,
+                                  c->st, pinned ? 256u : 8192u);
+                b0 = c->batchEnd[b];
+            }
+            if (!pinned && c->nout) SH_HIP(hipMemcpyAsync(recs, dst, c->nout * 8, hipMemcpyDeviceToHost, c->st));
+            SH_HIP(hipStreamSynchronize(c->st));
+        }
+        c->stats.output_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    } catch (...) {
+        drainAll(c);
+        c->blockRecs = nullptr;
+        freeHits(recs);
+        c->staged = c->streaming = false;
+        throw;
+    }
+    c->blockRecs = nullptr;
+    c->streaming = false;
+    c->stats.stage_ms = c->up.hostMs;
+    for (int b = 0; b < 3; ++b) c->stats.upload_chunks[b] = c->up.chunks[b];
+    const size_t nb = c->batchQ0.size();
+    auto* q0 = static_cast<uint64_t*>(std::malloc(std::max<size_t>(nb, 1) * 8));
+    auto* end = static_cast<uint64_t*>(std::malloc(std::max<size_t>(nb, 1) * 8));
+    if (!q0 || !end) {
+        std::free(q0);
+        std::free(end);
+        freeHits(recs);
+        throw Error("out of host memory for hit blocks");
+    }
+    for (size_t b = 0; b < nb; ++b) {
+        q0[b] = c->batchQ0[b];
+        end[b] = c->batchEnd[b];
+    }
+    if (c->recStartsEnd.size() != c->I.recStarts.size() + 1) {
+        c->recStartsEnd = c->I.recStarts;
+        c->recStartsEnd.push_back(c->I.n);
+    }
+    out->recs = recs;
+    out->n_hits = c->nout;
+    out->block_qid0 = q0;
+    out->block_end = end;
+    out->n_blocks = nb;
+    out->rec_starts = c->recStartsEnd.data();
+    out->n_records = c->I.recStarts.size();
+    c->lastHits = c->nout;
+    if (std::getenv("SAHARA_TIMING")) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[sahara] compact call %.1f ms (host packing %.1f ms), output %.1f ms\n", ms(tA, clk::now()),
+                     c->up.hostMs, c->stats.output_ms);
+        std::sort(c->trace.begin(), c->trace.end());
+        for (auto& m : c->trace) std::fprintf(stderr, "[sahara]   %8.2f %s\n", m.first, m.second.c_str());
+        c->traceOn = false;
+    }
+}
+
+int sahara_gpu_search_reads_compact(void* ctx, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
+                                    uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                                    uint32_t n_searches, int edit, sahara_hit_blocks* out) {
+    return guarded([&] {
+        if (!out) throw Error("sahara_gpu_search_reads_compact: null output");
+        *out = sahara_hit_blocks{};
+        searchReadsCompact(ctxOf(ctx), reads, n_reads, len, reverse, limit, pi, l, u, n_searches, edit, out);
+    });
+}
+
+void sahara_gpu_free_blocks(sahara_hit_blocks* b) {
+    if (!b) return;
+    freeHits(b->recs);
+    std::free(b->block_qid0);
+    std::free(b->block_end);
+    *b = sahara_hit_blocks{};
 }
 
 int sahara_gpu_search_best(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len, const uint32_t* pi,

@@ -351,6 +351,14 @@ struct Ctx {
     uint64_t downJobs = 0;                // batches handed to the expander this call
     std::vector<hipEvent_t> downEv;
     std::unique_ptr<Expander> expander;
+    // sahara_gpu_search_reads_compact: each batch's hits as 8-B records,
+    // written by kCompactHits (blockWriteBlocks workgroups) straight into
+    // this pinned host buffer (sinkCap records) on stF; per batch its first
+    // qid and one past its last record (the blocks of sahara_hit_blocks)
+    uint64_t* blockRecs = nullptr;
+    uint32_t blockWriteBlocks = 64;
+    std::vector<uint64_t> batchQ0, batchEnd;
+    std::vector<uint64_t> recStartsEnd;   // record starts + the text length (sahara_hit_blocks.rec_starts)
     // SAHARA_TIMING=2: host-side marks of one call (ms since its start, what)
     bool traceOn = false;
     std::chrono::steady_clock::time_point traceT0;

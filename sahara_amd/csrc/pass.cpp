@@ -158,6 +158,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
     if (const char* e = std::getenv("SAHARA_BATCH"))
         maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
+    if (c->blockRecs) maxBatch = std::min<uint64_t>(maxBatch, 1ull << 27);  // compact records: qid - q0 < 2^28
     const uint64_t batchesHere = (c->npat + maxBatch - 1) / maxBatch;
     if (!serial && batchesHere > 1 && c->verify) bpc = 1;
     if (const char* e = std::getenv("SAHARA_FM_BPC")) bpc = std::max(1, std::min(searchBlocksPerCU(sigma, c->edit, lds), std::atoi(e)));
@@ -274,7 +275,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
     c->sinkDone = 0;
-    c->sinkOk = c->sink != nullptr;
+    c->sinkOk = c->sink != nullptr || c->blockRecs != nullptr;
+    c->batchQ0.clear();
+    c->batchEnd.clear();
     // a slot's counters and queues are zero when its `free` event fires:
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
@@ -519,9 +522,15 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(c->ev[4], sC));
         // sahara_gpu_search's host sink: the batch's hits go to host memory
         // on stF while later batches search (while they fit the sink)
+        c->batchQ0.push_back(q0);
+        c->batchEnd.push_back(c->nout + rows);
         if (c->sinkOk && c->nout + rows <= c->sinkCap) {
             const bool compact = c->compactSink && rows * sizeof(uint64_t) <= Ctx::kDownSlot && nb < (1ull << 28);
-            if (rows && compact) {  // 8-B records, expanded on the host (Expander)
+            if (rows && c->blockRecs) {  // compact records written by the device into the pinned sink (PCIe writes)
+                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[4], 0));
+                launchCompactHits(c->out.ptr + c->nout, rows, q0, c->I.dRecStarts.ptr, c->blockRecs + c->nout, c->stF,
+                                  c->blockWriteBlocks);
+            } else if (rows && compact) {  // 8-B records, expanded on the host (Expander)
                 const uint64_t j = c->downJobs++;
                 const size_t slot = (size_t)(j % Ctx::kDownSlots);
                 if (j >= Ctx::kDownSlots) c->expander->waitFor(j + 1 - Ctx::kDownSlots);  // the slot is read

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -99,8 +100,124 @@ std::vector<Part> boxScheme(int P, int minK, int maxK) {
     return out;
 }
 
+// A published table {pi (1-based digits), l, u} per search, for errors in
+// [0, K]; minK raises the last lower bound (a search then reports only
+// alignments with >= minK errors; completeness holds, the total is the last
+// cumulative count).
+std::vector<Part> table(std::initializer_list<const char*> rows, int minK) {
+    std::vector<Part> out;
+    for (const char* r : rows) {  // "123,000,022"
+        Part p;
+        const char* f[3] = {r, std::strchr(r, ',') + 1, std::strrchr(r, ',') + 1};
+        for (const char* c = f[0]; *c != ','; ++c) p.pi.push_back(*c - '1');
+        for (const char* c = f[1]; *c != ','; ++c) p.l.push_back(*c - '0');
+        for (const char* c = f[2]; *c; ++c) p.u.push_back(*c - '0');
+        p.l.back() = std::max(p.l.back(), minK);
+        out.push_back(p);
+    }
+    return out;
+}
+
+// the order that starts at part j, sweeps right to the end, then left to 0
+std::vector<int> rightThenLeft(int P, int j) {
+    std::vector<int> o{j};
+    for (int t = j + 1; t < P; ++t) o.push_back(t);
+    for (int t = j - 1; t >= 0; --t) o.push_back(t);
+    return o;
+}
+
+// K = 0 for a table family: one exact search over its P parts
+std::vector<Part> exactOnly(int P) { return {Part{connected(P, 0, true), std::vector<int>(P, 0), std::vector<int>(P, 0)}}; }
+
 bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& out) {
     if (minK < 0 || maxK < minK || maxK > 15) return false;
+    // Lam et al. 2009 (bidirectional BWT, k <= 2), as Kucherov, Salikhov and
+    // Tsur (2016) state it: halves / thirds searched exactly first
+    if (name == "lam") {
+        if (maxK == 0) out = exactOnly(1);
+        else if (maxK == 1) out = table({"12,00,01", "21,00,01"}, minK);
+        else if (maxK == 2) out = table({"123,000,022", "321,000,012", "213,001,012"}, minK);
+        else return false;
+        return true;
+    }
+    // Kucherov, Salikhov, Tsur 2016, K + 1 parts (k1) and K + 2 parts (k2),
+    // K <= 2; the K + 2 tables are this build's tightest bounds for KST's
+    // three search shapes (forward, backward, bidirectional from part 2)
+    if (name == "kucherov-k1") {
+        if (maxK == 0) out = exactOnly(1);
+        else if (maxK == 1) out = table({"12,00,01", "21,01,01"}, minK);
+        else if (maxK == 2) out = table({"123,000,022", "321,000,012", "213,001,012"}, minK);
+        else return false;
+        return true;
+    }
+    if (name == "kucherov-k2") {
+        if (maxK == 0) out = exactOnly(2);
+        else if (maxK == 1) out = table({"123,000,011", "321,001,001"}, minK);
+        else if (maxK == 2) out = table({"1234,0000,0122", "4321,0001,0122", "2341,0012,0012"}, minK);
+        else return false;
+        return true;
+    }
+    // pigeonhole with fewer redundant searches: search j starts at part j,
+    // taken as the lowest error-free part, so the parts left of it hold >= 1
+    // error each (swept last: cumulative >= r after r of them; cumulative
+    // bounds cannot say "each", so some overlap stays) and the right sweep
+    // <= K - j
+    if (name == "pigeon_opt") {
+        const int P = maxK + 1;
+        out.clear();
+        for (int j = 0; j < P; ++j) {
+            Part p;
+            p.pi = rightThenLeft(P, j);
+            p.l.push_back(0);
+            p.u.push_back(0);
+            for (int t = j + 1; t < P; ++t) { p.l.push_back(0); p.u.push_back(maxK - j); }
+            for (int r = 1; r <= j; ++r) { p.l.push_back(r); p.u.push_back(maxK - (j - r)); }
+            p.l.back() = std::max(p.l.back(), minK);
+            out.push_back(p);
+        }
+        return true;
+    }
+    // suffix filter (Karkkainen and Na 2007): with <= K errors in K + 1 parts
+    // some part j starts a suffix whose first t + 1 parts hold <= t errors;
+    // search j checks that prefix bound on its right sweep, then goes left
+    if (name == "suffix") {
+        const int P = maxK + 1;
+        out.clear();
+        for (int j = 0; j < P; ++j) {
+            Part p;
+            p.pi = rightThenLeft(P, j);
+            for (int t = 0; t < P - j; ++t) { p.l.push_back(0); p.u.push_back(t); }
+            for (int r = 0; r < j; ++r) { p.l.push_back(0); p.u.push_back(maxK); }
+            p.l.back() = std::max(p.l.back(), minK);
+            out.push_back(p);
+        }
+        return true;
+    }
+    // 01*0 seeds (Vroland et al. 2016): <= K errors in K + 2 parts leave two
+    // error-free parts with only one-error parts between them; one search per
+    // such seed (start part i, s - 2 one-error parts), seed first, then right,
+    // then left
+    if (name == "01*0") {
+        const int P = maxK + 2;
+        out.clear();
+        for (int i = 0; i < P; ++i)
+            for (int sl = 2; i + sl <= P; ++sl) {
+                const int mid = sl - 2;
+                if (mid > maxK) continue;
+                Part p;
+                for (int t = i; t < P; ++t) p.pi.push_back(t);
+                for (int t = i - 1; t >= 0; --t) p.pi.push_back(t);
+                p.l.push_back(0);
+                p.u.push_back(0);
+                for (int t = 1; t <= mid; ++t) { p.l.push_back(t); p.u.push_back(t); }
+                p.l.push_back(mid);
+                p.u.push_back(mid);
+                while ((int)p.l.size() < P) { p.l.push_back(mid); p.u.push_back(maxK); }
+                p.l.back() = std::max(p.l.back(), minK);
+                out.push_back(p);
+            }
+        return true;
+    }
     if (name == "backtracking") {
         out = {Part{{0}, {minK}, {maxK}}};
         return true;
@@ -126,12 +243,22 @@ bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& ou
     return false;
 }
 
-const char* kNames[] = {"backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3"};
+// in the reference's listing order (search_scheme.cpp:192); the names it lists
+// beyond these (optimum, 01*0_opt, kianfar, hato, pex-*) have no construction
+// restatable offline and stay unknown (search.cpp:181's error)
+const char* kNames[] = {"backtracking", "01*0", "pigeon", "pigeon_opt", "suffix", "h2-k1", "h2-k2", "h2-k3",
+                        "kucherov-k1", "kucherov-k2", "lam"};
 const char* kDescs[] = {"single part, errors anywhere",
+                        "k+2 parts, one search per 0 1* 0 seed (Vroland et al.)",
                         "k+1 parts, one exact part per search (pigeonhole)",
+                        "k+1 parts, pigeonhole with tightened bounds",
+                        "k+1 parts, suffix filter (Karkkainen and Na)",
                         "k+1 parts, greedy-box optimum-style scheme",
                         "k+2 parts, greedy-box optimum-style scheme (default)",
-                        "k+3 parts, greedy-box optimum-style scheme"};
+                        "k+3 parts, greedy-box optimum-style scheme",
+                        "k+1 parts, Kucherov, Salikhov and Tsur (k <= 2)",
+                        "k+2 parts, Kucherov, Salikhov and Tsur shapes (k <= 2)",
+                        "Lam et al. bidirectional scheme (k <= 2)"};
 
 // expand(oss, len) with explicit part sizes: inside a part the order follows
 // the search direction; upper bounds hold for the whole part, lower bounds

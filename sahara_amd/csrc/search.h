@@ -136,7 +136,7 @@ struct MergeBufs {
 void sortHitsByQid(const sahara_hit* in, uint64_t n, uint64_t nqid, sahara_hit* out, MergeBufs& B, DevBuf<char>& tmp,
                    hipStream_t st);
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
-                       hipStream_t st);
+                       hipStream_t st, uint32_t maxBlocks = 8192);
 void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,
                      uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks, uint32_t* pats,
                      uint4* pats3, hipStream_t st);

@@ -1732,10 +1732,13 @@ __global__ void kCompactHits(const sahara_hit* __restrict__ h, uint64_t n, uint6
     }
 }
 
+// `out` may be page-locked host memory: then the kernel's stores are the
+// PCIe transfer (posted writes, ~link rate), and a few workgroups (maxBlocks)
+// keep it off most CUs.
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
-                       hipStream_t st) {
+                       hipStream_t st, uint32_t maxBlocks) {
     if (n == 0) return;
-    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, std::max<uint32_t>(maxBlocks, 1));
     hipLaunchKernelGGL(kCompactHits, dim3((unsigned)blocks), dim3(256), 0, st, h, n, qidBase, starts, out);
     SH_HIP(hipGetLastError());
 }

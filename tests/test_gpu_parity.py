@@ -57,6 +57,27 @@ CASES = [  # sigma, edit, k, m, gen, with_n, repeats
 MODES = [(True, True), (False, False), (True, False), (False, True)]  # (verify, locate_sa)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("gen,k,edit", [("lam", 2, True), ("kucherov-k1", 1, True), ("kucherov-k2", 2, True),
+                                        ("pigeon_opt", 3, True), ("suffix", 2, True), ("01*0", 2, True),
+                                        ("01*0", 3, False), ("suffix", 3, False)])
+def test_gpu_equals_oracle_published_generators(gpu_device, gen, k, edit):
+    """Each of the published generators (search_scheme.cpp:192 names): GPU ==
+    oracle multiset in every execution mode, seeds from the k-mer table and
+    text tasks included."""
+    rng = np.random.default_rng(k + len(gen))
+    recs = random_records(rng, [20000, 9000], 6, repeats=True)
+    reads = mutate_reads(rng, recs, 250, 60, k, 6)
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme(gen, 0, k, 60, hamming=not edit)
+    want, _ = O.Index.build(recs, 6, 16).search(pats, scheme, edit=edit, nthreads=8)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    for verify, locate_sa in MODES:
+        gpu.set_mode(verify=verify, locate_sa=locate_sa)
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, edit=edit)), hits_as_rows(want)), \
+            (verify, locate_sa)
+
+
 @pytest.mark.parametrize("sigma,edit,k,m,gen,with_n,repeats", CASES)
 def test_gpu_search_multiset_equals_oracle(gpu_device, sigma, edit, k, m, gen, with_n, repeats):
     rng = np.random.default_rng(7 * k + m + sigma + (1 if edit else 0))

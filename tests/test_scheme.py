@@ -6,7 +6,15 @@ import pytest
 import oracle as O
 import sahara_amd as sa
 
-GENS = ["backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3"]
+GENS = ["backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3", "lam", "kucherov-k1", "kucherov-k2", "pigeon_opt",
+        "suffix", "01*0"]
+# published tables for k <= 2 only (unknown generator beyond, like upstream's
+# generators outside their tables)
+KMAX = {"lam": 2, "kucherov-k1": 2, "kucherov-k2": 2}
+# the reference's listing (search_scheme.cpp:192); the rest stay unknown here
+REFERENCE_ORDER = ["backtracking", "optimum", "01*0", "01*0_opt", "pigeon", "pigeon_opt", "suffix", "h2-k1", "h2-k2",
+                   "h2-k3", "kianfar", "kucherov-k1", "kucherov-k2", "lam", "hato", "pex-td", "pex-td-l", "pex-bu",
+                   "pex-bu-l"]
 
 
 def covers(pi, l, u, d):
@@ -35,6 +43,10 @@ def dists(P, lo, hi):
 @pytest.mark.parametrize("gen", GENS)
 @pytest.mark.parametrize("k", [0, 1, 2, 3, 4])
 def test_complete_and_valid(gen, k):
+    if k > KMAX.get(gen, 99):
+        with pytest.raises(sa.SaharaError):
+            sa.scheme_parts(gen, 0, k)
+        return
     for mink in range(0, k + 1):
         pi, l, u = sa.scheme_parts(gen, mink, k)
         P = pi.shape[1]
@@ -56,6 +68,11 @@ def test_complete_and_valid(gen, k):
 @pytest.mark.parametrize("length", [7, 32, 100, 101, 250])
 @pytest.mark.parametrize("ham", [False, True])
 def test_product_scheme_equals_oracle(gen, k, length, ham):
+    if k > KMAX.get(gen, 99):
+        return
+    P = sa.scheme_parts(gen, 0, k)[0].shape[1]
+    if length < P:
+        return
     a = sa.search_scheme(gen, 0, k, length, hamming=ham)
     b = O.scheme(gen, 0, k, length, hamming=ham)
     for x, y in zip(a, b):
@@ -108,3 +125,42 @@ def test_dynamic_partition(gen, k, m, n):
         I = oracle.Index.build(recs, 6)
         h, _ = I.search(pats, (pi, l, u), edit=True)
         assert pset(h) == pset(oracle.bruteforce(recs, pats, k, edit=True))
+
+
+def test_generators_listed_in_reference_order():
+    """list-generators / the error text name the registered generators in the
+    reference's order (search_scheme.cpp:192), a subsequence of it."""
+    names = list(sa.scheme_generators())
+    assert names == [n for n in REFERENCE_ORDER if n in names]
+    assert set(GENS) == set(names)
+
+
+@pytest.mark.parametrize("gen,k,want", [
+    ("lam", 2, [([0, 1, 2], [0, 0, 0], [0, 2, 2]), ([2, 1, 0], [0, 0, 0], [0, 1, 2]), ([1, 0, 2], [0, 0, 1], [0, 1, 2])]),
+    ("kucherov-k1", 1, [([0, 1], [0, 0], [0, 1]), ([1, 0], [0, 1], [0, 1])]),
+    ("pigeon_opt", 2, [([0, 1, 2], [0, 0, 0], [0, 2, 2]), ([1, 2, 0], [0, 0, 1], [0, 1, 2]),
+                       ([2, 1, 0], [0, 1, 2], [0, 1, 2])]),
+    ("suffix", 2, [([0, 1, 2], [0, 0, 0], [0, 1, 2]), ([1, 2, 0], [0, 0, 0], [0, 1, 2]), ([2, 1, 0], [0, 0, 0], [0, 2, 2])]),
+])
+def test_published_shapes(gen, k, want):
+    """Spot values: Lam et al.'s k = 2 scheme and KST's non-redundant k = 1
+    scheme as Kucherov, Salikhov and Tsur (2016) print them (1-based there);
+    the pigeonhole and suffix-filter constructions at k = 2."""
+    pi, l, u = sa.scheme_parts(gen, 0, k)
+    got = [(pi[s].tolist(), l[s].tolist(), u[s].tolist()) for s in range(pi.shape[0])]
+    assert got == want
+
+
+def test_redundancy_where_published_schemes_differ():
+    """pigeon_opt's bounds (the parts left of the first error-free part hold
+    errors) cover each error distribution at most as often as pigeon's, and
+    in total less often; KST's k = 1 scheme is non-redundant, Lam's is not
+    (both search the exact match twice)."""
+    def multiplicity(gen, k):
+        pi, l, u = sa.scheme_parts(gen, 0, k)
+        return [sum(covers(pi[s], l[s], u[s], d) for s in range(pi.shape[0])) for d in dists(pi.shape[1], 0, k)]
+    for k in (1, 2, 3):
+        opt, plain = multiplicity("pigeon_opt", k), multiplicity("pigeon", k)
+        assert min(opt) == 1 and all(a <= b for a, b in zip(opt, plain)) and sum(opt) < sum(plain)
+    assert set(multiplicity("kucherov-k1", 1)) == {1}
+    assert max(multiplicity("lam", 1)) == 2

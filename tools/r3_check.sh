@@ -23,7 +23,7 @@ python3 - "$OUT/bench.json" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1])); c = d["config"]; r = d["roofline"] or {}
 print("value", d["value"], "ms/step", d["ms_per_step"], "kernel", r.get("kernel"), "launch_ms", r.get("launch_ms"), "frac", r.get("frac"))
-print("pcie", {k: (c.get(k) or {}).get("reads_per_s") for k in ("pcie_inclusive", "pcie_inclusive_patterns")},
+print("pcie", {k: (c.get(k) or {}).get("reads_per_s") for k in ("pcie_inclusive", "pcie_inclusive_full_records", "pcie_inclusive_patterns")},
       "same", (c.get("pcie_inclusive") or {}).get("same_hits"), "cpu", (d.get("cpu_baseline") or {}).get("value"),
       "recall", c.get("origin_recall"), "sa", c.get("sa_probe_ok"))
 PY
