@@ -1,0 +1,71 @@
+"""PCIe-inclusive path (sahara_gpu_search_reads_compact) at C3 under several
+knob settings in one process (the library reads its SAHARA_* variables per
+pass), alternating rounds: reads/s per setting.
+
+usage: python tools/pcie_sweep.py [--rounds 2] [--steps 10] [--reads N] NAME=VAR=VAL[,VAR=VAL...] ...
+  e.g. base= b2M=SAHARA_BATCH=2097152 ramp=SAHARA_RAMP=2
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--full", action="store_true", help="whole 24-B records (sahara_gpu_search_reads)")
+    ap.add_argument("settings", nargs="+")
+    a = ap.parse_args()
+    import bench
+    import sahara_amd as sa
+    lens = bench.record_lengths(3_000_000_000, 24)
+    flat, lens = sa.synth_reference(lens, sigma=6, seed=42)
+    idx = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=0)
+    reads = sa.synth_reads(flat, lens, a.reads, 100, 2, sigma=6, seed=7)
+    del flat
+    sch = sa.search_scheme("h2-k2", 0, 2, 100)
+    call = (lambda: sa.search_reads(idx, reads, sch)) if a.full else (lambda: sa.search_reads_compact(idx, reads, sch))
+    sets = []
+    for s in a.settings:
+        name, _, kv = s.partition("=")
+        env = dict(x.split("=", 1) for x in kv.split(",") if x)
+        sets.append((name, env))
+    known = {k for _, env in sets for k in env}
+    res = {n: [] for n, _ in sets}
+    for r in range(a.rounds):
+        for name, env in sets:
+            for k in known:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            for _ in range(2):
+                h = call()
+                del h
+            t = time.perf_counter()
+            st = {"stage_ms": 0.0}
+            h = None
+            for _ in range(a.steps):
+                h = None
+                h = call()
+                st["stage_ms"] += idx.stats()["stage_ms"]
+            el = time.perf_counter() - t
+            n = len(h)
+            del h
+            rps = a.reads * a.steps / el
+            res[name].append(rps)
+            print(f"round {r} {name:12s} {rps/1e6:7.1f}M reads/s  {el*1e3/a.steps:6.2f} ms/call  "
+                  f"packing {st['stage_ms']/a.steps:5.2f} ms  hits {n}", flush=True)
+    for name, v in res.items():
+        print(f"{name:12s} " + " ".join(f"{x/1e6:.1f}" for x in v) + f"  mean {np.mean(v)/1e6:.1f}M")
+
+
+if __name__ == "__main__":
+    main()
