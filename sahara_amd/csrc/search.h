@@ -98,6 +98,8 @@ struct TextArgs {
     uint32_t resolveRows;    // 1: task records carry SA rows; the kernel reads their text positions
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
+    uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
+                             // lane of their wave (with its window and pattern) once this many are idle (0: off)
 };
 
 struct LocateArgs {

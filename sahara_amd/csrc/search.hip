@@ -880,6 +880,56 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             qNext += take;
         }
         if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
+        // ---- work stealing inside the wave once the task queue is dry (wave-
+        // uniform: the queue state is the wave's). A launch ends on its longest
+        // subtrees, each on one lane while the others idle (C5: lanes busy
+        // 0.655 of the time); an idle lane takes the bottom (shallowest, so
+        // largest) stack entry of a busy lane, with that lane's window and
+        // pattern copied slot to slot in LDS, and the task state (pattern id,
+        // window start, scheme row) by shuffle. The DFS of the entry is the
+        // same whichever lane runs it, so the hits are too.
+        if (a.stealAt && qDone && !haveNext && qNext >= qEnd) {
+            const bool thief = !have && sp == 0u;
+            const uint64_t I = __ballot(thief);
+            const uint64_t D = __ballot(sp >= 2u || (sp == 1u && have));
+            const uint32_t nI = (uint32_t)__popcll(I), nD = (uint32_t)__popcll(D);
+            if (nI >= a.stealAt && nD) {  // wave-uniform
+                const uint32_t n = min(nI, nD);
+                const uint32_t r = (uint32_t)__popcll(I & ltMask);
+                // donor of thief rank r: the r-th set bit of D
+                uint32_t donor = 0, rr = r;
+                uint64_t dm = D;
+#pragma unroll
+                for (uint32_t w = 32; w; w >>= 1) {
+                    const uint32_t c = (uint32_t)__popcll(dm & ((1ull << w) - 1ull));
+                    if (rr >= c) { rr -= c; dm >>= w; donor += w; }
+                }
+                const bool takes = thief && r < n;
+                donor = takes ? donor : lane;
+                const uint32_t dPid = __shfl(pid, donor), dWb = __shfl(wb, donor), dBase = __shfl(sBase, donor);
+                const uint32_t dTid = (threadIdx.x & ~63u) | donor;
+                if (takes) {
+                    const uint32_t* src = slot + dTid;
+                    uint32_t* dst = slot + threadIdx.x;
+                    for (uint32_t k = 0; k < 3u * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
+                    const uint2 node = PK ? unpackNode(slot[3u * (winBlocks + patBlocks) * 256u + dTid])
+                                          : reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
+                    cur = node;
+                    pid = dPid;
+                    wb = dWb;
+                    sBase = dBase;
+                    have = true;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // donors (rank < n) drop their bottom entry
+                const bool gives = ((D >> lane) & 1ull) && (uint32_t)__popcll(D & ltMask) < n;
+                if (gives) {
+                    for (uint32_t d = 1; d < sp; ++d) stackPut(d - 1u, stackGet(d));
+                    --sp;
+                }
+            }
+        }
         if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);

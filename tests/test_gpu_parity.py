@@ -485,3 +485,25 @@ def test_long_reads(gpu_device, m, k, gen):
     hit = {(int(q) // 2, int(s), int(p)) for q, s, p, e in fwd}
     assert all(any((i, int(origin[i, 0]), int(origin[i, 1]) + d) in hit for d in range(-k, k + 1))
                for i in range(len(reads)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("steal", ["0", "1", "8", "64"])
+def test_text_phase_work_stealing(gpu_device, monkeypatch, steal):
+    """Idle lanes of a wave take the bottom stack entry (and the window and
+    pattern) of a busy lane once the task queue is dry (SAHARA_STEAL_AT):
+    the hits are the oracle's whatever the threshold, on repeat-rich text
+    (deep subtrees) with k = 3, several small batches (many launch ends)."""
+    monkeypatch.setenv("SAHARA_STEAL_AT", steal)
+    monkeypatch.setenv("SAHARA_BATCH", "333")
+    rng = np.random.default_rng(77)
+    recs = random_records(rng, [30000, 12000], 6, repeats=True)
+    reads = mutate_reads(rng, recs, 400, 80, 3, 6)
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme("h2-k3", 0, 3, 80)
+    want, _ = O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), hits_as_rows(want))
+    gpu.stage(pats, scheme)
+    gpu.run()
+    assert np.array_equal(hits_as_rows(gpu.fetch()), hits_as_rows(want))
