@@ -271,7 +271,8 @@ int  sahara_synth_reads_typed(const uint8_t* ranks, const uint64_t* rec_lens, ui
  * search calls do this themselves): n ranks -> (n + 3) / 4 bytes in out,
  * symbol i at bits 2 (i % 4) of byte i / 4, A C G T coded 0 1 2 3; dna5's N
  * (rank 4 of sigma 6) is coded 0 and its position listed in n_pos (first
- * pos_cap of them), *n_count = how many. scalar != 0 skips the AVX2 packer.
+ * pos_cap of them), *n_count = how many. scalar: 0 the widest SIMD packer the
+ * host has (AVX-512BW, else AVX2), 1 the scalar one, 2 AVX2 at most.
  * Returns 1 if a symbol is no rank in [1, sigma), 0 if all are, -1 on error. */
 int  sahara_pack_2bit(const uint8_t* ranks, uint64_t n, uint32_t sigma, int scalar, uint8_t* out, uint32_t* n_pos,
                       uint64_t pos_cap, uint64_t* n_count);

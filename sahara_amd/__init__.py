@@ -558,8 +558,9 @@ def synth_reads(flat, rec_lens, n_reads, length, errors, sigma=6, seed=7, with_o
 
 
 def pack_2bit(ranks, sigma=6, scalar=False):
-    """Host half of the streamed upload at two bits per symbol (capi.cpp
-    pack2Avx2 / pack2Scalar): (packed bytes, N positions, bad-rank flag)."""
+    """Host half of the streamed upload at two bits per symbol (staging.cpp
+    pack2Avx512 / pack2Avx2 / pack2Scalar): (packed bytes, N positions,
+    bad-rank flag). scalar: False = widest SIMD, True = scalar, 2 = AVX2 at most."""
     r = np.ascontiguousarray(ranks, dtype=np.uint8).ravel()
     out = np.zeros((r.size + 3) // 4, np.uint8)
     cnt = C.c_uint64(0)

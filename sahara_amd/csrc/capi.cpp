@@ -991,8 +991,11 @@ int sahara_pack_2bit(const uint8_t* ranks, uint64_t n, uint32_t sigma, int scala
         if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 or 6");
         if (n >= (1ull << 32)) throw Error("at most 2^32 - 1 symbols per chunk");
         std::vector<uint32_t> pos;
-        const uint64_t acc = (!scalar && hostHasAvx2()) ? pack2Avx2(ranks, out, n, sigma, 0, pos)
-                                                        : pack2Scalar(ranks, out, n, sigma, 0, pos);
+        // scalar: 0 the widest the host has (AVX-512 / AVX2), 1 scalar, 2 AVX2 at most
+        const uint64_t acc = scalar == 1 ? pack2Scalar(ranks, out, n, sigma, 0, pos)
+                             : scalar == 2 ? (hostHasAvx2() ? pack2Avx2(ranks, out, n, sigma, 0, pos)
+                                                            : pack2Scalar(ranks, out, n, sigma, 0, pos))
+                                           : pack2Best(ranks, out, n, sigma, 0, pos);
         bad = acc ? 1 : 0;
         *n_count = pos.size();
         if (n_pos && !pos.empty()) std::memcpy(n_pos, pos.data(), std::min<uint64_t>(pos.size(), pos_cap) * 4);

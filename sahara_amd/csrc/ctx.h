@@ -427,6 +427,11 @@ void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, u
 void textTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,
                const std::vector<uint32_t>& packed, std::vector<uint32_t>& out);
 bool hostHasAvx2();
+bool hostHasAvx512();
+uint64_t pack2Best(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
+                   std::vector<uint32_t>& exc);
+uint64_t pack2Avx512(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
+                     std::vector<uint32_t>& exc);
 uint64_t pack2Scalar(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
                      std::vector<uint32_t>& exc);
 uint64_t pack2Avx2(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,

@@ -286,9 +286,53 @@ __attribute__((target("avx2"))) uint64_t pack2Avx2(const uint8_t* in, uint8_t* o
     return (uint64_t)!_mm256_testz_si256(bad, bad) | pack2Scalar(in + i, out + i / 4, count - i, sigma, base + i, exc);
 }
 
+// The same with AVX-512 (BW), 64 symbols -> 16 bytes per step: rank checks
+// and the N / T recoding in mask registers, the four codes of a byte combined
+// by the same two multiply-adds, and the dwords narrowed to bytes in order
+// (vpmovdb) — about half the AVX2 instructions per byte. The packing of the
+// streamed upload is host-compute bound (one thread packs ~5 GB/s with AVX2),
+// and the GPU box's host (EPYC 9575F, Zen 5) runs 512-bit vectors natively.
+__attribute__((target("avx512f,avx512bw"))) uint64_t pack2Avx512(const uint8_t* in, uint8_t* out, uint64_t count,
+                                                                 uint32_t sigma, uint64_t base,
+                                                                 std::vector<uint32_t>& exc) {
+    const __m512i one = _mm512_set1_epi8(1), three = _mm512_set1_epi8(3), four = _mm512_set1_epi8(4);
+    const __m512i lim = _mm512_set1_epi8((char)(sigma - 2));
+    const __m512i m14 = _mm512_set1_epi16(0x0401), m116 = _mm512_set1_epi32(0x00100001);
+    const bool dna5 = sigma == 6;
+    __mmask64 bad = 0;
+    uint64_t i = 0;
+    for (; i + 64 <= count; i += 64) {
+        __m512i t = _mm512_sub_epi8(_mm512_loadu_si512(reinterpret_cast<const void*>(in + i)), one);
+        bad |= _mm512_cmpgt_epu8_mask(t, lim);
+        if (dna5) {
+            const __mmask64 isN = _mm512_cmpeq_epi8_mask(t, three);
+            for (uint64_t msk = (uint64_t)isN; msk; msk &= msk - 1u)
+                exc.push_back((uint32_t)(base + i + (uint32_t)__builtin_ctzll(msk)));
+            t = _mm512_mask_sub_epi8(t, _mm512_cmpeq_epi8_mask(t, four), t, one);  // T 4 -> 3
+            t = _mm512_maskz_mov_epi8(~isN, t);                                   // N 3 -> 0
+        }
+        t = _mm512_and_si512(t, three);
+        const __m512i d = _mm512_madd_epi16(_mm512_maddubs_epi16(t, m14), m116);
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(out + i / 4), _mm512_cvtepi32_epi8(d));
+    }
+    return (uint64_t)(bad != 0) | pack2Avx2(in + i, out + i / 4, count - i, sigma, base + i, exc);
+}
+
 bool hostHasAvx2() {
     static const bool has = __builtin_cpu_supports("avx2");
     return has;
+}
+
+bool hostHasAvx512() {
+    static const bool has = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512f");
+    return has;
+}
+
+uint64_t pack2Best(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
+                   std::vector<uint32_t>& exc) {
+    if (hostHasAvx512()) return pack2Avx512(in, out, count, sigma, base, exc);
+    if (hostHasAvx2()) return pack2Avx2(in, out, count, sigma, base, exc);
+    return pack2Scalar(in, out, count, sigma, base, exc);
 }
 
 HostPool& hostPool(Ctx* c) {
@@ -335,8 +379,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
             for (uint64_t k = t; k < pieces; k += nt) {  // pieces of 4 MB of symbols (1 MB packed)
                 const uint64_t lo = k * 4 * kPiece, hi = std::min(n, lo + 4 * kPiece);
                 const uint8_t* in = U.src + s0 + lo;
-                const uint64_t acc = avx2 ? pack2Avx2(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k])
-                                          : pack2Scalar(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k]);
+                const uint64_t acc = pack2Best(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k]);
                 if (acc) bad.store(1, std::memory_order_relaxed);
             }
         });

@@ -29,8 +29,8 @@ def _model_pack2(r, sigma):
 
 
 @pytest.mark.parametrize("sigma", [5, 6])
-@pytest.mark.parametrize("n", [0, 1, 3, 4, 127, 128, 129, 1000, 4099])
-@pytest.mark.parametrize("scalar", [False, True])
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 63, 64, 65, 127, 128, 129, 1000, 4099])
+@pytest.mark.parametrize("scalar", [False, True, 2])
 def test_pack_2bit_matches_model(sigma, n, scalar):
     rng = np.random.default_rng(n * 7 + sigma)
     r = rng.integers(1, sigma, n).astype(np.uint8)
@@ -51,6 +51,7 @@ def test_pack_2bit_flags_bad_ranks(sigma, value, where):
     r[where] = value
     assert sa.pack_2bit(r, sigma)[2]
     assert sa.pack_2bit(r, sigma, scalar=True)[2]
+    assert sa.pack_2bit(r, sigma, scalar=2)[2]
     r[where] = sigma  # one past the alphabet
     assert sa.pack_2bit(r, sigma)[2]
 
