@@ -617,7 +617,12 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
     c->sink = nullptr;
     c->sinkCap = 0;
     c->compactSink = c->sinkPinned = false;
-    if (!max_hits) {  // sized from the last call (the bench's steady state), else 2 hits per pattern
+    // --max_hits: per batch on the device (limitBatch), so the limited hits
+    // stream to the host like any others; a multi-part index limits after
+    // its parts merge, on the host (limitHits)
+    const bool hostLimit = max_hits && !c->more.empty();
+    c->limitN = hostLimit ? 0u : max_hits;
+    if (!hostLimit) {  // sized from the last call (the bench's steady state), else 2 hits per pattern
         // a first call takes a pooled buffer if there is one, but pins none:
         // pinning ~1 GB costs ~200 ms, ten times the pageable copy-out
         const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
@@ -653,10 +658,12 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
     const auto tC = clk::now();
     try {
         run(c, false);
+        c->limitN = 0;
         uint32_t bad = 0;
         SH_HIP(hipMemcpy(&bad, c->badFlag.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost));
         if (bad) throw Error("pattern rank out of range for this index");
     } catch (...) {
+        c->limitN = 0;
         drainAll(c);
         if (c->compactSink) {
             try {
@@ -686,7 +693,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
     sahara_hit* buf = c->sink;
     c->sink = nullptr;
     try {
-        if (max_hits) {
+        if (hostLimit) {
             std::vector<sahara_hit> v(c->nout);
             if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
             limitHits(v, max_hits);
@@ -911,7 +918,16 @@ int sahara_gpu_search_best(void* ctx, const uint8_t* ranks, uint64_t n_patterns,
                 src = sub.data();
             }
             stage(c, src, todo.size(), len, pi + off, l + off, u + off, n_searches[j], 1);
-            run(c, false);
+            // --max_hits per batch on the device (single part; the host pass
+            // below is then a no-op on what is left)
+            c->limitN = c->more.empty() ? max_hits : 0u;
+            try {
+                run(c, false);
+            } catch (...) {
+                c->limitN = 0;
+                throw;
+            }
+            c->limitN = 0;
             std::vector<sahara_hit> v(c->nout);
             if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
             acc.search_ms += c->stats.search_ms;

@@ -359,6 +359,12 @@ struct Ctx {
     uint32_t blockWriteBlocks = 64;
     std::vector<uint64_t> batchQ0, batchEnd;
     std::vector<uint64_t> recStartsEnd;   // record starts + the text length (sahara_hit_blocks.rec_starts)
+    // --max_hits n applied per batch on the device (single-part indexes;
+    // limitBatch), 0: off
+    uint32_t limitN = 0;
+    DevBuf<uint32_t> limitCnt;
+    DevBuf<uint64_t> limitOff;
+    DevBuf<sahara_hit> limitBuf;
     // SAHARA_TIMING=2: host-side marks of one call (ms since its start, what)
     bool traceOn = false;
     std::chrono::steady_clock::time_point traceT0;

@@ -525,6 +525,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         }
         sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, q0, c->I.dRecStarts.ptr,
                    (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, c->tmp.ptr, c->tmp.cap, sC);
+        if (c->limitN)  // --max_hits: this batch's queries keep their n best positions (search_n)
+            rows = limitBatch(c->out.ptr + c->nout, rows, c->qoff.ptr, (uint32_t)nb, c->limitN, c->limitCnt,
+                              c->limitOff, c->limitBuf, c->tmp, sC);
         SH_HIP(hipEventRecord(c->ev[4], sC));
         // sahara_gpu_search's host sink: the batch's hits go to host memory
         // on stF while later batches search (while they fit the sink)

@@ -130,6 +130,10 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst
 void launchUnpackNibbles(const uint8_t* nib, uint8_t* dst, uint64_t n, hipStream_t st);
 void launchOffsetSeq(const sahara_hit* in, uint64_t n, uint64_t rec0, sahara_hit* out, hipStream_t st);
+// --max_hits on the device: one batch's hits limited in place, kept rows returned
+uint64_t limitBatch(sahara_hit* out, uint64_t rows, const uint64_t* qoff, uint32_t nq, uint32_t n,
+                    DevBuf<uint32_t>& kcnt, DevBuf<uint64_t>& koff, DevBuf<sahara_hit>& buf, DevBuf<char>& tmp,
+                    hipStream_t st);
 // key / index buffers of the multi-part merge (kept by the context)
 struct MergeBufs {
     DevBuf<uint64_t> k0, k1;

@@ -1744,6 +1744,95 @@ __global__ void kGatherHits(const sahara_hit* __restrict__ in, const uint32_t* _
         out[i] = in[idx[i]];
 }
 
+// --max_hits n on the device (search_n, search.cpp:228,231; the policy U6 of
+// include/sahara_hip.h): per query, of its hits in canonical order, the n
+// distinct (seq_id, pos) with the fewest errors (each once, with its minimum
+// e: the first of its run), ties by (seq_id, pos). One thread per query: the
+// plan counts the distinct positions per error count and fixes the error
+// threshold e* and how many at e* are kept (quota); the write keeps, in
+// order, every first-of-run below e* and the first `quota` at e*.
+struct LimitPlan { uint32_t eStar, quota, kept; };
+__device__ __forceinline__ LimitPlan limitPlan(const sahara_hit* __restrict__ h, uint64_t b, uint64_t e, uint32_t n) {
+    uint32_t hist[16];
+#pragma unroll
+    for (uint32_t x = 0; x < 16; ++x) hist[x] = 0;
+    uint32_t distinct = 0, ps = 0xFFFFFFFFu;
+    uint64_t pp = ~0ull;
+    for (uint64_t i = b; i < e; ++i) {
+        const sahara_hit x = h[i];
+        if (x.seq_id != ps || x.pos != pp) {
+            ++distinct;
+#pragma unroll
+            for (uint32_t v = 0; v < 16; ++v) hist[v] += x.err == v ? 1u : 0u;
+            ps = x.seq_id;
+            pp = x.pos;
+        }
+    }
+    if (distinct <= n) return {16u, 0u, distinct};
+    uint32_t cum = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < 16; ++v) {
+        if (cum < n && cum + hist[v] >= n) return {v, n - cum, n};
+        cum += hist[v];
+    }
+    return {16u, 0u, distinct};  // unreachable: the histogram sums to distinct > n
+}
+
+__global__ void kLimitCount(const sahara_hit* __restrict__ h, const uint64_t* __restrict__ qoff, uint32_t nq,
+                            uint32_t n, uint32_t* __restrict__ kcnt) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q <= nq; q += gridDim.x * blockDim.x)
+        kcnt[q] = q < nq ? limitPlan(h, qoff[q], qoff[q + 1], n).kept : 0u;
+}
+
+__global__ void kLimitWrite(const sahara_hit* __restrict__ h, const uint64_t* __restrict__ qoff, uint32_t nq,
+                            uint32_t n, const uint64_t* __restrict__ koff, sahara_hit* __restrict__ dst) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        const uint64_t b = qoff[q], e = qoff[q + 1];
+        const LimitPlan P = limitPlan(h, b, e, n);
+        uint64_t w = koff[q];
+        uint32_t used = 0, ps = 0xFFFFFFFFu;
+        uint64_t pp = ~0ull;
+        for (uint64_t i = b; i < e; ++i) {
+            const sahara_hit x = h[i];
+            if (x.seq_id == ps && x.pos == pp) continue;
+            ps = x.seq_id;
+            pp = x.pos;
+            const bool keep = x.err < P.eStar || (x.err == P.eStar && used < P.quota);
+            used += x.err == P.eStar && keep ? 1u : 0u;
+            if (keep) dst[w++] = x;
+        }
+    }
+}
+
+// Applies --max_hits n to one batch's hits (out, rows; per-query segments
+// qoff[0..nq]) in place; returns the rows kept. Host-synchronous (the kept
+// total sizes the rest of the batch's chain).
+uint64_t limitBatch(sahara_hit* out, uint64_t rows, const uint64_t* qoff, uint32_t nq, uint32_t n,
+                    DevBuf<uint32_t>& kcnt, DevBuf<uint64_t>& koff, DevBuf<sahara_hit>& buf, DevBuf<char>& tmp,
+                    hipStream_t st) {
+    if (rows == 0 || nq == 0) return rows;
+    kcnt.reserve((size_t)nq + 1);
+    koff.reserve((size_t)nq + 1);
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((nq + 256) / 256, 16384));
+    hipLaunchKernelGGL(kLimitCount, dim3(blocks), dim3(256), 0, st, out, qoff, nq, n, kcnt.ptr);
+    SH_HIP(hipGetLastError());
+    size_t bytes = 0;
+    SH_HIP(rocprim::exclusive_scan(nullptr, bytes, kcnt.ptr, koff.ptr, (uint64_t)0, (size_t)nq + 1,
+                                   rocprim::plus<uint64_t>(), st));
+    tmp.reserve(bytes + 256);
+    SH_HIP(rocprim::exclusive_scan(tmp.ptr, bytes, kcnt.ptr, koff.ptr, (uint64_t)0, (size_t)nq + 1,
+                                   rocprim::plus<uint64_t>(), st));
+    uint64_t kept = 0;
+    SH_HIP(hipMemcpyAsync(&kept, koff.ptr + nq, 8, hipMemcpyDeviceToHost, st));
+    SH_HIP(hipStreamSynchronize(st));
+    if (kept == rows) return rows;  // nothing to drop in this batch
+    buf.reserve(std::max<uint64_t>(kept, 1));
+    hipLaunchKernelGGL(kLimitWrite, dim3(blocks), dim3(256), 0, st, out, qoff, nq, n, koff.ptr, buf.ptr);
+    SH_HIP(hipGetLastError());
+    if (kept) SH_HIP(hipMemcpyAsync(out, buf.ptr, kept * sizeof(sahara_hit), hipMemcpyDeviceToDevice, st));
+    return kept;
+}
+
 // Stable sort of hit records by qid (rocPRIM's LSD radix sort is stable):
 // the parts' hits, each part in canonical order and every part's records
 // after the previous part's, come out in canonical (qid, seq_id, pos, err)

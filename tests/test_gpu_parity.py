@@ -507,3 +507,29 @@ def test_text_phase_work_stealing(gpu_device, monkeypatch, steal):
     gpu.stage(pats, scheme)
     gpu.run()
     assert np.array_equal(hits_as_rows(gpu.fetch()), hits_as_rows(want))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 5])
+def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
+    """--max_hits n limited per batch on the device (search.hip limitBatch)
+    equals the documented policy (include/sahara_hip.h, test_golden's
+    limit_rows) over the oracle's hits: repeat-rich text (queries with many
+    positions and several error counts), several batches, reads and
+    patterns calls, and besthits."""
+    from test_golden import limit_rows
+    monkeypatch.setenv("SAHARA_BATCH", "257")
+    rng = np.random.default_rng(40 + n)
+    recs = random_records(rng, [25000, 8000], 6, repeats=True)
+    reads = mutate_reads(rng, recs, 500, 50, 2, 6)
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme("h2-k2", 0, 2, 50)
+    ref = O.Index.build(recs, 6, 16)
+    want, _ = ref.search(pats, scheme, edit=True, nthreads=8)
+    want = limit_rows(hits_as_rows(want), n)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, max_hits=n)), want)
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
+    best = [sa.search_scheme("h2-k2", j, j, 50) for j in range(3)]
+    bw = O.search_best(ref, pats, best, nthreads=8)
+    assert np.array_equal(hits_as_rows(sa.search_best(gpu, pats, best, max_hits=n)), limit_rows(hits_as_rows(bw), n))

@@ -33,6 +33,8 @@ def main():
     reads = sa.synth_reads(flat, lens, a.reads, 100, 2, sigma=6, seed=7)
     del flat
     sch = sa.search_scheme("h2-k2", 0, 2, 100)
+    aff = sorted(os.sched_getaffinity(0))
+    print(f"placement {idx.placement()}, process CPUs {len(aff)} ({aff[:4]}..{aff[-4:]})", flush=True)
     call = (lambda: sa.search_reads(idx, reads, sch)) if a.full else (lambda: sa.search_reads_compact(idx, reads, sch))
     sets = []
     for s in a.settings:
