@@ -212,8 +212,10 @@ int  sahara_gpu_stats(void* ctx, sahara_stats* stats);
 /* Where a context runs: the HIP device it opened (SAHARA_DEVICE_MAP may remap
  * the device argument of sahara_gpu_open / _build, a test hook), the NUMA node
  * of that device (-1 unknown) and the number of host CPUs of that node the
- * context's own threads (packing pool, finisher, hit expander) are bound to
- * (0: not bound; SAHARA_NUMA=0 turns binding off). Any pointer may be NULL. */
+ * context's own threads that touch its pinned buffers (finisher, hit
+ * expander, ring pinning) are bound to (0: not bound; SAHARA_NUMA=0 turns
+ * binding off). The packing threads read the caller's buffers and stay
+ * unbound (SAHARA_PACK_BIND=1 binds them too). Any pointer may be NULL. */
 int  sahara_gpu_placement(void* ctx, int* device, int* numa_node, int* n_cpus);
 
 /* Releases a hit buffer returned by sahara_gpu_search / sahara_gpu_search_best.

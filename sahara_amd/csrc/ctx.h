@@ -25,12 +25,11 @@ namespace sahara {
 
 extern thread_local std::string g_err;  // sahara_gpu_last_error
 
-// NUMA placement of a context's own host threads (the packing pool, the
-// pass's finisher, the hit expander, the ring pinning): the CPUs of the NUMA
-// node the GPU hangs off (/sys/bus/pci/devices/<bdf>/numa_node), as far as
-// the process may use them. The streamed path is host-memory-bandwidth bound
-// (DESIGN.md §3.6, §5); with 8 GPUs each context's packing must read its
-// reads from, and write its pinned ring in, the node next to its GPU.
+// NUMA placement of a context's own host threads that touch its pinned
+// buffers (the pass's finisher, the hit expander, the ring pinning): the CPUs
+// of the NUMA node the GPU hangs off (/sys/bus/pci/devices/<bdf>/numa_node),
+// as far as the process may use them. The packing pool reads the caller's
+// buffers, wherever those are, and stays unbound (staging.cpp hostPool).
 // node = -1 (unknown, or SAHARA_NUMA=0): threads stay where the OS puts them.
 struct Placement {
     int node = -1;

@@ -253,7 +253,12 @@ uint64_t pack2Scalar(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t s
 // The same with AVX2, 128 symbols -> 32 bytes per step: codes t = rank - 1
 // (dna5: T 4 -> 3, N 3 -> 0 and listed from a byte mask), pairs combined by
 // one multiply-add (t0 + 4 t1), pairs of pairs by another (+ 16), packed to
-// bytes and put back in order with one cross-lane permute.
+// bytes and put back in order with one cross-lane permute. The N masks of a
+// 16 KB sub-block are kept in a local array and listed after it: a possible
+// call (vector growth) inside the vector loop made the compiler spill and
+// reload the vector constants and pointers every step (3x slower).
+constexpr uint64_t kPackSub = 16384;  // symbols per sub-block
+
 __attribute__((target("avx2"))) uint64_t pack2Avx2(const uint8_t* in, uint8_t* out, uint64_t count,
                                                           uint32_t sigma, uint64_t base, std::vector<uint32_t>& exc) {
     const __m256i one = _mm256_set1_epi8(1), three = _mm256_set1_epi8(3), four = _mm256_set1_epi8(4);
@@ -263,25 +268,32 @@ __attribute__((target("avx2"))) uint64_t pack2Avx2(const uint8_t* in, uint8_t* o
     const bool dna5 = sigma == 6;
     __m256i bad = _mm256_setzero_si256();
     uint64_t i = 0;
-    for (; i + 128 <= count; i += 128) {
-        __m256i d[4];
-        for (int q = 0; q < 4; ++q) {
-            __m256i t = _mm256_sub_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + i + 32 * q)), one);
-            bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(t, lim), lim));
-            if (dna5) {
-                const __m256i isN = _mm256_cmpeq_epi8(t, three);
-                uint32_t msk = (uint32_t)_mm256_movemask_epi8(isN);
-                while (msk) {
-                    exc.push_back((uint32_t)(base + i + 32 * q + (uint32_t)__builtin_ctz(msk)));
-                    msk &= msk - 1u;
+    uint32_t nmask[kPackSub / 32], noff[kPackSub / 32];
+    while (i + 128 <= count) {
+        const uint64_t end = std::min(count & ~uint64_t(127), i + kPackSub);
+        uint32_t nn = 0;
+        for (; i < end; i += 128) {
+            __m256i d[4];
+            for (int q = 0; q < 4; ++q) {
+                __m256i t = _mm256_sub_epi8(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + i + 32 * q)), one);
+                bad = _mm256_or_si256(bad, _mm256_xor_si256(_mm256_max_epu8(t, lim), lim));
+                if (dna5) {
+                    const __m256i isN = _mm256_cmpeq_epi8(t, three);
+                    const uint32_t msk = (uint32_t)_mm256_movemask_epi8(isN);
+                    nmask[nn] = msk;
+                    noff[nn] = (uint32_t)(i + 32 * q);
+                    nn += msk ? 1u : 0u;
+                    t = _mm256_andnot_si256(isN, _mm256_add_epi8(t, _mm256_cmpeq_epi8(t, four)));
                 }
-                t = _mm256_andnot_si256(isN, _mm256_add_epi8(t, _mm256_cmpeq_epi8(t, four)));
+                t = _mm256_and_si256(t, three);
+                d[q] = _mm256_madd_epi16(_mm256_maddubs_epi16(t, m14), m116);
             }
-            t = _mm256_and_si256(t, three);
-            d[q] = _mm256_madd_epi16(_mm256_maddubs_epi16(t, m14), m116);
+            const __m256i b = _mm256_packus_epi16(_mm256_packus_epi32(d[0], d[1]), _mm256_packus_epi32(d[2], d[3]));
+            _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i / 4), _mm256_permutevar8x32_epi32(b, order));
         }
-        const __m256i b = _mm256_packus_epi16(_mm256_packus_epi32(d[0], d[1]), _mm256_packus_epi32(d[2], d[3]));
-        _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + i / 4), _mm256_permutevar8x32_epi32(b, order));
+        for (uint32_t k = 0; k < nn; ++k)
+            for (uint32_t msk = nmask[k]; msk; msk &= msk - 1u)
+                exc.push_back((uint32_t)(base + noff[k] + (uint32_t)__builtin_ctz(msk)));
     }
     return (uint64_t)!_mm256_testz_si256(bad, bad) | pack2Scalar(in + i, out + i / 4, count - i, sigma, base + i, exc);
 }
@@ -289,9 +301,7 @@ __attribute__((target("avx2"))) uint64_t pack2Avx2(const uint8_t* in, uint8_t* o
 // The same with AVX-512 (BW), 64 symbols -> 16 bytes per step: rank checks
 // and the N / T recoding in mask registers, the four codes of a byte combined
 // by the same two multiply-adds, and the dwords narrowed to bytes in order
-// (vpmovdb) — about half the AVX2 instructions per byte. The packing of the
-// streamed upload is host-compute bound (one thread packs ~5 GB/s with AVX2),
-// and the GPU box's host (EPYC 9575F, Zen 5) runs 512-bit vectors natively.
+// (vpmovdb). N masks listed per sub-block as above.
 __attribute__((target("avx512f,avx512bw"))) uint64_t pack2Avx512(const uint8_t* in, uint8_t* out, uint64_t count,
                                                                  uint32_t sigma, uint64_t base,
                                                                  std::vector<uint32_t>& exc) {
@@ -301,19 +311,29 @@ __attribute__((target("avx512f,avx512bw"))) uint64_t pack2Avx512(const uint8_t* 
     const bool dna5 = sigma == 6;
     __mmask64 bad = 0;
     uint64_t i = 0;
-    for (; i + 64 <= count; i += 64) {
-        __m512i t = _mm512_sub_epi8(_mm512_loadu_si512(reinterpret_cast<const void*>(in + i)), one);
-        bad |= _mm512_cmpgt_epu8_mask(t, lim);
-        if (dna5) {
-            const __mmask64 isN = _mm512_cmpeq_epi8_mask(t, three);
-            for (uint64_t msk = (uint64_t)isN; msk; msk &= msk - 1u)
-                exc.push_back((uint32_t)(base + i + (uint32_t)__builtin_ctzll(msk)));
-            t = _mm512_mask_sub_epi8(t, _mm512_cmpeq_epi8_mask(t, four), t, one);  // T 4 -> 3
-            t = _mm512_maskz_mov_epi8(~isN, t);                                   // N 3 -> 0
+    uint64_t nmask[kPackSub / 64];
+    uint32_t noff[kPackSub / 64];
+    while (i + 64 <= count) {
+        const uint64_t end = std::min(count & ~uint64_t(63), i + kPackSub);
+        uint32_t nn = 0;
+        for (; i < end; i += 64) {
+            __m512i t = _mm512_sub_epi8(_mm512_loadu_si512(reinterpret_cast<const void*>(in + i)), one);
+            bad |= _mm512_cmpgt_epu8_mask(t, lim);
+            if (dna5) {
+                const __mmask64 isN = _mm512_cmpeq_epi8_mask(t, three);
+                nmask[nn] = (uint64_t)isN;
+                noff[nn] = (uint32_t)i;
+                nn += isN ? 1u : 0u;
+                t = _mm512_mask_sub_epi8(t, _mm512_cmpeq_epi8_mask(t, four), t, one);  // T 4 -> 3
+                t = _mm512_maskz_mov_epi8(~isN, t);                                   // N 3 -> 0
+            }
+            t = _mm512_and_si512(t, three);
+            const __m512i d = _mm512_madd_epi16(_mm512_maddubs_epi16(t, m14), m116);
+            _mm_storeu_si128(reinterpret_cast<__m128i*>(out + i / 4), _mm512_cvtepi32_epi8(d));
         }
-        t = _mm512_and_si512(t, three);
-        const __m512i d = _mm512_madd_epi16(_mm512_maddubs_epi16(t, m14), m116);
-        _mm_storeu_si128(reinterpret_cast<__m128i*>(out + i / 4), _mm512_cvtepi32_epi8(d));
+        for (uint32_t k = 0; k < nn; ++k)
+            for (uint64_t msk = nmask[k]; msk; msk &= msk - 1u)
+                exc.push_back((uint32_t)(base + noff[k] + (uint32_t)__builtin_ctzll(msk)));
     }
     return (uint64_t)(bad != 0) | pack2Avx2(in + i, out + i / 4, count - i, sigma, base + i, exc);
 }
@@ -336,7 +356,17 @@ uint64_t pack2Best(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sig
 }
 
 HostPool& hostPool(Ctx* c) {
-    if (!c->pool) c->pool = std::make_unique<HostPool>(hostThreads(c, 16) - 1, &c->place);
+    // The packing threads read the caller's reads wherever their pages are,
+    // so they stay unbound (SAHARA_PACK_BIND=1: on the GPU's node like the
+    // context's other threads). Measured on the GPU box (2 NUMA nodes, 16 CPUs
+    // of quota; tools/probe/pack_bench numa): 16 threads bound to the GPU's
+    // node pack 250 GB/s of input on that node but 65 GB/s of input on the
+    // other; unbound they pack 194-210 GB/s either way.
+    if (!c->pool) {
+        const char* e = std::getenv("SAHARA_PACK_BIND");
+        const bool bind = e && std::atoi(e) != 0;
+        c->pool = std::make_unique<HostPool>(hostThreads(c, 16) - 1, bind ? &c->place : nullptr);
+    }
     return *c->pool;
 }
 
@@ -371,13 +401,17 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     if (bits != 8) SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
     uint8_t* out = c->ring + slot * Ctx::kRingSlot;
     if (bits == 2) {
-        const uint64_t n = s1 - s0, pieces = (n + 4 * kPiece - 1) / (4 * kPiece);
+        // symbols per piece (SAHARA_PACK_PIECE, a multiple of 4): a chunk's
+        // pieces spread over the pool's threads
+        uint64_t pieceSyms = 4 * kPiece;
+        if (const char* e = std::getenv("SAHARA_PACK_PIECE")) pieceSyms = std::max<uint64_t>(4096, std::atoll(e)) & ~uint64_t(3);
+        const uint64_t n = s1 - s0, pieces = (n + pieceSyms - 1) / pieceSyms;
         // one N list per piece: concatenated in piece order they are sorted
         if (c->excParts.size() < pieces) c->excParts.resize(pieces);
         for (auto& v : c->excParts) v.clear();
         P.run([&](unsigned t) {
             for (uint64_t k = t; k < pieces; k += nt) {  // pieces of 4 MB of symbols (1 MB packed)
-                const uint64_t lo = k * 4 * kPiece, hi = std::min(n, lo + 4 * kPiece);
+                const uint64_t lo = k * pieceSyms, hi = std::min(n, lo + pieceSyms);
                 const uint8_t* in = U.src + s0 + lo;
                 const uint64_t acc = pack2Best(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k]);
                 if (acc) bad.store(1, std::memory_order_relaxed);

@@ -3,6 +3,8 @@
 // by T threads, with and without software prefetch, AVX2 and AVX-512.
 // Build: g++ -O3 -std=c++17 -pthread tools/probe/pack_bench.cpp -o tools/probe/pack_bench
 #include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <chrono>
 #include <cstdint>
@@ -62,6 +64,55 @@ __attribute__((target("avx512f,avx512bw"))) uint64_t pack512(const uint8_t* in, 
     return nN + (bad != 0);
 }
 
+static void bindTo(int node) {  // GPU box: node 0 = CPUs 0-63, node 1 = 64-127 (+ SMT siblings 128-255)
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c = 0; c < 64; ++c) {
+        CPU_SET(node * 64 + c, &set);
+        CPU_SET(128 + node * 64 + c, &set);
+    }
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+// The library's pattern: T threads bound to `packNode` take 4 MB pieces round
+// robin, input first touched by a thread on `dataNode`.
+static void numaCase(uint64_t n, int dataNode, int packNode, unsigned T) {
+    uint8_t* in = nullptr;
+    uint8_t* out = nullptr;
+    std::thread([&] {
+        bindTo(dataNode);
+        in = static_cast<uint8_t*>(std::malloc(n));
+        out = static_cast<uint8_t*>(std::malloc(n / 4 + 64));
+        std::mt19937_64 g(1);
+        const uint8_t code[4] = {1, 2, 3, 5};
+        for (uint64_t i = 0; i < n; i += 32) {
+            uint64_t x = g();
+            for (int j = 0; j < 32 && i + j < n; ++j) in[i + j] = code[(x >> (2 * j)) & 3];
+        }
+        std::memset(out, 0, n / 4 + 64);
+    }).join();
+    const uint64_t piece = 4u << 20, np = (n + piece - 1) / piece;
+    double best = 1e9;
+    for (int rep = 0; rep < 3; ++rep) {
+        std::vector<std::thread> th;
+        auto t0 = std::chrono::steady_clock::now();
+        for (unsigned t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                if (packNode >= 0) bindTo(packNode);
+                for (uint64_t k = t; k < np; k += T) {
+                    const uint64_t b = k * piece, e = std::min(n, b + piece);
+                    volatile uint64_t r = pack512<false>(in + b, out + b / 4, e - b);
+                    (void)r;
+                }
+            });
+        for (auto& x : th) x.join();
+        best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::printf("pieces: data node %d, pack threads %u on node %d: %7.1f GB/s\n", dataNode, T, packNode, n / best / 1e9);
+    std::free(in);
+    std::free(out);
+}
+
 int main(int argc, char** argv) {
     const uint64_t n = (argc > 1 ? std::atoll(argv[1]) : 1024) << 20;
     std::vector<uint8_t> in(n), out(n / 4 + 64);
@@ -75,6 +126,12 @@ int main(int argc, char** argv) {
     const bool has512 = __builtin_cpu_supports("avx512bw");
     std::printf("cpus %u, avx512bw %d, %llu MB\n", std::thread::hardware_concurrency(), has512 ? 1 : 0,
                 (unsigned long long)(n >> 20));
+    if (argc > 2) {
+        for (unsigned T : {8u, 16u})
+            for (int dn : {0, 1})
+                for (int pn : {0, 1, -1}) numaCase(n, dn, pn, T);
+        return 0;
+    }
     for (unsigned T : {1u, 4u, 8u, 16u}) {
         for (int v = 0; v < 4; ++v) {
             if (v >= 2 && !has512) continue;
