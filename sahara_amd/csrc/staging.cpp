@@ -399,6 +399,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     uint32_t bits = U.bits;
     uint64_t nExc = 0, excOff = 0;  // 2 bits: the N list, at byte excOff of the chunk's region
     if (bits != 8) SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
+    c->mark("slot free", j);
     uint8_t* out = c->ring + slot * Ctx::kRingSlot;
     if (bits == 2) {
         // symbols per piece (SAHARA_PACK_PIECE, a multiple of 4): a chunk's
@@ -418,6 +419,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
             }
         });
         for (auto& v : c->excParts) nExc += v.size();
+        c->mark("pack cpu done", r0 / U.chunk);
         excOff = ((b0 + (n + 3) / 4 + 3) & ~uint64_t(3)) - b0;  // 4-aligned on the device
         if (excOff + 4 * nExc > b1 - b0) {
             bits = 4;  // N-rich chunk: the list would not fit, go as nibbles
@@ -428,6 +430,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
                 e += v.size() * 4;
             }
             SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, excOff + 4 * nExc, hipMemcpyHostToDevice, c->stE));
+            c->mark("dma enqueued", r0 / U.chunk);
         }
     }
     if (bits == 4 && !bad.load()) {

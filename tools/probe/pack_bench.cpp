@@ -1,7 +1,10 @@
 // Host packing throughput probe for the streamed upload (staging.cpp
 // pack2Avx2 / pack2Avx512): 1 GB of dna5 ranks packed to 2 bits per symbol
 // by T threads, with and without software prefetch, AVX2 and AVX-512.
-// Build: g++ -O3 -std=c++17 -pthread tools/probe/pack_bench.cpp -o tools/probe/pack_bench
+// Build: hipcc -O3 -std=c++17 -pthread tools/probe/pack_bench.cpp -o tools/probe/pack_bench
+// (`pack_bench <MB> numa [pinned]`: NUMA cases; pinned = the output in
+// hipHostMalloc memory like the library's upload ring)
+#include <hip/hip_runtime.h>
 #include <immintrin.h>
 #include <pthread.h>
 #include <sched.h>
@@ -12,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -76,13 +80,20 @@ static void bindTo(int node) {  // GPU box: node 0 = CPUs 0-63, node 1 = 64-127 
 
 // The library's pattern: T threads bound to `packNode` take 4 MB pieces round
 // robin, input first touched by a thread on `dataNode`.
+static bool g_pinned = false;
 static void numaCase(uint64_t n, int dataNode, int packNode, unsigned T) {
     uint8_t* in = nullptr;
     uint8_t* out = nullptr;
     std::thread([&] {
         bindTo(dataNode);
         in = static_cast<uint8_t*>(std::malloc(n));
-        out = static_cast<uint8_t*>(std::malloc(n / 4 + 64));
+        if (g_pinned) {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, n / 4 + 64, hipHostMallocPortable) != hipSuccess) std::abort();
+            out = static_cast<uint8_t*>(p);
+        } else {
+            out = static_cast<uint8_t*>(std::malloc(n / 4 + 64));
+        }
         std::mt19937_64 g(1);
         const uint8_t code[4] = {1, 2, 3, 5};
         for (uint64_t i = 0; i < n; i += 32) {
@@ -108,9 +119,11 @@ static void numaCase(uint64_t n, int dataNode, int packNode, unsigned T) {
         for (auto& x : th) x.join();
         best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
-    std::printf("pieces: data node %d, pack threads %u on node %d: %7.1f GB/s\n", dataNode, T, packNode, n / best / 1e9);
+    std::printf("pieces: data node %d, pack threads %u on node %d, out %s: %7.1f GB/s\n", dataNode, T, packNode,
+                g_pinned ? "pinned" : "malloc", n / best / 1e9);
     std::free(in);
-    std::free(out);
+    if (g_pinned) (void)hipHostFree(out);
+    else std::free(out);
 }
 
 int main(int argc, char** argv) {
@@ -127,6 +140,7 @@ int main(int argc, char** argv) {
     std::printf("cpus %u, avx512bw %d, %llu MB\n", std::thread::hardware_concurrency(), has512 ? 1 : 0,
                 (unsigned long long)(n >> 20));
     if (argc > 2) {
+        g_pinned = argc > 3 && std::string(argv[3]) == "pinned";
         for (unsigned T : {8u, 16u})
             for (int dn : {0, 1})
                 for (int pn : {0, 1, -1}) numaCase(n, dn, pn, T);
