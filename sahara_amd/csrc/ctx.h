@@ -293,7 +293,7 @@ struct Ctx {
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
     DevBuf<uint64_t> partial;             // tile sums of the segment scan
-    DevBuf<uint32_t> qcnt, big;           // per-query row counts (zero between batches); long segments
+    DevBuf<uint32_t> qcnt, big, huge;     // per-query row counts (zero between batches); long / huge segments
     DevBuf<uint32_t> hrank;               // per reported cursor: its first row's slot in its query's segment
     DevBuf<char> tmp;
     DevBuf<sahara_hit> out;

@@ -265,6 +265,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->qcnt.reserve(maxBatch + 1);
         c->qoff.reserve(maxBatch + 1);
         c->big.reserve(maxBatch);
+        c->huge.reserve(maxBatch);
     }
     SH_HIP(hipMemsetAsync(c->qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
     hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
@@ -484,16 +485,23 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->partial.reserve(scanTiles((uint32_t)nb));
         c->hrank.reserve(std::max<uint64_t>(nh, 1));
         querySegments(sl.hits.ptr, nh, c->qcnt.ptr, c->hrank.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr,
-                      c->big.ptr, c->small.ptr + 4, sC);
+                      c->big.ptr, c->small.ptr + 4, c->huge.ptr, c->small.ptr + 5, sC);
         uint64_t rows = 0;
-        uint32_t nbig = 0;
+        uint32_t nbig2[2] = {0, 0};  // long segments, huge ones
         SH_HIP(hipMemcpyAsync(&rows, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
-        SH_HIP(hipMemcpyAsync(&nbig, c->small.ptr + 4, 4, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipMemcpyAsync(nbig2, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipStreamSynchronize(sC));
         c->mark("rows", b);
         if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
+        uint32_t nbig = nbig2[0], nhuge = nbig2[1];
+        const uint32_t* hugeList = c->huge.ptr;
+        if (const char* v = getenv("SAHARA_LDS_SORT"); v && v[0] == '0') {  // A/B: every long segment by radix sort
+            hugeList = c->big.ptr;
+            nhuge = nbig;
+            nbig = 0;
+        }
         c->k0.reserve(std::max<uint64_t>(rows, 1));
-        if (nbig) c->k1.reserve(std::max<uint64_t>(rows, 1));
+        if (nhuge) c->k1.reserve(std::max<uint64_t>(rows, 1));
         LocateArgs la{};
         la.hits = sl.hits.ptr;
         la.nhits = nh;
@@ -511,7 +519,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         launchLocate(la, count, sC);
         SH_HIP(hipEventRecord(c->ev[3], sC));
         resetSlot(sl, sC);  // the slot's hits are consumed
-        if (nbig) c->tmp.reserve(bigSortTempBytes(rows, nbig) + 256);
+        if (nhuge) c->tmp.reserve(bigSortTempBytes(rows, nhuge) + 256);
         if (c->nout + rows > c->out.cap) {  // grow the device-resident output
             const size_t want = std::max<size_t>((c->nout + rows) + (c->nout + rows) / 2, 1024);
             sahara_hit* np = nullptr;
@@ -523,8 +531,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             c->out.ptr = np;
             c->out.cap = want;
         }
-        sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, q0, c->I.dRecStarts.ptr,
-                   (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, c->tmp.ptr, c->tmp.cap, sC);
+        sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, hugeList, nhuge, q0,
+                   c->I.dRecStarts.ptr, (uint32_t)c->I.recStarts.size(), c->out.ptr + c->nout, c->tmp.ptr, c->tmp.cap,
+                   sC);
         if (c->limitN)  // --max_hits: this batch's queries keep their n best positions (search_n)
             rows = limitBatch(c->out.ptr + c->nout, rows, c->qoff.ptr, (uint32_t)nb, c->limitN, c->limitCnt,
                               c->limitOff, c->limitBuf, c->tmp, sC);

@@ -156,16 +156,19 @@ void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, ui
 // locate + canonical order, per batch: querySegments (rows per query ->
 // segments; long segments listed in big, their count in *nbig, read back by
 // the host), launchLocate (keys into the segments), sortDecode (short
-// segments in registers, medium across a wave, long by segmented radix sort).
+// segments in registers, medium across a wave, long in LDS, huge by segmented
+// radix sort).
 uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
 // qcnt: all zero on entry and on return; rank: one slot per hit
 void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* rank, uint32_t nq, uint64_t* qoff,
-                   uint64_t* partial, uint32_t* big, uint32_t* nbig, hipStream_t st);
+                   uint64_t* partial, uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
 size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
+// long segments (> 64 rows, listed in big) are sorted in LDS, huge ones
+// (> 2048, listed in huge) by the segmented radix sort
 void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff, uint32_t nq, const uint32_t* big,
-                uint32_t nbig, uint64_t qidBase, const uint64_t* starts, uint32_t nrec, sahara_hit* out, void* tmp,
-                size_t tmpBytes, hipStream_t st);
+                uint32_t nbig, const uint32_t* huge, uint32_t nhuge, uint64_t qidBase, const uint64_t* starts,
+                uint32_t nrec, sahara_hit* out, void* tmp, size_t tmpBytes, hipStream_t st);
 void launchPackPatterns3(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patBlocks, uint4* dst,
                          hipStream_t st);
 void launchDigest(const sahara_hit* h, uint64_t n, unsigned long long* out, hipStream_t st);

@@ -1176,6 +1176,9 @@ __global__ void kCountRows(const uint4* __restrict__ hits, uint64_t nhits, uint3
 // ones by the segmented radix sort.
 constexpr uint32_t kSmallSeg = 8;
 constexpr uint32_t kMediumSeg = 64;
+// long segments of <= kLdsSeg rows: one workgroup each, bitonic sort in 16 KB
+// of LDS (kSortBigLds); longer ones ("huge"): the segmented radix sort
+constexpr uint32_t kLdsSeg = 2048;
 
 // Exclusive scan of the per-query row counts (n = queries + 1 entries, the
 // last one 0) into u64 segment offsets, reduce-then-scan over tiles of
@@ -1234,7 +1237,8 @@ __global__ __launch_bounds__(256) void kScanPartials(uint64_t* __restrict__ part
 
 __global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, uint32_t n,
                                                  const uint64_t* __restrict__ partial, uint64_t* __restrict__ off,
-                                                 uint32_t* __restrict__ list, uint32_t* __restrict__ nlist) {
+                                                 uint32_t* __restrict__ list, uint32_t* __restrict__ nlist,
+                                                 uint32_t* __restrict__ huge, uint32_t* __restrict__ nhuge) {
     __shared__ uint64_t wsum[4];
     __shared__ uint32_t llist[kScanTile];
     __shared__ uint32_t lcnt, lbase;
@@ -1257,6 +1261,7 @@ __global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, ui
             if ((int)lane == leader) wb = atomicAdd(&lcnt, (uint32_t)__popcll(m));
             wb = __shfl(wb, leader);
             if (v > kMediumSeg) llist[wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+            if (v > kLdsSeg) huge[atomicAdd(nhuge, 1u)] = i;  // rare: past the LDS sort (kSortBigLds)
         }
     }
     __syncthreads();
@@ -1495,6 +1500,46 @@ __global__ __launch_bounds__(256) void kDecodeBig(const uint64_t* __restrict__ k
         const uint32_t q = big[s];
         const uint64_t b = qoff[q], e = qoff[q + 1];
         for (uint64_t i = b + threadIdx.x; i < e; i += blockDim.x) out[i] = decodeKey(keys[i], qidBase + q, starts, nrec);
+    }
+}
+
+// Long segments (kMediumSeg < rows <= kLdsSeg): one workgroup per segment,
+// keys padded to a power of two with ~0 in LDS, bitonic sort, decoded hits
+// written in order. 16 KB of LDS and no scratch in HBM: it fits beside the
+// text phase's workgroups, where rocPRIM's segmented radix sort (whose blocks
+// need more LDS than the text phase leaves free) waited for the text launch
+// to drain, up to 1.3 ms per batch at C3 (profiles/r03_v5_c3_timeline.txt).
+__global__ __launch_bounds__(256) void kSortBigLds(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ qoff,
+                                                  const uint32_t* __restrict__ big, uint32_t nbig, uint64_t qidBase,
+                                                  const uint64_t* __restrict__ starts, uint32_t nrec,
+                                                  sahara_hit* __restrict__ out) {
+    __shared__ uint64_t K[kLdsSeg];
+    for (uint32_t s = blockIdx.x; s < nbig; s += gridDim.x) {
+        const uint32_t q = big[s];
+        const uint64_t b = qoff[q], e = qoff[q + 1];
+        const uint32_t n = (uint32_t)(e - b);
+        if (n > kLdsSeg) continue;  // a huge segment: the radix sort path (block-uniform)
+        uint32_t P = 1;
+        while (P < n) P <<= 1;
+        for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) K[i] = i < n ? keys[b + i] : ~0ull;
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                    const uint32_t p = i ^ j;
+                    if (p > i) {
+                        const uint64_t x = K[i], y = K[p];
+                        const bool up = (i & k) == 0;
+                        if ((x > y) == up) {
+                            K[i] = y;
+                            K[p] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) out[b + i] = decodeKey(K[i], qidBase + q, starts, nrec);
+        __syncthreads();
     }
 }
 
@@ -2046,7 +2091,7 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
 }
 
 void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* rank, uint32_t nq, uint64_t* qoff,
-                   uint64_t* partial, uint32_t* big, uint32_t* nbig, hipStream_t st) {
+                   uint64_t* partial, uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
     // qcnt[nq] stays 0, so qoff[nq] = total rows
     if (nhits) {
         const uint64_t blocks = std::min<uint64_t>((nhits + 255) / 256, 65536);
@@ -2056,7 +2101,7 @@ void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* 
     const uint32_t n = nq + 1, tiles = (n + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, n, partial);
     hipLaunchKernelGGL(kScanPartials, dim3(1), dim3(256), 0, st, partial, tiles);
-    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, n, partial, qoff, big, nbig);
+    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, n, partial, qoff, big, nbig, huge, nhuge);
     SH_HIP(hipGetLastError());
 }
 
@@ -2080,20 +2125,25 @@ size_t bigSortTempBytes(uint64_t rows, uint32_t nbig) {
 }
 
 void sortDecode(uint64_t* k0, uint64_t* k1, uint64_t rows, const uint64_t* qoff, uint32_t nq, const uint32_t* big,
-                uint32_t nbig, uint64_t qidBase, const uint64_t* starts, uint32_t nrec, sahara_hit* out, void* tmp,
-                size_t tmpBytes, hipStream_t st) {
+                uint32_t nbig, const uint32_t* huge, uint32_t nhuge, uint64_t qidBase, const uint64_t* starts,
+                uint32_t nrec, sahara_hit* out, void* tmp, size_t tmpBytes, hipStream_t st) {
     if (rows == 0) return;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((nq + 255) / 256, 65536));
     hipLaunchKernelGGL(kSortDecode, dim3(blocks), dim3(256), 0, st, k0, qoff, nq, qidBase, starts, nrec, out);
     SH_HIP(hipGetLastError());
-    if (nbig == 0) return;
-    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> bi(big, SegOff{qoff, 0});
-    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> ei(big, SegOff{qoff, 1});
+    if (nbig) {  // long segments in LDS; huge ones skipped there
+        hipLaunchKernelGGL(kSortBigLds, dim3(std::min<uint32_t>(nbig, 4096)), dim3(256), 0, st, k0, qoff, big, nbig,
+                           qidBase, starts, nrec, out);
+        SH_HIP(hipGetLastError());
+    }
+    if (nhuge == 0) return;
+    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> bi(huge, SegOff{qoff, 0});
+    rocprim::transform_iterator<const uint32_t*, SegOff, uint32_t> ei(huge, SegOff{qoff, 1});
     size_t tb = tmpBytes;
-    SH_HIP(rocprim::segmented_radix_sort_keys(tmp, tb, (const uint64_t*)k0, k1, (unsigned)rows, nbig, bi, ei, 0, 36,
+    SH_HIP(rocprim::segmented_radix_sort_keys(tmp, tb, (const uint64_t*)k0, k1, (unsigned)rows, nhuge, bi, ei, 0, 36,
                                               st));
-    hipLaunchKernelGGL(kDecodeBig, dim3(std::min<uint32_t>(nbig, 65536)), dim3(256), 0, st, k1, qoff, big, nbig, qidBase,
-                       starts, nrec, out);
+    hipLaunchKernelGGL(kDecodeBig, dim3(std::min<uint32_t>(nhuge, 65536)), dim3(256), 0, st, k1, qoff, huge, nhuge,
+                       qidBase, starts, nrec, out);
     SH_HIP(hipGetLastError());
 }
 

@@ -533,3 +533,35 @@ def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
     best = [sa.search_scheme("h2-k2", j, j, 50) for j in range(3)]
     bw = O.search_best(ref, pats, best, nthreads=8)
     assert np.array_equal(hits_as_rows(sa.search_best(gpu, pats, best, max_hits=n)), limit_rows(hits_as_rows(bw), n))
+
+
+@pytest.mark.parametrize("batch", [None, "37"])
+def test_long_and_huge_segments(gpu_device, monkeypatch, batch):
+    """Queries with 65..2048 located rows are sorted per workgroup in LDS
+    (kSortBigLds, bitonic over the segment padded to a power of two), longer
+    ones by the segmented radix sort (kScanTiles lists them): units tiled 90,
+    700, 1500 and 2600 times give segments on both sides of 2048 and of every
+    power of two, in one batch and across many."""
+    if batch:
+        monkeypatch.setenv("SAHARA_BATCH", batch)
+    rng = np.random.default_rng(77)
+    recs, pats = [], []
+    for tiles in (90, 700, 1500, 2600):
+        unit = random_records(rng, [50], 6)[0]
+        r = np.tile(unit, tiles)
+        r[rng.integers(0, len(r), tiles // 10)] = rng.integers(1, 6, tiles // 10)
+        recs.append(r)
+        for s in rng.integers(0, 50, 12):
+            p = np.roll(unit, -int(s))[:24].copy()
+            if s % 2:
+                p[rng.integers(0, 24)] = rng.integers(1, 6)
+            pats.append(p)
+    pats = np.vstack(pats + random_records(rng, [24] * 8, 6)).astype(np.uint8)
+    sch = sa.search_scheme("h2-k1", 0, 1, 24)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch, nthreads=8)[0])
+    per_q = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
+    assert ((per_q > 64) & (per_q <= 2048)).sum() >= 12 and (per_q > 2048).sum() >= 4
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    for verify, locate_sa in MODES:
+        gpu.set_mode(verify, locate_sa)
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
