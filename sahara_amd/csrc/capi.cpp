@@ -404,8 +404,20 @@ int sahara_gpu_stage(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint3
 int sahara_gpu_run(void* ctx, int count, uint64_t* n_hits) {
     return guarded([&] {
         Ctx* c = ctxOf(ctx);
+        const char* te = std::getenv("SAHARA_TIMING");  // 2: host-side marks of the call (stderr)
+        c->traceOn = te && std::atoi(te) >= 2;
+        if (c->traceOn) {
+            c->trace.clear();
+            c->traceT0 = std::chrono::steady_clock::now();
+        }
         run(c, count != 0);
         if (n_hits) *n_hits = c->nout;
+        if (c->traceOn) {
+            c->mark("run returns", 0);
+            std::sort(c->trace.begin(), c->trace.end());
+            for (auto& m : c->trace) std::fprintf(stderr, "[sahara]   %8.3f %s\n", m.first, m.second.c_str());
+            c->traceOn = false;
+        }
     });
 }
 

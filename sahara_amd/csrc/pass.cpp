@@ -255,11 +255,16 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         }
     }
     const uint64_t nbatch = bstart.size() - 1;
-    if (c->pinnedCap < nbatch * 8) {
+    // per batch, 16 words of pinned host memory: the slot's counters (0-6),
+    // the locate flags (7), the row total (8-9) and the long / huge segment
+    // counts (10, 11). Pinned, so that their copies are plain DMA writes: a
+    // copy into pageable memory waited behind the streamed upload's copies
+    // (4.5 ms for batch 0's row total at C3 over PCIe, r3)
+    if (c->pinnedCap < nbatch * 16) {
         if (c->pinned) SH_HIP(hipHostFree(c->pinned));
         c->pinned = nullptr;
         SH_HIP(hipHostMalloc(&c->pinned, nbatch * 8 * sizeof(uint32_t)));
-        c->pinnedCap = nbatch * 8;
+        c->pinnedCap = nbatch * 16;
     }
     if (c->qcnt.cap < maxBatch + 1) {
         c->qcnt.reserve(maxBatch + 1);
@@ -269,10 +274,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     }
     SH_HIP(hipMemsetAsync(c->qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
     hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
+    c->mark("pass", 0);
     SH_HIP(hipStreamSynchronize(c->st));
     SH_HIP(hipStreamSynchronize(c->stB));
     SH_HIP(hipStreamSynchronize(c->stC));
     SH_HIP(hipStreamSynchronize(c->stD));
+    c->mark("pass synced", 0);
     if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
     c->nout = 0;
     c->sinkDone = 0;
@@ -447,11 +454,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // the batch's counters, copied on sC (a copy on sB would wait for CU
         // slots between two text phases)
         SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
-        SH_HIP(hipMemcpyAsync(c->pinned + b * 8, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 16, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(c->ev[6], sC));
         SH_HIP(hipEventSynchronize(c->ev[6]));
         c->mark("text done", b);
-        const uint32_t* hs = c->pinned + b * 8;
+        const uint32_t* hs = c->pinned + b * 16;
         float ms = 0;
         SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
         S.seed_ms += ms;
@@ -486,11 +493,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->hrank.reserve(std::max<uint64_t>(nh, 1));
         querySegments(sl.hits.ptr, nh, c->qcnt.ptr, c->hrank.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr,
                       c->big.ptr, c->small.ptr + 4, c->huge.ptr, c->small.ptr + 5, sC);
-        uint64_t rows = 0;
-        uint32_t nbig2[2] = {0, 0};  // long segments, huge ones
-        SH_HIP(hipMemcpyAsync(&rows, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
-        SH_HIP(hipMemcpyAsync(nbig2, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));
+        uint32_t* pr = c->pinned + b * 16;
+        SH_HIP(hipMemcpyAsync(pr + 8, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipMemcpyAsync(pr + 10, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));  // long, huge segments
         SH_HIP(hipStreamSynchronize(sC));
+        uint64_t rows = 0;
+        std::memcpy(&rows, pr + 8, 8);
+        const uint32_t nbig2[2] = {pr[10], pr[11]};
         c->mark("rows", b);
         if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
         uint32_t nbig = nbig2[0], nhuge = nbig2[1];
@@ -578,7 +587,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         } else {
             c->sinkOk = false;
         }
-        SH_HIP(hipMemcpyAsync(c->pinned + b * 8 + 7, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipMemcpyAsync(c->pinned + b * 16 + 7, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(c->ev[5], sC));
         c->nout += rows;
         S.hits += rows;
@@ -586,12 +595,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     };
     auto finishCheck = [&](uint64_t b) {
         SH_HIP(hipEventSynchronize(c->ev[5]));
-        if (c->pinned[b * 8 + 7] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
+        if (c->pinned[b * 16 + 7] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
         float ms = 0;
         SH_HIP(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
         S.locate_ms += ms;
         SH_HIP(hipEventElapsedTime(&ms, c->ev[3], c->ev[4]));
         S.sort_ms += ms;
+        c->mark("checked", b);
     };
 
     if (!serial) {
@@ -665,6 +675,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         }
         cv.notify_all();
         finisher.join();
+        c->mark("finisher joined", 0);
         if (issueErr) std::rethrow_exception(issueErr);
         if (finErr) std::rethrow_exception(finErr);
         if (overflow) {
@@ -676,6 +687,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamSynchronize(sC));
         SH_HIP(hipStreamSynchronize(sD));
         SH_HIP(hipStreamSynchronize(c->stF));
+        c->mark("streams synced", 0);
         if (overflow) return;  // the caller redoes the pass serially with the grown buffers
     } else {
         for (uint64_t b = 0; b < nbatch; ++b) {

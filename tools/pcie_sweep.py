@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--full", action="store_true", help="whole 24-B records (sahara_gpu_search_reads)")
+    ap.add_argument("--marks", type=int, default=0, help="then this many calls with SAHARA_TIMING=2 (host marks, stderr)")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     import bench
@@ -67,6 +68,14 @@ def main():
                   f"packing {st['stage_ms']/a.steps:5.2f} ms  hits {n}", flush=True)
     for name, v in res.items():
         print(f"{name:12s} " + " ".join(f"{x/1e6:.1f}" for x in v) + f"  mean {np.mean(v)/1e6:.1f}M")
+    if a.marks:
+        for k in known:
+            os.environ.pop(k, None)
+        os.environ.update(sets[0][1])
+        os.environ["SAHARA_TIMING"] = "2"
+        for _ in range(a.marks):
+            h = call()
+            del h
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ cd /tmp && export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=8
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 "$R/bench.py" --no-cpu --no-count --no-verify --no-e2e --no-ref-path --steps 20 --warmup 2 "$@" > "$OUT/trace/b.json" 2> "$OUT/trace.err" || { echo "trace failed"; tail -5 "$OUT/trace.err"; exit 1; }
-cd "$R" && python3 tools/timeline.py "$OUT/trace/run_kernel_trace.csv" 5 > "$OUT/timeline.txt"; cp "$OUT/trace/run_kernel_stats.csv" "$OUT/kernel_stats.csv" && rm -f "$OUT/trace/run_kernel_trace.csv"
+cd "$R" && python3 tools/timeline.py "$OUT/trace/run_kernel_trace.csv" 5 > "$OUT/timeline.txt"; python3 tools/timeline.py "$OUT/trace/run_kernel_trace.csv" 5 gap > "$OUT/timeline_gap.txt"; cp "$OUT/trace/run_kernel_stats.csv" "$OUT/kernel_stats.csv" && rm -f "$OUT/trace/run_kernel_trace.csv"
 python3 tools/kstats.py "$OUT/kernel_stats.csv" > "$OUT/kstats.txt"; head -30 "$OUT/kstats.txt"
 python3 - "$OUT/bench.json" <<'PY'
 import json, sys

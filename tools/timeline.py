@@ -1,5 +1,8 @@
 """Timeline of the last search step in a rocprofv3 kernel trace: one line per
-kernel dispatch (start/end relative to the step's first seed kernel, in us)."""
+kernel dispatch (start/end relative to the step's first seed kernel, in us).
+With a third argument "gap": the step before the last one instead, from the
+dispatches before its first seed kernel (the previous step's tail) through the
+last step's first seed kernel, so that the idle time between steps shows."""
 import csv
 import re
 import sys
@@ -14,9 +17,10 @@ ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"
 ev.sort()
 seeds = [i for i, e in enumerate(ev) if e[2] == "kSeedItems"]
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-first = seeds[-nb]
+gap = len(sys.argv) > 3 and sys.argv[3] == "gap"
+first = seeds[-2 * nb] if gap else seeds[-nb]
 t0 = ev[first][0]
-for s, e, n, st, q in ev[first:]:
+for s, e, n, st, q in ev[max(0, first - 12) if gap else first:seeds[-nb] + 1 if gap else None]:
     if n.startswith("kDigest"):
         break
     print(f"{(s - t0) / 1e3:9.1f} {(e - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  q{q} {n}")
