@@ -174,6 +174,7 @@ Ctx* newCtx(int device) {
     SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stF, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
+    for (auto& e : c->evSleep) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     for (auto& e : c->ringEv) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // the streamed upload's pinned ring, pinned while the caller builds or
     // loads the index (pinning 256 MB takes ~50 ms)

@@ -302,6 +302,10 @@ struct Ctx {
     uint32_t hitCap = 0, taskCap = 0;
     sahara_stats stats{};
     hipEvent_t ev[8] = {};
+    // the finisher's waits in a streamed call (text done, row total, batch
+    // checked): blocking-sync events, so that it sleeps instead of spinning a
+    // CPU that the packing threads need (a 16-CPU quota on the GPU box)
+    hipEvent_t evSleep[3] = {};
 
     // Streamed query upload (sahara_gpu_search, sahara_gpu_search_reads): the
     // source rows go up in chunks, each packed on the host (two symbols per
@@ -333,6 +337,7 @@ struct Ctx {
     DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
     DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
     std::unique_ptr<HostPool> pool;
+    unsigned poolCap = 0;
     // host sink of sahara_gpu_search: each batch's sorted hits go to host
     // memory (pinned) on stF while later batches search
     sahara_hit* sink = nullptr;
@@ -384,6 +389,8 @@ struct Ctx {
         for (hipEvent_t e : downEv) (void)hipEventDestroy(e);
         if (downRing) (void)hipHostFree(downRing);
         for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : evSleep)
             if (e) (void)hipEventDestroy(e);
         for (auto& e : ringEv)
             if (e) (void)hipEventDestroy(e);

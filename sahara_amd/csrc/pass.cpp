@@ -447,6 +447,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // batch's counts (host waits for its text phase). Returns false on
     // overflow; `finishCheck` then reads the locate flags and timings.
     uint32_t seenTask = 0, seenHit = 0;  // pipelined overflow: the caps the re-run needs
+    // a streamed call's finisher sleeps in its waits while the calling thread
+    // and the pool pack (SAHARA_SLEEPY_SYNC=0: spins, as in device-resident runs)
+    const char* sleepEnv = std::getenv("SAHARA_SLEEPY_SYNC");
+    const bool sleepy = c->streaming && !serial && (!sleepEnv || std::atoi(sleepEnv) != 0);
     auto finish = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
@@ -455,8 +459,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // slots between two text phases)
         SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
         SH_HIP(hipMemcpyAsync(c->pinned + b * 16, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
-        SH_HIP(hipEventRecord(c->ev[6], sC));
-        SH_HIP(hipEventSynchronize(c->ev[6]));
+        SH_HIP(hipEventRecord(sleepy ? c->evSleep[0] : c->ev[6], sC));
+        SH_HIP(hipEventSynchronize(sleepy ? c->evSleep[0] : c->ev[6]));
         c->mark("text done", b);
         const uint32_t* hs = c->pinned + b * 16;
         float ms = 0;
@@ -496,7 +500,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         uint32_t* pr = c->pinned + b * 16;
         SH_HIP(hipMemcpyAsync(pr + 8, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipMemcpyAsync(pr + 10, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));  // long, huge segments
-        SH_HIP(hipStreamSynchronize(sC));
+        if (sleepy) {
+            SH_HIP(hipEventRecord(c->evSleep[1], sC));
+            SH_HIP(hipEventSynchronize(c->evSleep[1]));
+        } else {
+            SH_HIP(hipStreamSynchronize(sC));
+        }
         uint64_t rows = 0;
         std::memcpy(&rows, pr + 8, 8);
         const uint32_t nbig2[2] = {pr[10], pr[11]};
@@ -589,11 +598,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         }
         SH_HIP(hipMemcpyAsync(c->pinned + b * 16 + 7, c->small.ptr + 2, 4, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(c->ev[5], sC));
+        if (sleepy) SH_HIP(hipEventRecord(c->evSleep[2], sC));
         c->nout += rows;
         S.hits += rows;
         return true;
     };
     auto finishCheck = [&](uint64_t b) {
+        if (sleepy) SH_HIP(hipEventSynchronize(c->evSleep[2]));  // recorded beside ev[5]
         SH_HIP(hipEventSynchronize(c->ev[5]));
         if (c->pinned[b * 16 + 7] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
         float ms = 0;

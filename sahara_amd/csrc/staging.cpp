@@ -362,10 +362,16 @@ HostPool& hostPool(Ctx* c) {
     // of quota; tools/probe/pack_bench numa): 16 threads bound to the GPU's
     // node pack 250 GB/s of input on that node but 65 GB/s of input on the
     // other; unbound they pack 194-210 GB/s either way.
-    if (!c->pool) {
+    // (SAHARA_PACK_THREADS: threads packing, the caller's included; default
+    // 16; read per call, the pool is rebuilt when it changes)
+    unsigned cap = 16;
+    if (const char* t = std::getenv("SAHARA_PACK_THREADS")) cap = (unsigned)std::max(1, std::min(64, std::atoi(t)));
+    if (!c->pool || c->poolCap != cap) {
         const char* e = std::getenv("SAHARA_PACK_BIND");
         const bool bind = e && std::atoi(e) != 0;
-        c->pool = std::make_unique<HostPool>(hostThreads(c, 16) - 1, bind ? &c->place : nullptr);
+        c->pool.reset();
+        c->pool = std::make_unique<HostPool>(hostThreads(c, cap) - 1, bind ? &c->place : nullptr);
+        c->poolCap = cap;
     }
     return *c->pool;
 }
