@@ -256,8 +256,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     }
     const uint64_t nbatch = bstart.size() - 1;
     // per batch, 16 words of pinned host memory: the slot's counters (0-6),
-    // the locate flags (7), the row total (8-9) and the long / huge segment
-    // counts (10, 11). Pinned, so that their copies are plain DMA writes: a
+    // the locate flags (7), the row total (8-9), the long / huge segment
+    // counts (10, 11) and the rows --max_hits keeps (12-13). Pinned, so that their copies are plain DMA writes: a
     // copy into pageable memory waited behind the streamed upload's copies
     // (4.5 ms for batch 0's row total at C3 over PCIe, r3)
     if (c->pinnedCap < nbatch * 16) {
@@ -554,7 +554,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                    sC);
         if (c->limitN)  // --max_hits: this batch's queries keep their n best positions (search_n)
             rows = limitBatch(c->out.ptr + c->nout, rows, c->qoff.ptr, (uint32_t)nb, c->limitN, c->limitCnt,
-                              c->limitOff, c->limitBuf, c->tmp, sC);
+                              c->limitOff, c->limitBuf, c->tmp, reinterpret_cast<uint64_t*>(pr + 12), sC);
         SH_HIP(hipEventRecord(c->ev[4], sC));
         // sahara_gpu_search's host sink: the batch's hits go to host memory
         // on stF while later batches search (while they fit the sink)

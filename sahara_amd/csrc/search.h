@@ -133,7 +133,7 @@ void launchOffsetSeq(const sahara_hit* in, uint64_t n, uint64_t rec0, sahara_hit
 // --max_hits on the device: one batch's hits limited in place, kept rows returned
 uint64_t limitBatch(sahara_hit* out, uint64_t rows, const uint64_t* qoff, uint32_t nq, uint32_t n,
                     DevBuf<uint32_t>& kcnt, DevBuf<uint64_t>& koff, DevBuf<sahara_hit>& buf, DevBuf<char>& tmp,
-                    hipStream_t st);
+                    uint64_t* hostKept, hipStream_t st);
 // key / index buffers of the multi-part merge (kept by the context)
 struct MergeBufs {
     DevBuf<uint64_t> k0, k1;

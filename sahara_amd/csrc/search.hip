@@ -1851,10 +1851,11 @@ __global__ void kLimitWrite(const sahara_hit* __restrict__ h, const uint64_t* __
 
 // Applies --max_hits n to one batch's hits (out, rows; per-query segments
 // qoff[0..nq]) in place; returns the rows kept. Host-synchronous (the kept
-// total sizes the rest of the batch's chain).
+// total sizes the rest of the batch's chain): read back through hostKept,
+// 8 B of pinned memory.
 uint64_t limitBatch(sahara_hit* out, uint64_t rows, const uint64_t* qoff, uint32_t nq, uint32_t n,
                     DevBuf<uint32_t>& kcnt, DevBuf<uint64_t>& koff, DevBuf<sahara_hit>& buf, DevBuf<char>& tmp,
-                    hipStream_t st) {
+                    uint64_t* hostKept, hipStream_t st) {
     if (rows == 0 || nq == 0) return rows;
     kcnt.reserve((size_t)nq + 1);
     koff.reserve((size_t)nq + 1);
@@ -1867,9 +1868,9 @@ uint64_t limitBatch(sahara_hit* out, uint64_t rows, const uint64_t* qoff, uint32
     tmp.reserve(bytes + 256);
     SH_HIP(rocprim::exclusive_scan(tmp.ptr, bytes, kcnt.ptr, koff.ptr, (uint64_t)0, (size_t)nq + 1,
                                    rocprim::plus<uint64_t>(), st));
-    uint64_t kept = 0;
-    SH_HIP(hipMemcpyAsync(&kept, koff.ptr + nq, 8, hipMemcpyDeviceToHost, st));
+    SH_HIP(hipMemcpyAsync(hostKept, koff.ptr + nq, 8, hipMemcpyDeviceToHost, st));
     SH_HIP(hipStreamSynchronize(st));
+    const uint64_t kept = *hostKept;
     if (kept == rows) return rows;  // nothing to drop in this batch
     buf.reserve(std::max<uint64_t>(kept, 1));
     hipLaunchKernelGGL(kLimitWrite, dim3(blocks), dim3(256), 0, st, out, qoff, nq, n, koff.ptr, buf.ptr);
