@@ -608,6 +608,7 @@ static void copyOut(Ctx* c, void* dst, const void* src, size_t bytes) {
 // Waits for every stream of the context (after a failed streamed search: the
 // issued batches may still run and copy into the sink).
 static void drainAll(Ctx* c) {
+    drainPacking(c);  // chunks packed ahead: nothing reads the caller's buffer after the call
     for (hipStream_t s : {c->st, c->stB, c->stC, c->stD, c->stE, c->stF}) (void)hipStreamSynchronize(s);
 }
 

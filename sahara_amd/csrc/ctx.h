@@ -10,6 +10,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -101,6 +102,86 @@ private:
     uint64_t gen_ = 0;
     unsigned pending_ = 0;
     bool stop_ = false;
+};
+
+// Host threads that pack the streamed upload (staging.cpp): a FIFO of tasks
+// rather than fork-join rounds, so that the pieces of several chunks are in
+// flight at once. A fork-join round per chunk (13 pieces of 4M symbols on 16
+// threads at C3) left threads idle at every chunk's end and stopped packing
+// whenever the issuing thread was not inside it; queued chunks keep every
+// thread busy while the issuing thread enqueues kernels or waits for a slot.
+class TaskPool {
+public:
+    explicit TaskPool(unsigned workers, const Placement* pl = nullptr) {
+        for (unsigned i = 0; i < std::max(workers, 1u); ++i)
+            ts_.emplace_back([this, pl] {
+                if (pl) pl->bind();
+                loop();
+            });
+    }
+    ~TaskPool() {  // tasks still queued are dropped (callers wait for theirs first)
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : ts_) t.join();
+    }
+    unsigned size() const { return (unsigned)ts_.size(); }
+    void post(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+    void postMany(std::vector<std::function<void()>>& fs) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (auto& f : fs) q_.push_back(std::move(f));
+        }
+        cv_.notify_all();
+        fs.clear();
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (stop_) return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::vector<std::thread> ts_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+};
+
+// A group of tasks posted to a TaskPool that the poster waits for.
+struct TaskGroup {
+    std::atomic<uint64_t> left{0};
+    std::mutex mu;
+    std::condition_variable cv;
+    void begin(uint64_t n) { left.store(n, std::memory_order_relaxed); }
+    void oneDone() {
+        if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+            std::lock_guard<std::mutex> g(mu);
+            cv.notify_all();
+        }
+    }
+    void wait() {
+        if (left.load(std::memory_order_acquire) == 0) return;
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return left.load(std::memory_order_acquire) == 0; });
+    }
 };
 
 // Host side of sahara_gpu_search's compact hit download: batch by batch, the
@@ -322,21 +403,33 @@ struct Ctx {
         uint64_t rows = 0;             // source rows
         uint64_t chunk = 0;            // source rows per chunk (even: chunks start at even symbols)
         uint64_t done = 0;             // source rows enqueued
+        uint64_t submitted = 0;        // chunks whose packing is posted to the pool (2 bits)
+        uint32_t ahead = 6;            // chunks packed ahead of the issued ones (SAHARA_PACK_AHEAD)
         bool bad = false;              // a chunk held a byte that is no rank of this index
         double hostMs = 0;             // host time spent packing and enqueueing
         uint64_t chunks[3] = {0, 0, 0};  // chunks sent at 2 / 4 / 8 bits per symbol
     } up;
-    std::vector<std::vector<uint32_t>> excParts;  // per packing thread: N positions of a 2-bit chunk
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
     static constexpr size_t kRingSlots = 8, kRingSlot = 32u << 20;  // 256 MB pinned
     uint8_t* ring = nullptr;
     hipEvent_t ringEv[kRingSlots] = {};
+    // Chunks packed ahead (2-bit upload): chunk j packs into ring slot
+    // j % kRingSlots on the pool's threads while the issuing thread still
+    // enqueues earlier batches; uploadChunk waits for its pieces, then lists
+    // the N positions and enqueues the DMA (staging.cpp packAhead).
+    struct PackJob {
+        uint64_t chunk = UINT64_MAX;               // in flight or finished: chunk index
+        uint64_t pieces = 0, pieceSyms = 0;
+        std::atomic<int> bad{0};
+        std::vector<std::vector<uint32_t>> exc;    // per piece: N positions (chunk-relative symbols)
+        TaskGroup group;
+    } packJobs[kRingSlots];
     std::thread ringInit;                 // pins the ring (started by newCtx)
     bool ringFailed = false;
     DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
     DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
-    std::unique_ptr<HostPool> pool;
+    std::unique_ptr<TaskPool> pool;       // declared after packJobs: its threads end first
     unsigned poolCap = 0;
     // host sink of sahara_gpu_search: each batch's sorted hits go to host
     // memory (pinned) on stF while later batches search
@@ -431,7 +524,10 @@ void handOver(const std::vector<sahara_hit>& v, sahara_hit** hits, uint64_t* n_h
 Ctx* newCtx(int device);
 unsigned hostThreads(const Ctx* c, unsigned cap);
 Ctx* ctxOf(void* p);
-HostPool& hostPool(Ctx* c);
+TaskPool& hostPool(Ctx* c);
+// every pack job posted by the streamed upload is finished (the caller's
+// source buffer is no longer read): before a new call stages, after a failed one
+void drainPacking(Ctx* c);
 
 // staging.cpp: scheme tables, the query packers, the streamed upload
 void packSchemeTable(const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, uint32_t m,

@@ -355,33 +355,102 @@ uint64_t pack2Best(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sig
     return pack2Scalar(in, out, count, sigma, base, exc);
 }
 
-HostPool& hostPool(Ctx* c) {
+TaskPool& hostPool(Ctx* c) {
     // The packing threads read the caller's reads wherever their pages are,
     // so they stay unbound (SAHARA_PACK_BIND=1: on the GPU's node like the
     // context's other threads). Measured on the GPU box (2 NUMA nodes, 16 CPUs
     // of quota; tools/probe/pack_bench numa): 16 threads bound to the GPU's
     // node pack 250 GB/s of input on that node but 65 GB/s of input on the
     // other; unbound they pack 194-210 GB/s either way.
-    // (SAHARA_PACK_THREADS: threads packing, the caller's included; default
-    // 16; read per call, the pool is rebuilt when it changes)
+    // (SAHARA_PACK_THREADS: packing threads, default 16; read per call, the
+    // pool is rebuilt when it changes)
     unsigned cap = 16;
     if (const char* t = std::getenv("SAHARA_PACK_THREADS")) cap = (unsigned)std::max(1, std::min(64, std::atoi(t)));
     if (!c->pool || c->poolCap != cap) {
+        drainPacking(c);
         const char* e = std::getenv("SAHARA_PACK_BIND");
         const bool bind = e && std::atoi(e) != 0;
         c->pool.reset();
-        c->pool = std::make_unique<HostPool>(hostThreads(c, cap) - 1, bind ? &c->place : nullptr);
+        c->pool = std::make_unique<TaskPool>(hostThreads(c, cap), bind ? &c->place : nullptr);
         c->poolCap = cap;
     }
     return *c->pool;
 }
 
-// Packs the next chunk of the streamed upload (Ctx::Upload) on the host into
-// its ring slot, enqueues the slot's DMA on stE (nothing else: the DMAs run
-// back to back at the link's rate) and, on stream `kst` after the DMA's event,
-// the unpack (and reverse-complement interleave) kernel and both pattern
-// packings. A chunk with a byte that is no rank sets up.bad and enqueues
-// nothing.
+// f(k) for k in [0, n) on the pool's threads; returns when all are done
+static void runPieces(TaskPool& P, uint64_t n, const std::function<void(uint64_t)>& f) {
+    TaskGroup g;
+    g.begin(n);
+    std::vector<std::function<void()>> fs;
+    fs.reserve(n);
+    for (uint64_t k = 0; k < n; ++k)
+        fs.emplace_back([&f, &g, k] {
+            f(k);
+            g.oneDone();
+        });
+    P.postMany(fs);
+    g.wait();
+}
+
+static uint64_t chunkCount(const Ctx::Upload& U) { return U.chunk ? (U.rows + U.chunk - 1) / U.chunk : 0; }
+
+// Posts the 2-bit packing of chunk j (the next one not yet posted) to the
+// pool: its pieces pack into ring slot j % kRingSlots, each piece listing its
+// N positions. The slot's previous DMA (chunk j - kRingSlots) must be done.
+static void submitPack(Ctx* c, uint64_t j) {
+    Ctx::Upload& U = c->up;
+    const size_t slot = (size_t)(j % Ctx::kRingSlots);
+    Ctx::PackJob& J = c->packJobs[slot];
+    J.group.wait();  // (finished by its uploadChunk already; never blocks)
+    SH_HIP(hipEventSynchronize(c->ringEv[slot]));
+    const uint32_t m = c->m, sigma = c->I.sigma;
+    const uint64_t r0 = j * U.chunk, r1 = std::min(U.rows, r0 + U.chunk);
+    const uint64_t s0 = r0 * m, n = (r1 - r0) * m;
+    // symbols per piece (SAHARA_PACK_PIECE, a multiple of 4; 4M: 1 MB packed)
+    uint64_t pieceSyms = 4u << 20;
+    if (const char* e = std::getenv("SAHARA_PACK_PIECE")) pieceSyms = std::max<uint64_t>(4096, std::atoll(e)) & ~uint64_t(3);
+    J.chunk = j;
+    J.pieceSyms = pieceSyms;
+    J.pieces = (n + pieceSyms - 1) / pieceSyms;
+    J.bad.store(0, std::memory_order_relaxed);
+    if (J.exc.size() < J.pieces) J.exc.resize(J.pieces);
+    for (auto& v : J.exc) v.clear();
+    J.group.begin(J.pieces);
+    uint8_t* out = c->ring + slot * Ctx::kRingSlot;
+    const uint8_t* src = U.src + s0;
+    std::vector<std::function<void()>> fs;
+    fs.reserve(J.pieces);
+    for (uint64_t k = 0; k < J.pieces; ++k)
+        fs.emplace_back([&J, out, src, n, sigma, k] {
+            const uint64_t lo = k * J.pieceSyms, hi = std::min(n, lo + J.pieceSyms);
+            if (pack2Best(src + lo, out + lo / 4, hi - lo, sigma, lo, J.exc[k])) J.bad.store(1, std::memory_order_relaxed);
+            J.group.oneDone();
+        });
+    hostPool(c).postMany(fs);
+    U.submitted = j + 1;
+    c->mark("pack posted", j);
+}
+
+// Keeps the next U.ahead chunks after the last enqueued one posted to the
+// pool (2-bit upload), within the ring's slots.
+static void packAhead(Ctx* c) {
+    Ctx::Upload& U = c->up;
+    if (!c->streaming || U.bits != 2 || U.bad) return;
+    const uint64_t doneChunks = U.done / U.chunk + (U.done % U.chunk ? 1 : 0);
+    const uint64_t want = std::min({chunkCount(U), doneChunks + U.ahead, doneChunks + Ctx::kRingSlots - 1});
+    while (U.submitted < want) submitPack(c, U.submitted);
+}
+
+void drainPacking(Ctx* c) {
+    for (auto& J : c->packJobs) J.group.wait();
+}
+
+// Enqueues the next chunk of the streamed upload (Ctx::Upload): packed on the
+// host into its ring slot (2 bits: posted ahead by packAhead, waited for
+// here), its DMA on stE (nothing else: the DMAs run back to back at the link's
+// rate) and, on stream `kst` after the DMA's event, the unpack (and
+// reverse-complement interleave) kernel and both pattern packings. A chunk
+// with a byte that is no rank sets up.bad and enqueues nothing.
 void uploadChunk(Ctx* c, hipStream_t kst) {
     Ctx::Upload& U = c->up;
     const auto t0 = std::chrono::steady_clock::now();
@@ -390,11 +459,8 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     const uint32_t m = c->m, sigma = c->I.sigma;
     const uint64_t s0 = r0 * m, s1 = r1 * m, nsym = U.rows * m;  // symbols
     uint8_t* raw = U.rc ? c->readRaw.ptr : c->rawPats.ptr;
-    HostPool& P = hostPool(c);
-    const unsigned nt = P.size();
+    TaskPool& P = hostPool(c);
     std::atomic<int> bad{0};
-    // pieces of 1 MB of packed bytes spread over the pool (a chunk at C3 is
-    // ~25 MB packed); one DMA per chunk, overlapping the next chunk's packing
     constexpr uint64_t kPiece = 1u << 20;
     const bool avx2 = hostHasAvx2();
     const uint64_t j = r0 / U.chunk;
@@ -404,63 +470,51 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     const uint64_t b0 = s0 / 2, b1 = (s1 + 1) / 2;
     uint32_t bits = U.bits;
     uint64_t nExc = 0, excOff = 0;  // 2 bits: the N list, at byte excOff of the chunk's region
-    if (bits != 8) SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
-    c->mark("slot free", j);
     uint8_t* out = c->ring + slot * Ctx::kRingSlot;
     if (bits == 2) {
-        // symbols per piece (SAHARA_PACK_PIECE, a multiple of 4): a chunk's
-        // pieces spread over the pool's threads
-        uint64_t pieceSyms = 4 * kPiece;
-        if (const char* e = std::getenv("SAHARA_PACK_PIECE")) pieceSyms = std::max<uint64_t>(4096, std::atoll(e)) & ~uint64_t(3);
-        const uint64_t n = s1 - s0, pieces = (n + pieceSyms - 1) / pieceSyms;
-        // one N list per piece: concatenated in piece order they are sorted
-        if (c->excParts.size() < pieces) c->excParts.resize(pieces);
-        for (auto& v : c->excParts) v.clear();
-        P.run([&](unsigned t) {
-            for (uint64_t k = t; k < pieces; k += nt) {  // pieces of 4 MB of symbols (1 MB packed)
-                const uint64_t lo = k * pieceSyms, hi = std::min(n, lo + pieceSyms);
-                const uint8_t* in = U.src + s0 + lo;
-                const uint64_t acc = pack2Best(in, out + lo / 4, hi - lo, sigma, lo, c->excParts[k]);
-                if (acc) bad.store(1, std::memory_order_relaxed);
-            }
-        });
-        for (auto& v : c->excParts) nExc += v.size();
-        c->mark("pack cpu done", r0 / U.chunk);
+        if (U.submitted <= j) submitPack(c, j);  // (U.submitted == j: chunks post in order)
+        Ctx::PackJob& J = c->packJobs[slot];
+        J.group.wait();
+        c->mark("slot free", j);
+        if (J.bad.load(std::memory_order_relaxed)) bad.store(1);
+        const uint64_t n = s1 - s0;
+        for (uint64_t k = 0; k < J.pieces; ++k) nExc += J.exc[k].size();
+        c->mark("pack cpu done", j);
         excOff = ((b0 + (n + 3) / 4 + 3) & ~uint64_t(3)) - b0;  // 4-aligned on the device
         if (excOff + 4 * nExc > b1 - b0) {
             bits = 4;  // N-rich chunk: the list would not fit, go as nibbles
         } else if (!bad.load()) {
+            // the pieces' lists, concatenated in piece order, are sorted
             uint8_t* e = out + excOff;
-            for (auto& v : c->excParts) {
+            for (uint64_t k = 0; k < J.pieces; ++k) {
+                const auto& v = J.exc[k];
                 if (!v.empty()) std::memcpy(e, v.data(), v.size() * 4);
                 e += v.size() * 4;
             }
             SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, excOff + 4 * nExc, hipMemcpyHostToDevice, c->stE));
-            c->mark("dma enqueued", r0 / U.chunk);
+            c->mark("dma enqueued", j);
         }
+    } else {
+        SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous DMA is done
+        c->mark("slot free", j);
     }
     if (bits == 4 && !bad.load()) {
         const uint64_t pieces = (b1 - b0 + kPiece - 1) / kPiece;
-        P.run([&](unsigned t) {
-            for (uint64_t k = t; k < pieces; k += nt) {
-                const uint64_t lo = b0 + k * kPiece, hi = std::min(b1, lo + kPiece);
-                const uint64_t full = std::min(hi, std::max(lo, nsym / 2)) - lo;  // bytes with two symbols
-                const uint8_t* in = U.src + 2 * lo;
-                const uint64_t acc = avx2 ? packNibblesAvx2(in, out + (lo - b0), full, hi - lo, sigma)
-                                          : packNibblesScalar(in, out + (lo - b0), full, hi - lo, sigma);
-                if (acc) bad.store(1, std::memory_order_relaxed);
-            }
+        runPieces(P, pieces, [&](uint64_t k) {
+            const uint64_t lo = b0 + k * kPiece, hi = std::min(b1, lo + kPiece);
+            const uint64_t full = std::min(hi, std::max(lo, nsym / 2)) - lo;  // bytes with two symbols
+            const uint8_t* in = U.src + 2 * lo;
+            const uint64_t acc = avx2 ? packNibblesAvx2(in, out + (lo - b0), full, hi - lo, sigma)
+                                      : packNibblesScalar(in, out + (lo - b0), full, hi - lo, sigma);
+            if (acc) bad.store(1, std::memory_order_relaxed);
         });
         if (!bad.load()) SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, b1 - b0, hipMemcpyHostToDevice, c->stE));
     } else if (bits == 8) {  // one byte per symbol (SAHARA_UPLOAD_BITS=8): check, then copy as given
         const uint64_t pieces = (s1 - s0 + kPiece - 1) / kPiece;
-        P.run([&](unsigned t) {
-            for (uint64_t k = t; k < pieces; k += nt) {
-                const uint64_t lo = s0 + k * kPiece, hi = std::min(s1, lo + kPiece);
-                const uint64_t acc = avx2 ? badRanksAvx2(U.src + lo, hi - lo, sigma)
-                                          : badRanksScalar(U.src + lo, hi - lo, sigma);
-                if (acc) bad.store(1, std::memory_order_relaxed);
-            }
+        runPieces(P, pieces, [&](uint64_t k) {
+            const uint64_t lo = s0 + k * kPiece, hi = std::min(s1, lo + kPiece);
+            const uint64_t acc = avx2 ? badRanksAvx2(U.src + lo, hi - lo, sigma) : badRanksScalar(U.src + lo, hi - lo, sigma);
+            if (acc) bad.store(1, std::memory_order_relaxed);
         });
         if (!bad.load()) SH_HIP(hipMemcpyAsync(raw + s0, U.src + s0, s1 - s0, hipMemcpyHostToDevice, c->stE));
     }
@@ -505,8 +559,12 @@ void ensureUploaded(Ctx* c, uint64_t patEnd, hipStream_t kst) {
     auto covered = [&] { return U.rc ? std::min(2 * U.done, c->npat) : U.done; };
     while (covered() < patEnd) {
         uploadChunk(c, kst);
-        if (U.bad) throw Error("pattern rank out of range for this index");
+        if (U.bad) {
+            drainPacking(c);  // chunks posted ahead still read the caller's buffer
+            throw Error("pattern rank out of range for this index");
+        }
     }
+    packAhead(c);  // the pool packs the next chunks while this batch searches
 }
 
 // The scheme half of staging: host tables, their upload, the k-mer starts.
@@ -559,8 +617,10 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     c->pats3.reserve(npat * c->patBlocks);
     if (rc) c->readRaw.reserve(rows * m);
     c->badFlag.reserve(1);
+    drainPacking(c);  // (a failed call drained already)
     Ctx::Upload& U = c->up;
     U = Ctx::Upload{};
+    if (const char* e = std::getenv("SAHARA_PACK_AHEAD")) U.ahead = (uint32_t)std::max(0, std::atoi(e));
     U.src = src;
     U.rc = rc;
     U.rows = rows;

@@ -17,6 +17,24 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 
+def cgroup_stat():
+    """cgroup v2 cpu.stat of this process's cgroup (throttling under a CPU quota), or {}."""
+    try:
+        rel = open("/proc/self/cgroup").read().strip().split("::")[-1]
+        base = "/sys/fs/cgroup" + rel
+        d = {}
+        for line in open(os.path.join(base, "cpu.stat")):
+            k, v = line.split()
+            d[k] = int(v)
+        try:
+            d["cpu.max"] = open(os.path.join(base, "cpu.max")).read().strip()
+        except OSError:
+            pass
+        return d
+    except (OSError, ValueError):
+        return {}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
@@ -36,6 +54,8 @@ def main():
     sch = sa.search_scheme("h2-k2", 0, 2, 100)
     aff = sorted(os.sched_getaffinity(0))
     print(f"placement {idx.placement()}, process CPUs {len(aff)} ({aff[:4]}..{aff[-4:]})", flush=True)
+    cg0 = cgroup_stat()
+    print(f"cgroup cpu.max {cg0.get('cpu.max')}, stat {cg0}", flush=True)
     call = (lambda: sa.search_reads(idx, reads, sch)) if a.full else (lambda: sa.search_reads_compact(idx, reads, sch))
     sets = []
     for s in a.settings:
@@ -52,6 +72,8 @@ def main():
             for _ in range(2):
                 h = call()
                 del h
+            cg = cgroup_stat()
+            ct = os.times()
             t = time.perf_counter()
             st = {"stage_ms": 0.0}
             h = None
@@ -60,12 +82,16 @@ def main():
                 h = call()
                 st["stage_ms"] += idx.stats()["stage_ms"]
             el = time.perf_counter() - t
+            ct1 = os.times()
+            cg1 = cgroup_stat()
+            cpu_ms = ((ct1.user - ct.user) + (ct1.system - ct.system)) * 1e3 / a.steps
+            thr = {k: cg1.get(k, 0) - cg.get(k, 0) for k in ("nr_periods", "nr_throttled", "throttled_usec")}
             n = len(h)
             del h
             rps = a.reads * a.steps / el
             res[name].append(rps)
             print(f"round {r} {name:12s} {rps/1e6:7.1f}M reads/s  {el*1e3/a.steps:6.2f} ms/call  "
-                  f"packing {st['stage_ms']/a.steps:5.2f} ms  hits {n}", flush=True)
+                  f"packing {st['stage_ms']/a.steps:5.2f} ms  cpu {cpu_ms:6.1f} ms/call  cgroup {thr}  hits {n}", flush=True)
     for name, v in res.items():
         print(f"{name:12s} " + " ".join(f"{x/1e6:.1f}" for x in v) + f"  mean {np.mean(v)/1e6:.1f}M")
     if a.marks:
