@@ -29,6 +29,9 @@
 #include "../../include/sahara_hip.h"
 #include "device_index.h"
 #include "idx_format.h"
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "ctx.h"
 #include "search.h"
 
@@ -97,6 +100,53 @@ static int mapDevice(int device) {
     return map[(size_t)device];
 }
 
+// The CPUs of NUMA node `node` that this process may run on.
+Placement placementOfNode(int node) {
+    Placement pl;
+    pl.node = node;
+    if (node < 0) return pl;
+    std::FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+    if (!f) return pl;
+    char buf[8192] = {0};
+    const size_t got = std::fread(buf, 1, sizeof(buf) - 1, f);
+    std::fclose(f);
+    buf[got] = 0;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return pl;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (const char* p = buf; *p && *p != '\n';) {  // "0-15,64-79"
+        char* end = nullptr;
+        const long a = std::strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        if (*end == '-') b = std::strtol(end + 1, &end, 10);
+        for (long i = a; i <= b && i < CPU_SETSIZE; ++i)
+            if (CPU_ISSET(i, &allowed)) CPU_SET(i, &set);
+        p = *end == ',' ? end + 1 : end;
+    }
+    pl.cpus = set;
+    pl.ncpus = CPU_COUNT(&set);
+    return pl;
+}
+
+// The NUMA node holding most of [p, p + n) (16 sampled pages, move_pages
+// with no target: a query), or -1
+int nodeOfBuffer(const void* p, uint64_t n) {
+    if (!p || n == 0) return -1;
+    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+    void* pages[16];
+    int status[16];
+    for (int k = 0; k < 16; ++k)
+        pages[k] = reinterpret_cast<void*>(((uintptr_t)p + (uintptr_t)(n * (uint64_t)k / 16)) & ~(pg - 1));
+    if (syscall(SYS_move_pages, 0, 16UL, pages, nullptr, status, 0) != 0) return -1;
+    int votes[64] = {0}, best = -1;
+    for (int k = 0; k < 16; ++k)
+        if (status[k] >= 0 && status[k] < 64 && ++votes[status[k]] > (best >= 0 ? votes[best] : 0)) best = status[k];
+    return best;
+}
+
 // The CPUs of the device's NUMA node that this process may run on (Placement).
 static void placeNear(Ctx* c) {
     const char* e = std::getenv("SAHARA_NUMA");
@@ -113,31 +163,7 @@ static void placeNear(Ctx* c) {
         if (std::fscanf(f, "%d", &node) != 1) node = -1;
         std::fclose(f);
     }
-    c->place.node = node;
-    if (node < 0) return;
-    std::FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
-    if (!f) return;
-    char buf[8192] = {0};
-    const size_t got = std::fread(buf, 1, sizeof(buf) - 1, f);
-    std::fclose(f);
-    buf[got] = 0;
-    cpu_set_t allowed;
-    CPU_ZERO(&allowed);
-    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    for (const char* p = buf; *p && *p != '\n';) {  // "0-15,64-79"
-        char* end = nullptr;
-        const long a = std::strtol(p, &end, 10);
-        if (end == p) break;
-        long b = a;
-        if (*end == '-') b = std::strtol(end + 1, &end, 10);
-        for (long i = a; i <= b && i < CPU_SETSIZE; ++i)
-            if (CPU_ISSET(i, &allowed)) CPU_SET(i, &set);
-        p = *end == ',' ? end + 1 : end;
-    }
-    c->place.cpus = set;
-    c->place.ncpus = CPU_COUNT(&set);
+    c->place = placementOfNode(node);
 }
 
 // host threads a context uses for one job: its node's allowed CPUs (or the
@@ -609,7 +635,20 @@ static void copyOut(Ctx* c, void* dst, const void* src, size_t bytes) {
 // issued batches may still run and copy into the sink).
 static void drainAll(Ctx* c) {
     drainPacking(c);  // chunks packed ahead: nothing reads the caller's buffer after the call
-    for (hipStream_t s : {c->st, c->stB, c->stC, c->stD, c->stE, c->stF}) (void)hipStreamSynchronize(s);
+    for (hipStream_t s : {c->st, c->stB, c->stC, c->stD, c->stE, c->stF, c->stUp[0], c->stUp[1], c->stUp[2]})
+        if (s) (void)hipStreamSynchronize(s);
+}
+
+// SAHARA_TIMING=2: each chunk DMA's duration and rate from its events
+static void printDmaTimes(Ctx* c) {
+    for (size_t i = 0; i < c->dmaUsed; ++i) {
+        float ms = 0;
+        auto& d = c->dmaEv[i];
+        if (hipEventElapsedTime(&ms, d.second.first, d.second.second) == hipSuccess)
+            std::fprintf(stderr, "[sahara]   dma %zu: %.1f MB in %.3f ms, %.1f GB/s\n", i, d.first / 1e6, ms,
+                         ms > 0 ? d.first / (ms * 1e6) : 0.0);
+    }
+    c->dmaUsed = 0;
 }
 
 // sahara_gpu_search / sahara_gpu_search_reads: streamed upload, the pipelined
@@ -751,6 +790,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
                      ms(tA, tB), ms(tB, tC), ms(tC, t0), c->up.hostMs, c->stats.output_ms);
         std::sort(c->trace.begin(), c->trace.end());
         for (auto& m : c->trace) std::fprintf(stderr, "[sahara]   %8.2f %s\n", m.first, m.second.c_str());
+        printDmaTimes(c);
         c->traceOn = false;
     }
 }
@@ -812,6 +852,13 @@ static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, u
     if (const char* e = std::getenv("SAHARA_BLOCK_WRITE_WG")) c->blockWriteBlocks = (uint32_t)std::max(1, std::atoi(e));
     c->blockRecs = pinned ? static_cast<uint64_t*>(sinkMem) : nullptr;
     c->sinkCap = pinned ? capBytes / 8 : 0;
+    {
+        // SAHARA_COMPACT_DMA=0: the kernel writes the records into the sink
+        // itself (PCIe writes from 64 workgroups beside the text phase)
+        const char* e = std::getenv("SAHARA_COMPACT_DMA");
+        c->compactDma = !e || std::atoi(e) != 0;
+        if (c->compactDma && c->sinkCap) c->outRecs.reserve(c->sinkCap);
+    }
     auto* recs = static_cast<uint64_t*>(sinkMem);
     uint64_t recCap = capBytes / 8;
     try {
@@ -887,6 +934,7 @@ static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, u
                      c->up.hostMs, c->stats.output_ms);
         std::sort(c->trace.begin(), c->trace.end());
         for (auto& m : c->trace) std::fprintf(stderr, "[sahara]   %8.2f %s\n", m.first, m.second.c_str());
+        printDmaTimes(c);
         c->traceOn = false;
     }
 }

@@ -411,6 +411,17 @@ struct Ctx {
     } up;
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
+    // more upload streams (SAHARA_UPLOAD_STREAMS = 1 + how many are used): a
+    // chunk's DMA splits into equal parts, one per stream, so that several
+    // copy engines move it; stE waits for the others' parts (upPartEv) before
+    // it records the chunk's ringEv
+    static constexpr int kUpStreams = 3;
+    hipStream_t stUp[kUpStreams] = {};
+    hipEvent_t upPartEv[kUpStreams] = {};
+    uint32_t upStreams = 1;
+    // SAHARA_TIMING=2: timing events around each chunk's DMA (bytes, events)
+    std::vector<std::pair<uint64_t, std::pair<hipEvent_t, hipEvent_t>>> dmaEv;
+    size_t dmaUsed = 0;
     static constexpr size_t kRingSlots = 8, kRingSlot = 32u << 20;  // 256 MB pinned
     uint8_t* ring = nullptr;
     hipEvent_t ringEv[kRingSlots] = {};
@@ -431,6 +442,9 @@ struct Ctx {
     DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
     std::unique_ptr<TaskPool> pool;       // declared after packJobs: its threads end first
     unsigned poolCap = 0;
+    Placement packPlace;                  // the pool's CPUs when bound
+    int poolNode = -2;                    // NUMA node the pool is bound to (-1: unbound)
+    int srcNode = -1;                     // node of the streamed call's source rows (SAHARA_PACK_BIND=2)
     // host sink of sahara_gpu_search: each batch's sorted hits go to host
     // memory (pinned) on stF while later batches search
     sahara_hit* sink = nullptr;
@@ -454,6 +468,12 @@ struct Ctx {
     // qid and one past its last record (the blocks of sahara_hit_blocks)
     uint64_t* blockRecs = nullptr;
     uint32_t blockWriteBlocks = 64;
+    // the records are made in HBM (outRecs, sinkCap entries) and copied down
+    // by a copy engine (SAHARA_COMPACT_DMA=0: written by the kernel into the
+    // sink over PCIe; C3 592M -> 632M reads/s with the copy engine,
+    // profiles/r03_pcie_compact_dma.txt)
+    bool compactDma = false;
+    DevBuf<uint64_t> outRecs;
     std::vector<uint64_t> batchQ0, batchEnd;
     std::vector<uint64_t> recStartsEnd;   // record starts + the text length (sahara_hit_blocks.rec_starts)
     // --max_hits n applied per batch on the device (single-part indexes;
@@ -489,6 +509,14 @@ struct Ctx {
             if (e) (void)hipEventDestroy(e);
         if (ring) (void)hipHostFree(ring);
         if (stE) (void)hipStreamDestroy(stE);
+        for (auto& d : dmaEv) {
+            (void)hipEventDestroy(d.second.first);
+            (void)hipEventDestroy(d.second.second);
+        }
+        for (int i = 0; i < kUpStreams; ++i) {
+            if (stUp[i]) (void)hipStreamDestroy(stUp[i]);
+            if (upPartEv[i]) (void)hipEventDestroy(upPartEv[i]);
+        }
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
             for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
@@ -525,6 +553,8 @@ Ctx* newCtx(int device);
 unsigned hostThreads(const Ctx* c, unsigned cap);
 Ctx* ctxOf(void* p);
 TaskPool& hostPool(Ctx* c);
+Placement placementOfNode(int node);
+int nodeOfBuffer(const void* p, uint64_t n);
 // every pack job posted by the streamed upload is finished (the caller's
 // source buffer is no longer read): before a new call stages, after a failed one
 void drainPacking(Ctx* c);

@@ -153,9 +153,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // text 3 + FM 2 883-905M and FM 3 847-890M, alternating runs on one box:
     // 115-131 VGPRs per FM wave leave the SIMDs' registers to the text waves
     // and the locate chain.)
-    // patterns per batch: 4M, fewer for schemes with many searches (work
-    // items must fit 2^31); SAHARA_BATCH lowers it (tests of the pipeline)
-    uint64_t maxBatch = std::min<uint64_t>(1ull << 22, (1ull << 31) / c->nsearch);
+    // patterns per batch: 4M (2M in a streamed call: its first batch waits
+    // for the host to pack and upload it, its last one's hits for the
+    // download, so smaller ones shorten both ends; C3 compact reads path
+    // 584-615M -> 668-689M reads/s, profiles/r03_pcie_batch_sweep.txt),
+    // fewer for schemes with many searches (work items must fit 2^31);
+    // SAHARA_BATCH sets it (tests of the pipeline)
+    uint64_t maxBatch = std::min<uint64_t>(c->streaming ? 1ull << 21 : 1ull << 22, (1ull << 31) / c->nsearch);
     if (const char* e = std::getenv("SAHARA_BATCH"))
         maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
     if (c->blockRecs) maxBatch = std::min<uint64_t>(maxBatch, 1ull << 27);  // compact records: qid - q0 < 2^28
@@ -562,7 +566,17 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->batchEnd.push_back(c->nout + rows);
         if (c->sinkOk && c->nout + rows <= c->sinkCap) {
             const bool compact = c->compactSink && rows * sizeof(uint64_t) <= Ctx::kDownSlot && nb < (1ull << 28);
-            if (rows && c->blockRecs) {  // compact records written by the device into the pinned sink (PCIe writes)
+            if (rows && c->blockRecs && c->compactDma) {
+                // compact records made in HBM on sC (full grid, ~20 us), then
+                // one D2H copy on stF: a copy engine moves them, no workgroup
+                // waits on PCIe writes beside the text phase
+                launchCompactHits(c->out.ptr + c->nout, rows, q0, c->I.dRecStarts.ptr, c->outRecs.ptr + c->nout, sC,
+                                  1u << 16);
+                SH_HIP(hipEventRecord(c->ev[7], sC));
+                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[7], 0));
+                SH_HIP(hipMemcpyAsync(c->blockRecs + c->nout, c->outRecs.ptr + c->nout, rows * sizeof(uint64_t),
+                                      hipMemcpyDeviceToHost, c->stF));
+            } else if (rows && c->blockRecs) {  // compact records written by the device into the pinned sink (PCIe writes)
                 SH_HIP(hipStreamWaitEvent(c->stF, c->ev[4], 0));
                 launchCompactHits(c->out.ptr + c->nout, rows, q0, c->I.dRecStarts.ptr, c->blockRecs + c->nout, c->stF,
                                   c->blockWriteBlocks);

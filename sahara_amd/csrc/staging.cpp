@@ -366,13 +366,19 @@ TaskPool& hostPool(Ctx* c) {
     // pool is rebuilt when it changes)
     unsigned cap = 16;
     if (const char* t = std::getenv("SAHARA_PACK_THREADS")) cap = (unsigned)std::max(1, std::min(64, std::atoi(t)));
-    if (!c->pool || c->poolCap != cap) {
+    // SAHARA_PACK_BIND: 1 the GPU's node, 2 the node holding the call's
+    // source rows (sampled pages), else unbound
+    const char* e = std::getenv("SAHARA_PACK_BIND");
+    const int mode = e ? std::atoi(e) : 0;
+    const int node = mode == 1 ? c->place.node : mode == 2 ? c->srcNode : -1;
+    if (!c->pool || c->poolCap != cap || c->poolNode != node) {
         drainPacking(c);
-        const char* e = std::getenv("SAHARA_PACK_BIND");
-        const bool bind = e && std::atoi(e) != 0;
         c->pool.reset();
-        c->pool = std::make_unique<TaskPool>(hostThreads(c, cap), bind ? &c->place : nullptr);
+        c->packPlace = placementOfNode(node);
+        c->pool = std::make_unique<TaskPool>(std::min(cap, c->packPlace.ncpus > 0 ? (unsigned)c->packPlace.ncpus : cap),
+                                             node >= 0 ? &c->packPlace : nullptr);
         c->poolCap = cap;
+        c->poolNode = node;
     }
     return *c->pool;
 }
@@ -445,6 +451,43 @@ void drainPacking(Ctx* c) {
     for (auto& J : c->packJobs) J.group.wait();
 }
 
+// H2D copy of one chunk's staged bytes: on stE, or split into equal parts
+// over stE and c->upStreams - 1 more streams (their parts joined into stE, so
+// that the chunk's ringEv, recorded on stE, covers all of them)
+static void uploadCopy(Ctx* c, void* dst, const void* src, uint64_t bytes) {
+    const uint32_t ns = std::min<uint32_t>(c->upStreams, 1 + Ctx::kUpStreams);
+    if (c->traceOn) {  // SAHARA_TIMING=2: the DMA's own duration (printed with the marks)
+        if (c->dmaUsed == c->dmaEv.size()) {
+            hipEvent_t a, b;
+            SH_HIP(hipEventCreate(&a));
+            SH_HIP(hipEventCreate(&b));
+            c->dmaEv.push_back({0, {a, b}});
+        }
+        auto& d = c->dmaEv[c->dmaUsed++];
+        d.first = bytes;
+        SH_HIP(hipEventRecord(d.second.first, c->stE));
+        SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stE));
+        SH_HIP(hipEventRecord(d.second.second, c->stE));
+        return;
+    }
+    if (ns <= 1 || bytes < (16u << 10)) {
+        SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stE));
+        return;
+    }
+    const uint64_t part = ((bytes + ns - 1) / ns + 4095) & ~uint64_t(4095);
+    for (uint32_t i = 0; i < ns; ++i) {
+        const uint64_t lo = std::min<uint64_t>(bytes, i * part), hi = std::min<uint64_t>(bytes, lo + part);
+        if (hi <= lo) break;
+        hipStream_t s = i == 0 ? c->stE : c->stUp[i - 1];
+        SH_HIP(hipMemcpyAsync(static_cast<char*>(dst) + lo, static_cast<const char*>(src) + lo, hi - lo,
+                              hipMemcpyHostToDevice, s));
+        if (i > 0) {
+            SH_HIP(hipEventRecord(c->upPartEv[i - 1], s));
+            SH_HIP(hipStreamWaitEvent(c->stE, c->upPartEv[i - 1], 0));
+        }
+    }
+}
+
 // Enqueues the next chunk of the streamed upload (Ctx::Upload): packed on the
 // host into its ring slot (2 bits: posted ahead by packAhead, waited for
 // here), its DMA on stE (nothing else: the DMAs run back to back at the link's
@@ -491,7 +534,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
                 if (!v.empty()) std::memcpy(e, v.data(), v.size() * 4);
                 e += v.size() * 4;
             }
-            SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, excOff + 4 * nExc, hipMemcpyHostToDevice, c->stE));
+            uploadCopy(c, c->nibPats.ptr + b0, out, excOff + 4 * nExc);
             c->mark("dma enqueued", j);
         }
     } else {
@@ -508,7 +551,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
                                       : packNibblesScalar(in, out + (lo - b0), full, hi - lo, sigma);
             if (acc) bad.store(1, std::memory_order_relaxed);
         });
-        if (!bad.load()) SH_HIP(hipMemcpyAsync(c->nibPats.ptr + b0, out, b1 - b0, hipMemcpyHostToDevice, c->stE));
+        if (!bad.load()) uploadCopy(c, c->nibPats.ptr + b0, out, b1 - b0);
     } else if (bits == 8) {  // one byte per symbol (SAHARA_UPLOAD_BITS=8): check, then copy as given
         const uint64_t pieces = (s1 - s0 + kPiece - 1) / kPiece;
         runPieces(P, pieces, [&](uint64_t k) {
@@ -621,9 +664,19 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     Ctx::Upload& U = c->up;
     U = Ctx::Upload{};
     if (const char* e = std::getenv("SAHARA_PACK_AHEAD")) U.ahead = (uint32_t)std::max(0, std::atoi(e));
+    c->upStreams = 1;
+    c->dmaUsed = 0;
+    if (const char* e = std::getenv("SAHARA_UPLOAD_STREAMS"))
+        c->upStreams = (uint32_t)std::max(1, std::min(1 + Ctx::kUpStreams, std::atoi(e)));
+    for (uint32_t i = 0; i + 1 < c->upStreams; ++i)
+        if (!c->stUp[i]) {
+            SH_HIP(hipStreamCreateWithFlags(&c->stUp[i], hipStreamNonBlocking));
+            SH_HIP(hipEventCreateWithFlags(&c->upPartEv[i], hipEventDisableTiming));
+        }
     U.src = src;
     U.rc = rc;
     U.rows = rows;
+    if (const char* e = std::getenv("SAHARA_PACK_BIND"); e && std::atoi(e) == 2) c->srcNode = nodeOfBuffer(src, rows * m);
     // symbols cross PCIe at 2 bits (DNA: A C G T codes, N positions listed),
     // 4 bits (any alphabet) or 8 (as given): SAHARA_UPLOAD_BITS, or
     // SAHARA_NIBBLE_UPLOAD=0 for 8

@@ -56,6 +56,29 @@ def test_compact_equals_full_records(gpu_device, monkeypatch, batch, chunk):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"SAHARA_COMPACT_DMA": "0"}, {"SAHARA_UPLOAD_STREAMS": "3", "SAHARA_UPLOAD_CHUNK": "2048"},
+                                 {"SAHARA_PACK_BIND": "2"}, {"SAHARA_PACK_AHEAD": "0"},
+                                 {"SAHARA_PACK_AHEAD": "7", "SAHARA_PACK_PIECE": "4096"}])
+def test_compact_host_path_settings(gpu_device, monkeypatch, env):
+    """The streamed call's host-side variants give the same records: the
+    kernel writing them over PCIe instead of a copy engine, each chunk's DMA
+    split over three streams, packers bound to the source rows' NUMA node,
+    packing on demand (no chunks ahead) and many small pieces seven chunks
+    ahead; small batches and chunks so that the ring wraps."""
+    monkeypatch.setenv("SAHARA_BATCH", "701")
+    monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "96")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    flat, lens, reads, sch = _setup(n_reads=2400)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    want = _ordered(sa.search_reads(gpu, reads, sch))
+    for _ in range(2):
+        c = sa.search_reads_compact(gpu, reads, sch)
+        assert np.array_equal(_ordered(c.to_hits()), want)
+        c.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("reverse,limit", [(True, 0), (True, 1999), (False, 0), (False, 777)])
 def test_compact_limit_and_no_reverse(gpu_device, monkeypatch, reverse, limit):
     monkeypatch.setenv("SAHARA_BATCH", "500")
