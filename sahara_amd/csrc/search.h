@@ -100,6 +100,8 @@ struct TextArgs {
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
+    uint32_t prefetch;       // at each refill, the lanes holding the next `prefetch` tasks of the current
+                             // chunk touch their window's and pattern's lines (into L2) (0: off)
 };
 
 struct LocateArgs {
@@ -141,6 +143,8 @@ struct MergeBufs {
 };
 void sortHitsByQid(const sahara_hit* in, uint64_t n, uint64_t nqid, sahara_hit* out, MergeBufs& B, DevBuf<char>& tmp,
                    hipStream_t st);
+void launchGatherPatterns(const uint32_t* pats, const uint4* pats3, const uint64_t* idx, uint64_t n, uint32_t patWords,
+                          uint32_t patBlocks, uint32_t* opats, uint4* opats3, hipStream_t st);
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
                        hipStream_t st, uint32_t maxBlocks = 8192);
 void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,

@@ -530,9 +530,46 @@ def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
     gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
     assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, max_hits=n)), want)
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
+    # one round: the full scheme on every query, then the cut (no exact round first)
+    monkeypatch.setenv("SAHARA_MAXHITS_ROUNDS", "1")
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
+    monkeypatch.delenv("SAHARA_MAXHITS_ROUNDS")
     best = [sa.search_scheme("h2-k2", j, j, 50) for j in range(3)]
     bw = O.search_best(ref, pats, best, nthreads=8)
     assert np.array_equal(hits_as_rows(sa.search_best(gpu, pats, best, max_hits=n)), limit_rows(hits_as_rows(bw), n))
+
+
+@pytest.mark.parametrize("n", [1, 3, 40])
+def test_max_hits_exact_round_first(gpu_device, monkeypatch, n):
+    """--max_hits n runs an exact round first and the full scheme only on the
+    queries with fewer than n exact positions (capi.cpp searchExactFirst):
+    equal to the policy over the oracle's full hits, with queries of every
+    kind — exact repeats with hundreds of positions (leave after the exact
+    round), exact reads with a few positions, and reads with 1-2 errors (need
+    the full scheme) — over several batches, reads with and without reverse
+    complements, and the patterns call."""
+    from test_golden import limit_rows
+    monkeypatch.setenv("SAHARA_BATCH", "173")
+    rng = np.random.default_rng(90 + n)
+    unit = random_records(rng, [60], 6)[0]
+    rep = np.tile(unit, 300)
+    rep[rng.integers(0, len(rep), 40)] = rng.integers(1, 6, 40)
+    recs = [rep] + random_records(rng, [30000, 9000], 6)
+    exact = mutate_reads(rng, recs, 300, 50, 0, 6)
+    errs = mutate_reads(rng, recs, 300, 50, 2, 6)
+    reads = np.concatenate([exact, errs])[rng.permutation(600)]
+    scheme = sa.search_scheme("h2-k2", 0, 2, 50)
+    ref = O.Index.build(recs, 6, 16)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    for rc in (True, False):
+        pats = sa.interleave_rc(reads, 6) if rc else reads
+        want, _ = ref.search(pats, scheme, edit=True, nthreads=8)
+        want = limit_rows(hits_as_rows(want), n)
+        assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, reverse=rc, max_hits=n)), want)
+        if rc:
+            assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, max_hits=n)), want)
+    q_with_n = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
+    assert (q_with_n == n).any() and (q_with_n < n).any()  # both kinds of query occur
 
 
 @pytest.mark.parametrize("batch", [None, "37"])
