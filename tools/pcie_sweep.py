@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--full", action="store_true", help="whole 24-B records (sahara_gpu_search_reads)")
+    ap.add_argument("--max-hits", type=int, default=0, help="sahara_gpu_search_reads with --max_hits N")
+    ap.add_argument("--read-errors", type=int, default=2, help="errors simulated per read (search k stays 2)")
     ap.add_argument("--marks", type=int, default=0, help="then this many calls with SAHARA_TIMING=2 (host marks, stderr)")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
@@ -49,7 +51,7 @@ def main():
     lens = bench.record_lengths(3_000_000_000, 24)
     flat, lens = sa.synth_reference(lens, sigma=6, seed=42)
     idx = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=0)
-    reads = sa.synth_reads(flat, lens, a.reads, 100, 2, sigma=6, seed=7)
+    reads = sa.synth_reads(flat, lens, a.reads, 100, a.read_errors, sigma=6, seed=7)
     del flat
     sch = sa.search_scheme("h2-k2", 0, 2, 100)
     aff = sorted(os.sched_getaffinity(0))
@@ -57,6 +59,8 @@ def main():
     cg0 = cgroup_stat()
     print(f"cgroup cpu.max {cg0.get('cpu.max')}, stat {cg0}", flush=True)
     call = (lambda: sa.search_reads(idx, reads, sch)) if a.full else (lambda: sa.search_reads_compact(idx, reads, sch))
+    if a.max_hits:
+        call = lambda: sa.search_reads(idx, reads, sch, max_hits=a.max_hits)
     sets = []
     for s in a.settings:
         name, _, kv = s.partition("=")
