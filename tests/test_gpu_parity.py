@@ -568,8 +568,8 @@ def test_max_hits_exact_round_first(gpu_device, monkeypatch, n):
         assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, reverse=rc, max_hits=n)), want)
         if rc:
             assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, max_hits=n)), want)
-    q_with_n = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
-    assert (q_with_n == n).any() and (q_with_n < n).any()  # both kinds of query occur
+            q_with_n = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
+            assert (q_with_n == n).any() and (q_with_n < n).any()  # both kinds of query occur
 
 
 @pytest.mark.parametrize("batch", [None, "37"])

@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU box: the --max_hits / compact / golden / CLI GPU tests, then --max_hits 1
+# timed at C3 with one round and two (reads with 2 errors and exact reads),
+# then the text-window prefetch A/B. Stops after a GPU fault, abort or time limit.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$(realpath -m "$1"); shift
+mkdir -p "$OUT"
+cd "$R"
+stop() { [ "$1" -ge 124 ] && { echo "stopping after exit $1"; exit "$1"; }; return 0; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_compact.py tests/test_golden.py tests/test_cli.py \
+    -x -q --timeout 120 --timeout-method thread -m gpu > "$OUT/tests.log" 2>&1; rc=$?; tail -3 "$OUT/tests.log"; stop $rc
+for e in 2 0; do
+  SAHARA_TIMING=1 timeout -k 10 400 python -u tools/pcie_sweep.py --rounds 2 --steps 3 --max-hits 1 --read-errors $e \
+      two= one=SAHARA_MAXHITS_ROUNDS=1 > "$OUT/maxhits_e$e.txt" 2>&1; rc=$?; grep -E "mean|exact round" "$OUT/maxhits_e$e.txt" | tail -4; stop $rc
+done
+timeout -k 10 600 python -u tools/ab_inproc.py --config c3 --rounds 3 --steps 10 base= pf16=SAHARA_TEXT_PREFETCH=16 \
+    pf48=SAHARA_TEXT_PREFETCH=48 > "$OUT/prefetch_ab.txt" 2>&1; rc=$?; tail -4 "$OUT/prefetch_ab.txt"; stop $rc
