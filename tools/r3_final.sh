@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round-3 evidence on the GPU box, outputs in $1 (under gpurun_out/): the
 # round evidence (GPU tests, C3 / C2 / C5 / C6 bench lines, C3 kernel trace),
-# then --max_hits 1 timed at C3 with one round and two, then the text-window
-# prefetch A/B. Stops after a GPU fault, abort or time limit.
+# then --max_hits 1 timed at C3 with one round and two. Stops after a GPU
+# fault, abort or time limit.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$(realpath -m "$1"); shift
@@ -15,5 +15,3 @@ for e in 2 0; do
   SAHARA_TIMING=1 timeout -k 10 300 python -u tools/pcie_sweep.py --rounds 2 --steps 3 --max-hits 1 --read-errors $e \
       two= one=SAHARA_MAXHITS_ROUNDS=1 > "$OUT/maxhits_e$e.txt" 2>&1; rc=$?; grep -E "mean|exact round" "$OUT/maxhits_e$e.txt" | tail -3; stop $rc
 done
-timeout -k 10 400 python -u tools/ab_inproc.py --config c3 --rounds 2 --steps 10 base= pf16=SAHARA_TEXT_PREFETCH=16 \
-    pf48=SAHARA_TEXT_PREFETCH=48 > "$OUT/prefetch_ab.txt" 2>&1; rc=$?; tail -4 "$OUT/prefetch_ab.txt"; stop $rc
