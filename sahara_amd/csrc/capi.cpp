@@ -737,6 +737,7 @@ static void searchExactFirst(Ctx* c, const uint8_t* src, uint64_t rows, bool rc,
         c->staged = c->streaming = false;
         throw;
     }
+    c->staged = false;  // the device holds a subset now: sahara_gpu_run has nothing to re-run
     std::sort(all.begin(), all.end(), hitLess);
     acc.patterns = npat;
     acc.hits = all.size();
