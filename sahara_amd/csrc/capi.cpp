@@ -658,8 +658,12 @@ static void printDmaTimes(Ctx* c) {
 // (seq_id, pos), each with e = 0, and the exact round finds all of them. Only
 // the other queries run the full scheme, as a subset gathered on the device
 // from the patterns the first round staged. A repetitive query, which costs
-// the most in the full search, leaves after the cheap round.
-// (SAHARA_MAXHITS_ROUNDS=1: the full scheme on every query, then the cut.)
+// the most in the full search, leaves after the cheap round. Off by default
+// (SAHARA_MAXHITS_ROUNDS=2 turns it on): at C3 (reads with two errors, so the
+// exact round retires 0.08% of the queries) the two rounds and their host-side
+// merge took 1.5 s per call against 16.5 ms for one round, and 0.66 s against
+// 0.25 s with error-free reads (half the queries retired;
+// profiles/r03_final_maxhits_e{2,0}.txt, before the merge replaced a sort).
 static void searchExactFirst(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t len,
                              const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit,
                              uint32_t n, sahara_hit** hits, uint64_t* n_hits) {
@@ -705,6 +709,7 @@ static void searchExactFirst(Ctx* c, const uint8_t* src, uint64_t rows, bool rc,
             if (cnt[q] < n) todo.push_back(q);
         for (const auto& h : v)
             if (cnt[h.qid] >= n) all.push_back(h);
+        const size_t kept = all.size();
         rest = todo.size();
         if (!todo.empty()) {
             DevBuf<uint64_t> idx;
@@ -730,6 +735,8 @@ static void searchExactFirst(Ctx* c, const uint8_t* src, uint64_t rows, bool rc,
                 h.qid = todo[h.qid];
                 all.push_back(h);
             }
+            // both runs are in (qid, seq_id, pos, err) order: one linear merge
+            std::inplace_merge(all.begin(), all.begin() + (ptrdiff_t)kept, all.end(), hitLess);
         }
     } catch (...) {
         c->limitN = 0;
@@ -738,7 +745,6 @@ static void searchExactFirst(Ctx* c, const uint8_t* src, uint64_t rows, bool rc,
         throw;
     }
     c->staged = false;  // the device holds a subset now: sahara_gpu_run has nothing to re-run
-    std::sort(all.begin(), all.end(), hitLess);
     acc.patterns = npat;
     acc.hits = all.size();
     acc.total_ms = std::chrono::duration<double, std::milli>(clk::now() - tA).count();
@@ -771,7 +777,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         uint32_t maxU = 0;
         for (uint64_t i = 0; i < (uint64_t)n_searches * len; ++i) maxU = std::max(maxU, u[i]);
         const char* r = std::getenv("SAHARA_MAXHITS_ROUNDS");
-        if (maxU > 0 && (!r || std::atoi(r) != 1)) {
+        if (maxU > 0 && r && std::atoi(r) == 2) {
             searchExactFirst(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit, max_hits, hits, n_hits);
             c->traceOn = false;
             return;

@@ -530,8 +530,8 @@ def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
     gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
     assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, max_hits=n)), want)
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
-    # one round: the full scheme on every query, then the cut (no exact round first)
-    monkeypatch.setenv("SAHARA_MAXHITS_ROUNDS", "1")
+    # two rounds: an exact round first, the full scheme on the rest
+    monkeypatch.setenv("SAHARA_MAXHITS_ROUNDS", "2")
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
     monkeypatch.delenv("SAHARA_MAXHITS_ROUNDS")
     best = [sa.search_scheme("h2-k2", j, j, 50) for j in range(3)]
@@ -541,8 +541,9 @@ def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
 
 @pytest.mark.parametrize("n", [1, 3, 40])
 def test_max_hits_exact_round_first(gpu_device, monkeypatch, n):
-    """--max_hits n runs an exact round first and the full scheme only on the
-    queries with fewer than n exact positions (capi.cpp searchExactFirst):
+    """--max_hits n with SAHARA_MAXHITS_ROUNDS=2 runs an exact round first and
+    the full scheme only on the queries with fewer than n exact positions
+    (capi.cpp searchExactFirst):
     equal to the policy over the oracle's full hits, with queries of every
     kind — exact repeats with hundreds of positions (leave after the exact
     round), exact reads with a few positions, and reads with 1-2 errors (need
@@ -550,6 +551,7 @@ def test_max_hits_exact_round_first(gpu_device, monkeypatch, n):
     complements, and the patterns call."""
     from test_golden import limit_rows
     monkeypatch.setenv("SAHARA_BATCH", "173")
+    monkeypatch.setenv("SAHARA_MAXHITS_ROUNDS", "2")
     rng = np.random.default_rng(90 + n)
     unit = random_records(rng, [60], 6)[0]
     rep = np.tile(unit, 300)
