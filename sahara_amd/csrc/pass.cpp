@@ -426,8 +426,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
             t.stealAt = 8;
             if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-            t.prefetch = 0;
-            if (const char* e = std::getenv("SAHARA_TEXT_PREFETCH")) t.prefetch = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
             if (resolveMode == 0)
                 launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
             if (split0) {

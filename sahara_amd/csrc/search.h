@@ -100,8 +100,6 @@ struct TextArgs {
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
-    uint32_t prefetch;       // at each refill, the lanes holding the next `prefetch` tasks of the current
-                             // chunk touch their window's and pattern's lines (into L2) (0: off)
 };
 
 struct LocateArgs {

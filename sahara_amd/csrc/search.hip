@@ -808,7 +808,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     }
     SlotRange hitSlots;
     uint2 cur = make_uint2(0, 0);
-    uint32_t pf[4] = {0u, 0u, 0u, 0u}, pfAcc = 0u;  // a.prefetch: the touched words (consumed, never used)
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
 
@@ -879,64 +878,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             }
             pending &= ~__ballot(mine);
             qNext += take;
-        }
-        if (a.prefetch && refill) {
-            // the lanes holding the current chunk's next tasks (records one
-            // per lane, positions resolved) touch the lines of their windows
-            // and patterns, so that the refills that start them find the
-            // lines in L2; the values are folded into pfAcc after the next
-            // refill's own copies, which wait for younger loads anyway
-            pfAcc ^= pf[0] ^ pf[1] ^ pf[2] ^ pf[3];
-            const uint32_t slotIdx = qBase + lane;
-            const bool pfMine = slotIdx >= qNext && slotIdx < qNext + a.prefetch && slotIdx < qEnd && curRec.y != 0u;
-            uint32_t o0 = kBufOOB, o1 = kBufOOB, o2 = kBufOOB, o3 = kBufOOB;
-            if (pfMine) {
-                const uint32_t pb = (curRec.w >> 24) * m, pm = curRec.w & 0x00FFFFFFu;
-                const uint32_t ppos = pm & 0xFFFFu, pe = (pm >> 16) & 0xFu;
-                const uint32_t pca = SC[pb + ppos].y & 0xFFFu;
-                const uint32_t pK = (SC[pb + m - 1u].x >> 20) & 0xFu;
-                const uint32_t pleft = pca + (pK > pe ? pK - pe : 0u);
-                const uint32_t pwb = curRec.x > pleft ? curRec.x - pleft : 0u;
-                const uint32_t t0 = (pwb >> 5) * 16u, t1 = t0 + (winBlocks + 1u) * 16u - 4u;
-                o0 = t0 & ~63u;
-                o1 = (t1 & ~63u) != o0 ? (t1 & ~63u) : kBufOOB;
-                const uint32_t q0 = curRec.z * patBlocks * 16u, q1 = q0 + patBlocks * 16u - 4u;
-                o2 = q0 & ~63u;
-                o3 = (q1 & ~63u) != o2 ? (q1 & ~63u) : kBufOOB;
-            }
-            pf[0] = __builtin_amdgcn_raw_buffer_load_b32(textBuf, o0, 0, 0);
-            pf[1] = __builtin_amdgcn_raw_buffer_load_b32(textBuf, o1, 0, 0);
-            pf[2] = __builtin_amdgcn_raw_buffer_load_b32(patBuf, o2, 0, 0);
-            pf[3] = __builtin_amdgcn_raw_buffer_load_b32(patBuf, o3, 0, 0);
-        }
-        if (a.prefetch && refill) {
-            // the lanes holding the current chunk's next tasks (records one
-            // per lane, positions resolved) touch the lines of their windows
-            // and patterns, so that the refills that start them find the
-            // lines in L2; the values are folded into pfAcc after the next
-            // refill's own copies, which wait for younger loads anyway
-            pfAcc ^= pf[0] ^ pf[1] ^ pf[2] ^ pf[3];
-            const uint32_t slotIdx = qBase + lane;
-            const bool pfMine = slotIdx >= qNext && slotIdx < qNext + a.prefetch && slotIdx < qEnd && curRec.y != 0u;
-            uint32_t o0 = kBufOOB, o1 = kBufOOB, o2 = kBufOOB, o3 = kBufOOB;
-            if (pfMine) {
-                const uint32_t pb = (curRec.w >> 24) * m, pm = curRec.w & 0x00FFFFFFu;
-                const uint32_t ppos = pm & 0xFFFFu, pe = (pm >> 16) & 0xFu;
-                const uint32_t pca = SC[pb + ppos].y & 0xFFFu;
-                const uint32_t pK = (SC[pb + m - 1u].x >> 20) & 0xFu;
-                const uint32_t pleft = pca + (pK > pe ? pK - pe : 0u);
-                const uint32_t pwb = curRec.x > pleft ? curRec.x - pleft : 0u;
-                const uint32_t t0 = (pwb >> 5) * 16u, t1 = t0 + (winBlocks + 1u) * 16u - 4u;
-                o0 = t0 & ~63u;
-                o1 = (t1 & ~63u) != o0 ? (t1 & ~63u) : kBufOOB;
-                const uint32_t q0 = curRec.z * patBlocks * 16u, q1 = q0 + patBlocks * 16u - 4u;
-                o2 = q0 & ~63u;
-                o3 = (q1 & ~63u) != o2 ? (q1 & ~63u) : kBufOOB;
-            }
-            pf[0] = __builtin_amdgcn_raw_buffer_load_b32(textBuf, o0, 0, 0);
-            pf[1] = __builtin_amdgcn_raw_buffer_load_b32(textBuf, o1, 0, 0);
-            pf[2] = __builtin_amdgcn_raw_buffer_load_b32(patBuf, o2, 0, 0);
-            pf[3] = __builtin_amdgcn_raw_buffer_load_b32(patBuf, o3, 0, 0);
         }
         if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
         // ---- work stealing inside the wave once the task queue is dry (wave-
@@ -1196,8 +1137,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         if (COUNT) cyEmit += clock64() - t0;
     }
     hitSlots.close(lane, a.hits, a.hitCap);
-    pfAcc ^= pf[0] ^ pf[1] ^ pf[2] ^ pf[3];
-    if (a.prefetch == 0xFFFFFFFFu && pfAcc == 0x5A5A5A5Au) atomicOr(a.flags, 0u);  // keeps the touches (never true)
     if (filled) atomicAdd(a.filled, filled);  // per-lane counts
     if (__any(bad) && lane == 0) atomicOr(a.flags, 16u);
     if (COUNT) {
