@@ -160,6 +160,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // fewer for schemes with many searches (work items must fit 2^31);
     // SAHARA_BATCH sets it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(c->streaming ? 1ull << 21 : 1ull << 22, (1ull << 31) / c->nsearch);
+    // (SAHARA_STREAM_BATCHES: a streamed call takes at least this many
+    // batches, >= 256K patterns each, so that a small call still overlaps its
+    // upload with its search; 0 = off)
+    if (c->streaming)
+        if (const char* e = std::getenv("SAHARA_STREAM_BATCHES"); e && std::atoi(e) > 0)
+            maxBatch = std::min(maxBatch, std::max<uint64_t>(1ull << 18, (c->npat + std::atoi(e) - 1) / std::atoi(e)));
     if (const char* e = std::getenv("SAHARA_BATCH"))
         maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
     if (c->blockRecs) maxBatch = std::min<uint64_t>(maxBatch, 1ull << 27);  // compact records: qid - q0 < 2^28

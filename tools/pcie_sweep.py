@@ -44,23 +44,28 @@ def main():
     ap.add_argument("--max-hits", type=int, default=0, help="sahara_gpu_search_reads with --max_hits N")
     ap.add_argument("--read-errors", type=int, default=2, help="errors simulated per read (search k stays 2)")
     ap.add_argument("--marks", type=int, default=0, help="then this many calls with SAHARA_TIMING=2 (host marks, stderr)")
+    ap.add_argument("--config", default=None, help="a bench.py config (c2, c3, c5): its text, reads and scheme")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     import bench
     import sahara_amd as sa
-    lens = bench.record_lengths(3_000_000_000, 24)
+    ref_len, nrec, nreads, rlen, k, edit, gen = bench.CONFIGS[a.config or "c3"]
+    if a.config:
+        a.reads, a.read_errors = nreads, k
+    lens = bench.record_lengths(ref_len, nrec)
     flat, lens = sa.synth_reference(lens, sigma=6, seed=42)
     idx = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=0)
-    reads = sa.synth_reads(flat, lens, a.reads, 100, a.read_errors, sigma=6, seed=7)
+    reads = sa.synth_reads(flat, lens, a.reads, rlen, a.read_errors, sigma=6, seed=7)
     del flat
-    sch = sa.search_scheme("h2-k2", 0, 2, 100)
+    sch = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
     aff = sorted(os.sched_getaffinity(0))
     print(f"placement {idx.placement()}, process CPUs {len(aff)} ({aff[:4]}..{aff[-4:]})", flush=True)
     cg0 = cgroup_stat()
     print(f"cgroup cpu.max {cg0.get('cpu.max')}, stat {cg0}", flush=True)
-    call = (lambda: sa.search_reads(idx, reads, sch)) if a.full else (lambda: sa.search_reads_compact(idx, reads, sch))
+    call = ((lambda: sa.search_reads(idx, reads, sch, edit=edit)) if a.full
+            else (lambda: sa.search_reads_compact(idx, reads, sch, edit=edit)))
     if a.max_hits:
-        call = lambda: sa.search_reads(idx, reads, sch, max_hits=a.max_hits)
+        call = lambda: sa.search_reads(idx, reads, sch, edit=edit, max_hits=a.max_hits)
     sets = []
     for s in a.settings:
         name, _, kv = s.partition("=")
