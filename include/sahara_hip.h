@@ -140,10 +140,8 @@ int  sahara_gpu_set_mode(void* ctx, int verify, int locate_sa);
  * applied by the caller for edit == 0, search.cpp:226).
  * max_hits > 0 is search_n (search.cpp:228,231): per query at most max_hits
  * distinct (seq_id, pos), fewest errors first, each once with its minimum e
- * (upstream's counting rule is unverified); with
- * SAHARA_MAXHITS_ROUNDS=2 a query with max_hits distinct exact positions is
- * answered by an exact round alone, the full scheme runs only on the others
- * (single-part indexes). Hits come back sorted by
+ * (upstream's counting rule is unverified), applied per batch
+ * on the device before the download. Hits come back sorted by
  * (qid, seq_id, pos, err) in a buffer released with sahara_gpu_free. */
 int  sahara_gpu_search(void* ctx, const uint8_t* ranks, uint64_t n_patterns, uint32_t len,
                        const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,

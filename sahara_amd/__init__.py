@@ -385,17 +385,34 @@ def search_reads(index, reads, scheme, edit=True, reverse=True, limit=0, max_hit
     return _hits_array(out, n.value)
 
 
+class _OwnedRecords:
+    """numpy array interface over library-owned records that keeps their owner
+    alive: an array made from it (CompactHits.recs, and every view of that)
+    holds the CompactHits, so its memory cannot go back to the library's pool
+    while any of them exists."""
+
+    def __init__(self, owner, addr, n):
+        self._owner = owner
+        self.__array_interface__ = {"shape": (n,), "typestr": "<u8", "data": (addr, True), "version": 3}
+
+
 class CompactHits:
     """Hits of sahara_gpu_search_reads_compact (include/sahara_hip.h
     sahara_hit_blocks): 8-B records in page-locked host memory, one block per
-    batch. `recs` is a zero-copy view; to_hits() expands them to HIT_DTYPE.
-    The library memory goes back with close() or the last reference."""
+    batch. `recs` is a read-only zero-copy view that keeps this object (and so
+    the memory) alive; close() releases the memory at once, after which views
+    taken earlier must not be read (copy them first). to_hits() expands the
+    records to HIT_DTYPE."""
 
     def __init__(self, blocks, index):
         self._b = blocks
         self._index = index  # rec_starts belongs to the context
         n = blocks.n_hits
-        self.recs = np.ctypeslib.as_array(blocks.recs, shape=(n,)) if n else np.zeros(0, np.uint64)
+        if n:
+            addr = C.cast(blocks.recs, C.c_void_p).value
+            self.recs = np.asarray(_OwnedRecords(self, addr, n))
+        else:
+            self.recs = np.zeros(0, np.uint64)
         nb = blocks.n_blocks
         self.block_qid0 = np.ctypeslib.as_array(blocks.block_qid0, shape=(nb,)).copy() if nb else np.zeros(0, np.uint64)
         self.block_end = np.ctypeslib.as_array(blocks.block_end, shape=(nb,)).copy() if nb else np.zeros(0, np.uint64)

@@ -131,22 +131,6 @@ Placement placementOfNode(int node) {
     return pl;
 }
 
-// The NUMA node holding most of [p, p + n) (16 sampled pages, move_pages
-// with no target: a query), or -1
-int nodeOfBuffer(const void* p, uint64_t n) {
-    if (!p || n == 0) return -1;
-    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
-    void* pages[16];
-    int status[16];
-    for (int k = 0; k < 16; ++k)
-        pages[k] = reinterpret_cast<void*>(((uintptr_t)p + (uintptr_t)(n * (uint64_t)k / 16)) & ~(pg - 1));
-    if (syscall(SYS_move_pages, 0, 16UL, pages, nullptr, status, 0) != 0) return -1;
-    int votes[64] = {0}, best = -1;
-    for (int k = 0; k < 16; ++k)
-        if (status[k] >= 0 && status[k] < 64 && ++votes[status[k]] > (best >= 0 ? votes[best] : 0)) best = status[k];
-    return best;
-}
-
 // The CPUs of the device's NUMA node that this process may run on (Placement).
 static void placeNear(Ctx* c) {
     const char* e = std::getenv("SAHARA_NUMA");
@@ -635,7 +619,7 @@ static void copyOut(Ctx* c, void* dst, const void* src, size_t bytes) {
 // issued batches may still run and copy into the sink).
 static void drainAll(Ctx* c) {
     drainPacking(c);  // chunks packed ahead: nothing reads the caller's buffer after the call
-    for (hipStream_t s : {c->st, c->stB, c->stC, c->stD, c->stE, c->stF, c->stUp[0], c->stUp[1], c->stUp[2]})
+    for (hipStream_t s : {c->st, c->stB, c->stC, c->stD, c->stE, c->stF})
         if (s) (void)hipStreamSynchronize(s);
 }
 
@@ -651,114 +635,6 @@ static void printDmaTimes(Ctx* c) {
     c->dmaUsed = 0;
 }
 
-// --max_hits n in two rounds (search_n stopping early, exact under U6): an
-// exact search of every query first (one error-free search over the whole
-// pattern), limited on the device to n positions per query. A query with n
-// exact positions is done: its n best are exact ones, the n smallest
-// (seq_id, pos), each with e = 0, and the exact round finds all of them. Only
-// the other queries run the full scheme, as a subset gathered on the device
-// from the patterns the first round staged. A repetitive query, which costs
-// the most in the full search, leaves after the cheap round. Off by default
-// (SAHARA_MAXHITS_ROUNDS=2 turns it on): at C3 (reads with two errors, so the
-// exact round retires 0.08% of the queries) the two rounds and their host-side
-// merge took 1.5 s per call against 16.5 ms for one round, and 0.66 s against
-// 0.25 s with error-free reads (half the queries retired;
-// profiles/r03_final_maxhits_e{2,0}.txt, before the merge replaced a sort).
-static void searchExactFirst(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t len,
-                             const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit,
-                             uint32_t n, sahara_hit** hits, uint64_t* n_hits) {
-    using clk = std::chrono::steady_clock;
-    const auto tA = clk::now();
-    std::vector<uint32_t> epi(len), ezero(len, 0);
-    for (uint32_t i = 0; i < len; ++i) epi[i] = i;
-    sahara_stats acc{};
-    auto addStats = [&] {
-        acc.batches += c->stats.batches;
-        acc.cursors += c->stats.cursors;
-        acc.search_ms += c->stats.search_ms;
-        acc.locate_ms += c->stats.locate_ms;
-        acc.sort_ms += c->stats.sort_ms;
-        acc.text_ms += c->stats.text_ms;
-    };
-    auto download = [&](std::vector<sahara_hit>& v) {
-        v.resize(c->nout);
-        if (c->nout) SH_HIP(hipMemcpy(v.data(), c->out.ptr, c->nout * sizeof(sahara_hit), hipMemcpyDeviceToHost));
-    };
-    std::vector<sahara_hit> all, v;
-    uint64_t rest = 0;
-    try {
-        stageStreamed(c, src, rows, rc, npat, len, epi.data(), ezero.data(), ezero.data(), 1, edit);
-        c->sink = nullptr;
-        c->sinkCap = 0;
-        c->compactSink = c->sinkPinned = false;
-        c->blockRecs = nullptr;
-        c->limitN = n;
-        run(c, false);
-        c->limitN = 0;
-        uint32_t bad = 0;
-        SH_HIP(hipMemcpy(&bad, c->badFlag.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost));
-        if (bad) throw Error("pattern rank out of range for this index");
-        c->streaming = false;  // every pattern is staged on the device
-        acc.stage_ms += c->up.hostMs;
-        addStats();
-        download(v);
-        std::vector<uint32_t> cnt(npat, 0);
-        for (const auto& h : v) ++cnt[h.qid];
-        std::vector<uint64_t> todo;
-        for (uint64_t q = 0; q < npat; ++q)
-            if (cnt[q] < n) todo.push_back(q);
-        for (const auto& h : v)
-            if (cnt[h.qid] >= n) all.push_back(h);
-        const size_t kept = all.size();
-        rest = todo.size();
-        if (!todo.empty()) {
-            DevBuf<uint64_t> idx;
-            idx.reserve(todo.size());
-            SH_HIP(hipMemcpy(idx.ptr, todo.data(), todo.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-            DevBuf<uint32_t> np;
-            DevBuf<uint4> np3;
-            np.reserve(todo.size() * c->patWords + 4);  // + tail words read by paired loads
-            np3.reserve(todo.size() * c->patBlocks);
-            launchGatherPatterns(c->pats.ptr, c->pats3.ptr, idx.ptr, todo.size(), c->patWords, c->patBlocks, np.ptr,
-                                 np3.ptr, c->st);
-            SH_HIP(hipStreamSynchronize(c->st));
-            std::swap(c->pats, np);
-            std::swap(c->pats3, np3);
-            stageScheme(c, todo.size(), len, pi, l, u, ns, edit);
-            c->npat = todo.size();
-            c->limitN = n;
-            run(c, false);
-            c->limitN = 0;
-            addStats();
-            download(v);
-            for (auto h : v) {
-                h.qid = todo[h.qid];
-                all.push_back(h);
-            }
-            // both runs are in (qid, seq_id, pos, err) order: one linear merge
-            std::inplace_merge(all.begin(), all.begin() + (ptrdiff_t)kept, all.end(), hitLess);
-        }
-    } catch (...) {
-        c->limitN = 0;
-        drainAll(c);
-        c->staged = c->streaming = false;
-        throw;
-    }
-    c->staged = false;  // the device holds a subset now: sahara_gpu_run has nothing to re-run
-    acc.patterns = npat;
-    acc.hits = all.size();
-    acc.total_ms = std::chrono::duration<double, std::milli>(clk::now() - tA).count();
-    c->stats = acc;
-    c->stats.upload_chunks[0] = c->up.chunks[0];
-    c->stats.upload_chunks[1] = c->up.chunks[1];
-    c->stats.upload_chunks[2] = c->up.chunks[2];
-    if (std::getenv("SAHARA_TIMING"))
-        std::fprintf(stderr, "[sahara] --max_hits %u: exact round kept %llu of %llu queries, full scheme on %llu, %.1f ms\n",
-                     n, (unsigned long long)(npat - rest), (unsigned long long)npat, (unsigned long long)rest,
-                     acc.total_ms);
-    handOver(all, hits, n_hits);
-}
-
 // sahara_gpu_search / sahara_gpu_search_reads: streamed upload, the pipelined
 // pass, the hits streamed into a pinned host sink batch by batch, then handed
 // to the caller (search.cpp:218-250 from host queries to host hits).
@@ -772,16 +648,6 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         c->traceOn = te && std::atoi(te) >= 2;
         c->traceT0 = tA;
         c->trace.clear();
-    }
-    if (max_hits && c->more.empty()) {  // two rounds, exact first (multi-part: the cut after merging)
-        uint32_t maxU = 0;
-        for (uint64_t i = 0; i < (uint64_t)n_searches * len; ++i) maxU = std::max(maxU, u[i]);
-        const char* r = std::getenv("SAHARA_MAXHITS_ROUNDS");
-        if (maxU > 0 && r && std::atoi(r) == 2) {
-            searchExactFirst(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit, max_hits, hits, n_hits);
-            c->traceOn = false;
-            return;
-        }
     }
     stageStreamed(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit);
     const auto tB = clk::now();
@@ -956,8 +822,9 @@ static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, u
         c->traceT0 = tA;
         c->trace.clear();
     }
+    for (uint64_t i = 0; i < (uint64_t)n_searches * len; ++i)  // before staging: a refused call stages nothing
+        if (u[i] > 15) throw Error("compact hit records hold at most 15 errors");
     stageStreamed(c, reads, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit);
-    if (c->maxErr > 15) throw Error("compact hit records hold at most 15 errors");
     c->sink = nullptr;
     c->compactSink = c->sinkPinned = false;
     // the sink, sized from the last call (else 2 hits per pattern), always
@@ -965,17 +832,19 @@ static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, u
     const uint64_t est = c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * npat + 1024;
     bool pinned = false;
     size_t capBytes = 0;
-    void* sinkMem = allocPinned(est * 8, &pinned, &capBytes, true, true);
-    if (!sinkMem) throw Error("out of host memory for hits");
-    if (const char* e = std::getenv("SAHARA_BLOCK_WRITE_WG")) c->blockWriteBlocks = (uint32_t)std::max(1, std::atoi(e));
-    c->blockRecs = pinned ? static_cast<uint64_t*>(sinkMem) : nullptr;
-    c->sinkCap = pinned ? capBytes / 8 : 0;
-    {
-        // SAHARA_COMPACT_DMA=0: the kernel writes the records into the sink
-        // itself (PCIe writes from 64 workgroups beside the text phase)
-        const char* e = std::getenv("SAHARA_COMPACT_DMA");
-        c->compactDma = !e || std::atoi(e) != 0;
-        if (c->compactDma && c->sinkCap) c->outRecs.reserve(c->sinkCap);
+    void* sinkMem = nullptr;
+    try {
+        sinkMem = allocPinned(est * 8, &pinned, &capBytes, true, true);
+        if (!sinkMem) throw Error("out of host memory for hits");
+        c->blockRecs = pinned ? static_cast<uint64_t*>(sinkMem) : nullptr;
+        c->sinkCap = pinned ? capBytes / 8 : 0;
+        if (c->sinkCap) c->outRecs.reserve(c->sinkCap);
+    } catch (...) {  // nothing may stream from the caller's reads after the call
+        drainPacking(c);
+        freeHits(sinkMem);
+        c->blockRecs = nullptr;
+        c->staged = c->streaming = false;
+        throw;
     }
     auto* recs = static_cast<uint64_t*>(sinkMem);
     uint64_t recCap = capBytes / 8;

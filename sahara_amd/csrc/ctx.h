@@ -411,14 +411,6 @@ struct Ctx {
     } up;
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
-    // more upload streams (SAHARA_UPLOAD_STREAMS = 1 + how many are used): a
-    // chunk's DMA splits into equal parts, one per stream, so that several
-    // copy engines move it; stE waits for the others' parts (upPartEv) before
-    // it records the chunk's ringEv
-    static constexpr int kUpStreams = 3;
-    hipStream_t stUp[kUpStreams] = {};
-    hipEvent_t upPartEv[kUpStreams] = {};
-    uint32_t upStreams = 1;
     // SAHARA_TIMING=2: timing events around each chunk's DMA (bytes, events)
     std::vector<std::pair<uint64_t, std::pair<hipEvent_t, hipEvent_t>>> dmaEv;
     size_t dmaUsed = 0;
@@ -444,7 +436,6 @@ struct Ctx {
     unsigned poolCap = 0;
     Placement packPlace;                  // the pool's CPUs when bound
     int poolNode = -2;                    // NUMA node the pool is bound to (-1: unbound)
-    int srcNode = -1;                     // node of the streamed call's source rows (SAHARA_PACK_BIND=2)
     // host sink of sahara_gpu_search: each batch's sorted hits go to host
     // memory (pinned) on stF while later batches search
     sahara_hit* sink = nullptr;
@@ -463,16 +454,13 @@ struct Ctx {
     std::vector<hipEvent_t> downEv;
     std::unique_ptr<Expander> expander;
     // sahara_gpu_search_reads_compact: each batch's hits as 8-B records,
-    // written by kCompactHits (blockWriteBlocks workgroups) straight into
-    // this pinned host buffer (sinkCap records) on stF; per batch its first
-    // qid and one past its last record (the blocks of sahara_hit_blocks)
+    // made by kCompactHits in HBM (outRecs, sinkCap entries) and copied by a
+    // copy engine on stF into this pinned host buffer (sinkCap records); per
+    // batch its first qid and one past its last record (the blocks of
+    // sahara_hit_blocks). (Written by the kernel straight into the sink over
+    // PCIe, the records held CU slots beside the text phase: C3 592M against
+    // 632M reads/s with the copy engine, profiles/r03_pcie_compact_dma.txt.)
     uint64_t* blockRecs = nullptr;
-    uint32_t blockWriteBlocks = 64;
-    // the records are made in HBM (outRecs, sinkCap entries) and copied down
-    // by a copy engine (SAHARA_COMPACT_DMA=0: written by the kernel into the
-    // sink over PCIe; C3 592M -> 632M reads/s with the copy engine,
-    // profiles/r03_pcie_compact_dma.txt)
-    bool compactDma = false;
     DevBuf<uint64_t> outRecs;
     std::vector<uint64_t> batchQ0, batchEnd;
     std::vector<uint64_t> recStartsEnd;   // record starts + the text length (sahara_hit_blocks.rec_starts)
@@ -513,10 +501,6 @@ struct Ctx {
             (void)hipEventDestroy(d.second.first);
             (void)hipEventDestroy(d.second.second);
         }
-        for (int i = 0; i < kUpStreams; ++i) {
-            if (stUp[i]) (void)hipStreamDestroy(stUp[i]);
-            if (upPartEv[i]) (void)hipEventDestroy(upPartEv[i]);
-        }
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
             for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
@@ -554,7 +538,6 @@ unsigned hostThreads(const Ctx* c, unsigned cap);
 Ctx* ctxOf(void* p);
 TaskPool& hostPool(Ctx* c);
 Placement placementOfNode(int node);
-int nodeOfBuffer(const void* p, uint64_t n);
 // every pack job posted by the streamed upload is finished (the caller's
 // source buffer is no longer read): before a new call stages, after a failed one
 void drainPacking(Ctx* c);

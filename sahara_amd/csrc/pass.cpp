@@ -108,6 +108,8 @@ void run(Ctx* c, bool count) {
 void runOne(Ctx* c, bool count) {
     if (!c->staged) throw Error("sahara_gpu_run: nothing staged");
     auto t0 = std::chrono::steady_clock::now();
+    // SAHARA_PIPELINE=0 (profiling hook): batch after batch on one stream, so
+    // that a kernel trace shows each kernel's stand-alone duration
     if (const char* e = std::getenv("SAHARA_PIPELINE")) c->pipeline = std::atol(e) != 0;
     sahara_stats S{};
     bool overflow = false;
@@ -160,12 +162,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // fewer for schemes with many searches (work items must fit 2^31);
     // SAHARA_BATCH sets it (tests of the pipeline)
     uint64_t maxBatch = std::min<uint64_t>(c->streaming ? 1ull << 21 : 1ull << 22, (1ull << 31) / c->nsearch);
-    // (SAHARA_STREAM_BATCHES: a streamed call takes at least this many
-    // batches, >= 256K patterns each, so that a small call still overlaps its
-    // upload with its search; 0 = off)
-    if (c->streaming)
-        if (const char* e = std::getenv("SAHARA_STREAM_BATCHES"); e && std::atoi(e) > 0)
-            maxBatch = std::min(maxBatch, std::max<uint64_t>(1ull << 18, (c->npat + std::atoi(e) - 1) / std::atoi(e)));
     if (const char* e = std::getenv("SAHARA_BATCH"))
         maxBatch = std::max<uint64_t>(1, std::min<uint64_t>((1ull << 31) / c->nsearch, std::atoll(e)));
     if (c->blockRecs) maxBatch = std::min<uint64_t>(maxBatch, 1ull << 27);  // compact records: qid - q0 < 2^28
@@ -184,21 +180,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // window: |t| + what both sides can still consume <= m + 2k symbols, plus
     // the block alignment of its start (31 symbols); 3 words per block
     // (exact start: m + 2k symbols in whole blocks, copied funnel-shifted from
-    // one block more; SAHARA_EXACT_WINDOW=0: the block-aligned start below it)
-    const char* exactEnv = std::getenv("SAHARA_EXACT_WINDOW");
+    // one block more, where both fit the copy's 8 loads; else the block-aligned
+    // start below it)
     const uint32_t exactBlocks = (c->m + 2 * c->maxErr + 31) / 32;
-    const bool exactWindow = (!exactEnv || std::atoi(exactEnv) != 0) && exactBlocks + 1 <= 8 && c->patBlocks <= 8;
+    const bool exactWindow = exactBlocks + 1 <= 8 && c->patBlocks <= 8;
     const uint32_t winBlocks = exactWindow ? exactBlocks : (c->m + 2 * c->maxErr + 31 + 31) / 32;
     const uint32_t textStack = 2 * c->maxErr + 2;
-    // one-word stack entries where a node fits 30 bits (search.hip packNode)
-    // (SAHARA_PACKED_STACK; off by default: at m = 100 it buys a fourth text
-    // workgroup per CU, but costs a pack / unpack per micro-step, and three
-    // workgroups leave LDS for an FM workgroup beside them)
-    const bool packedStack = c->m <= 127 && winBlocks <= 7 && c->maxErr <= 7 && std::getenv("SAHARA_PACKED_STACK") &&
-                             std::atoi(std::getenv("SAHARA_PACKED_STACK")) != 0;
     const uint32_t tableWords = std::max<uint32_t>(2 * c->nsearch * c->m, kTextTableMin);
-    const size_t textLds = (size_t)tableWords * 4 +
-                           (size_t)256 * (3 * (winBlocks + c->patBlocks) + (packedStack ? 1 : 2) * textStack) * 4;
+    const size_t textLds = (size_t)tableWords * 4 + (size_t)256 * (3 * (winBlocks + c->patBlocks) + 2 * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
@@ -207,30 +196,19 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
-        tbpc = textBlocksPerCU(sigma, c->edit, packedStack, textLds);
+        tbpc = textBlocksPerCU(sigma, c->edit, textLds);
     // overlapped with the FM phase, three text workgroups per CU beside its one
     // (four would fit: r2 v8 measured text 4 against 3 in alternating pairs,
     // C3 914-943M vs 880-952M on one box and 873-914M vs 953-956M on another,
     // C2 950-1013M vs 956-1026M: the sign flips with the box)
     if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
-    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, packedStack, textLds), std::atoi(e)));
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, textLds), std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
-    // where a task's SA row becomes its text position: 2 = inside the text
-    // kernel, a chunk of task records ahead (default: no pass between the FM
-    // and text phases); 1 = kResolveTasks after the FM phase on its stream;
-    // 0 = kResolveTasks before the text phase (SAHARA_RESOLVE)
-    uint32_t fmPrio = 0;
-    if (const char* e = std::getenv("SAHARA_FM_PRIO")) fmPrio = (uint32_t)std::max(0, std::min(3, std::atoi(e)));
-    int resolveMode = 2;
-    if (const char* e = std::getenv("SAHARA_RESOLVE")) resolveMode = std::max(0, std::min(2, std::atoi(e)));
-    // (pipelined, in-kernel task resolve) the first batch's text phase starts
-    // on its seed tasks while its FM phase runs (SAHARA_EARLY_TEXT=0: after it)
-    const char* earlyEnv = std::getenv("SAHARA_EARLY_TEXT");
-    // (only with several batches: a lone batch's FM phase runs at full
-    // occupancy, and its text phase split in two measured 45M against 68M
-    // reads/s at C5)
-    const bool early = !serial && split && resolveMode == 2 && batchesHere > 1 &&
-                       (!earlyEnv || std::atoi(earlyEnv) != 0);
+    // (pipelined) the first batch's text phase starts on its seed tasks while
+    // its FM phase runs; only with several batches: a lone batch's FM phase
+    // runs at full occupancy, and its text phase split in two measured 45M
+    // against 68M reads/s at C5
+    const bool early = !serial && split && batchesHere > 1;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -243,27 +221,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
     }
-    // batch boundaries. SAHARA_RAMP (pipelined only): 1 makes the first two
-    // batches smaller (1/4, 1/2 of the others) so that the FM phase of the
-    // first, which overlaps nothing, is short; 2 also the last two
+    // batch boundaries: equal batches of <= maxBatch patterns
     std::vector<uint64_t> bstart{0};
-    {
-        const int rampMode = std::getenv("SAHARA_RAMP") ? std::atoi(std::getenv("SAHARA_RAMP")) : 0;
-        const bool up = !serial && rampMode >= 1 && c->npat > 3 * maxBatch;
-        const bool down = up && rampMode >= 2;
-        const uint64_t edge[2] = {std::max<uint64_t>(maxBatch / 4, 1), std::max<uint64_t>(maxBatch / 2, 1)};
-        const uint64_t mid = c->npat - (up ? edge[0] + edge[1] : 0) - (down ? edge[0] + edge[1] : 0);
-        if (up) {
-            bstart.push_back(edge[0]);
-            bstart.push_back(edge[0] + edge[1]);
-        }
-        const uint64_t nmid = (mid + maxBatch - 1) / maxBatch, q0 = bstart.back();
-        for (uint64_t i = 1; i <= nmid; ++i) bstart.push_back(q0 + mid * i / nmid);
-        if (down) {
-            bstart.push_back(bstart.back() + edge[1]);
-            bstart.push_back(bstart.back() + edge[0]);
-        }
-    }
+    for (uint64_t i = 1; i <= batchesHere; ++i) bstart.push_back(c->npat * i / batchesHere);
     const uint64_t nbatch = bstart.size() - 1;
     // per batch, 16 words of pinned host memory: the slot's counters (0-6),
     // the locate flags (7), the row total (8-9), the long / huge segment
@@ -273,8 +233,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     if (c->pinnedCap < nbatch * 16) {
         if (c->pinned) SH_HIP(hipHostFree(c->pinned));
         c->pinned = nullptr;
-        SH_HIP(hipHostMalloc(&c->pinned, nbatch * 8 * sizeof(uint32_t)));
         c->pinnedCap = nbatch * 16;
+        SH_HIP(hipHostMalloc(&c->pinned, c->pinnedCap * sizeof(uint32_t)));
     }
     if (c->qcnt.cap < maxBatch + 1) {
         c->qcnt.reserve(maxBatch + 1);
@@ -336,7 +296,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.taskCap = c->taskCap;
         a.split = split;
         a.ldsDepth = fmLdsDepth;
-        a.prio = serial ? 0u : fmPrio;
         // starting cursors; reference execution (verify off) ranks every node
         // from the root, so it does not use the k-mer table
         SeedArgs sd{};
@@ -371,18 +330,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // the batches before it search; unpacked on sD ahead of its seeds)
         ensureUploaded(c, bstart[b + 1], sD);
         SH_HIP(hipEventRecord(sl.fmStart, sD));
-        // (SAHARA_SEED_BPC: workgroups per CU of the seeds after the first batch's)
-        uint32_t seedBpc = 8;
-        if (const char* e = std::getenv("SAHARA_SEED_BPC"); e && b > 0) seedBpc = (uint32_t)std::max(1, std::min(8, std::atoi(e)));
-        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * seedBpc), sD);
+        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sD);
         if (early && b == 0)  // the seed tasks end here: the text phase may start on them
             SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
         SH_HIP(hipEventRecord(sl.seedDone, sD));
         SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
         SH_HIP(hipEventRecord(sl.fmBegin, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
-        if (split && resolveMode == 1)
-            launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sA);
         SH_HIP(hipEventRecord(sl.fmDone, sA));
         ++S.search_launches;
     };
@@ -416,14 +370,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.counters = c->counters.ptr;
             t.winBlocks = winBlocks;
             t.exactWindow = exactWindow ? 1u : 0u;
-            // (SAHARA_PRUNE=0 turns it off; C3: 43 -> 28 micro-steps per read,
-            // C5: 439 -> 303 and 68M -> 82M reads/s)
-            const char* pruneEnv = std::getenv("SAHARA_PRUNE");
-            t.prune = !pruneEnv || std::atoi(pruneEnv) != 0 ? 1u : 0u;
             t.stackCap = textStack;
-            t.packedStack = packedStack ? 1u : 0u;
             t.tableWords = tableWords;
-            t.resolveRows = resolveMode == 2 ? 1u : 0u;
             t.steps = c->textSteps;
             t.refillAt = c->refillAt;
             // in-wave work stealing at the launch's end, once SAHARA_STEAL_AT
@@ -432,8 +380,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
             t.stealAt = 8;
             if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-            if (resolveMode == 0)
-                launchResolveTasks(sl.tasks.ptr, sl.small.ptr + 4, c->taskCap, c->I.saFull.ptr, c->numCU * 8, sB);
             if (split0) {
                 // the first batch's seed tasks while its FM phase runs, then the
                 // tasks the FM phase appended after them
@@ -458,9 +404,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // overflow; `finishCheck` then reads the locate flags and timings.
     uint32_t seenTask = 0, seenHit = 0;  // pipelined overflow: the caps the re-run needs
     // a streamed call's finisher sleeps in its waits while the calling thread
-    // and the pool pack (SAHARA_SLEEPY_SYNC=0: spins, as in device-resident runs)
-    const char* sleepEnv = std::getenv("SAHARA_SLEEPY_SYNC");
-    const bool sleepy = c->streaming && !serial && (!sleepEnv || std::atoi(sleepEnv) != 0);
+    // and the pool pack (device-resident runs spin)
+    const bool sleepy = c->streaming && !serial;
     auto finish = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
@@ -521,13 +466,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         const uint32_t nbig2[2] = {pr[10], pr[11]};
         c->mark("rows", b);
         if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
-        uint32_t nbig = nbig2[0], nhuge = nbig2[1];
+        const uint32_t nbig = nbig2[0], nhuge = nbig2[1];
         const uint32_t* hugeList = c->huge.ptr;
-        if (const char* v = getenv("SAHARA_LDS_SORT"); v && v[0] == '0') {  // A/B: every long segment by radix sort
-            hugeList = c->big.ptr;
-            nhuge = nbig;
-            nbig = 0;
-        }
         c->k0.reserve(std::max<uint64_t>(rows, 1));
         if (nhuge) c->k1.reserve(std::max<uint64_t>(rows, 1));
         LocateArgs la{};
@@ -572,7 +512,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->batchEnd.push_back(c->nout + rows);
         if (c->sinkOk && c->nout + rows <= c->sinkCap) {
             const bool compact = c->compactSink && rows * sizeof(uint64_t) <= Ctx::kDownSlot && nb < (1ull << 28);
-            if (rows && c->blockRecs && c->compactDma) {
+            if (rows && c->blockRecs) {
                 // compact records made in HBM on sC (full grid, ~20 us), then
                 // one D2H copy on stF: a copy engine moves them, no workgroup
                 // waits on PCIe writes beside the text phase
@@ -582,10 +522,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                 SH_HIP(hipStreamWaitEvent(c->stF, c->ev[7], 0));
                 SH_HIP(hipMemcpyAsync(c->blockRecs + c->nout, c->outRecs.ptr + c->nout, rows * sizeof(uint64_t),
                                       hipMemcpyDeviceToHost, c->stF));
-            } else if (rows && c->blockRecs) {  // compact records written by the device into the pinned sink (PCIe writes)
-                SH_HIP(hipStreamWaitEvent(c->stF, c->ev[4], 0));
-                launchCompactHits(c->out.ptr + c->nout, rows, q0, c->I.dRecStarts.ptr, c->blockRecs + c->nout, c->stF,
-                                  c->blockWriteBlocks);
             } else if (rows && compact) {  // 8-B records, expanded on the host (Expander)
                 const uint64_t j = c->downJobs++;
                 const size_t slot = (size_t)(j % Ctx::kDownSlots);

@@ -37,7 +37,6 @@ struct SearchArgs {
     uint32_t* taskCount;
     uint32_t split;          // intervals of <= split rows go to the text phase (0: never)
     uint32_t ldsDepth;       // DFS levels kept in LDS (after the scheme table; the rest spill to HBM)
-    uint32_t prio;           // wave priority (s_setprio 0..3) when overlapped with the text phase
 };
 
 struct SeedArgs {
@@ -69,7 +68,7 @@ struct SeedArgs {
 constexpr uint32_t kTextTableMin = 3u * 256u;
 
 struct TextArgs {
-    const uint32_t* sa;      // full SA (resolveRows; else tasks arrive resolved by launchResolveTasks)
+    const uint32_t* sa;      // full SA: task records carry SA rows, the kernel reads their text positions
     const uint4* text3;      // text as 3-bit-plane blocks of 32 symbols (device_index.h)
     const uint4* pats3;      // patterns as 3-bit-plane blocks, patBlocks per pattern
     uint32_t patBlocks;
@@ -91,11 +90,8 @@ struct TextArgs {
     unsigned long long* counters;
     uint32_t winBlocks;      // window blocks per lane (32 symbols each)
     uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
-    uint32_t prune;          // 1: drop error children of e + 2 = u nodes that die in their first step
     uint32_t stackCap;       // text DFS stack entries per lane
-    uint32_t packedStack;    // 1: one-word stack entries (m <= 127, winBlocks <= 7, maxErr <= 7)
     uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)
-    uint32_t resolveRows;    // 1: task records carry SA rows; the kernel reads their text positions
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
@@ -119,12 +115,10 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
-int textBlocksPerCU(uint32_t sigma, bool edit, bool packedStack, size_t lds);
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);
-void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const uint32_t* sa, uint32_t blocks,
-                        hipStream_t st);
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st);
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst
@@ -141,15 +135,11 @@ struct MergeBufs {
 };
 void sortHitsByQid(const sahara_hit* in, uint64_t n, uint64_t nqid, sahara_hit* out, MergeBufs& B, DevBuf<char>& tmp,
                    hipStream_t st);
-void launchGatherPatterns(const uint32_t* pats, const uint4* pats3, const uint64_t* idx, uint64_t n, uint32_t patWords,
-                          uint32_t patBlocks, uint32_t* opats, uint4* opats3, hipStream_t st);
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
                        hipStream_t st, uint32_t maxBlocks = 8192);
 void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,
                      uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks, uint32_t* pats,
                      uint4* pats3, hipStream_t st);
-void launchUnpack2(const uint8_t* packed, uint8_t* dst, uint64_t n, uint32_t sigma, hipStream_t st);
-void launchPatchRank(const uint32_t* pos, uint64_t n, uint8_t* dst, uint32_t rank, hipStream_t st);
 // reads [r0, r1) (m bytes each) -> patterns [2 r0, min(2 r1, pEnd)): read, reverse complement, ...
 void launchInterleaveRC(const uint8_t* reads, uint64_t r0, uint64_t r1, uint32_t m, uint32_t sigma, uint64_t pEnd,
                         uint8_t* pats, hipStream_t st);

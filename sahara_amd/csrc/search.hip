@@ -352,14 +352,6 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
 template <int SIGMA, bool EDIT, bool COUNT>
 __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     extern __shared__ uint32_t sch[];
-    // Overlapped with the text phase, this latency-bound kernel's few
-    // instructions go first: the text phase (issue-bound) fills the rest.
-    switch (a.prio) {  // s_setprio takes an immediate
-        case 1: __builtin_amdgcn_s_setprio(1); break;
-        case 2: __builtin_amdgcn_s_setprio(2); break;
-        case 3: __builtin_amdgcn_s_setprio(3); break;
-        default: break;
-    }
     for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) sch[i] = a.scheme[i];
     __syncthreads();
 
@@ -710,26 +702,6 @@ __device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_
         if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[j][0]; D[256] = vb[j][1]; D[512] = vb[j][2]; }
 }
 
-// Text tasks carry an SA row; replace it by its text position (one SA read
-// per task, fully parallel) so the text kernel starts a task with one round trip.
-__global__ void kResolveTasks(uint4* __restrict__ tasks, const uint32_t* __restrict__ count, uint32_t cap,
-                              const uint32_t* __restrict__ sa) {
-    const uint32_t n = min(*count, cap);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        tasks[i].x = sa[tasks[i].x];
-}
-
-// One-word form of a text DFS node (PK): xo, yo (8 bits each) | pos (7) | e (3)
-// | lastL, lastR (2 each). Frees LDS for a fourth workgroup per CU at m = 100.
-__device__ __forceinline__ uint32_t packNode(uint2 v) {
-    return (v.x & 0xFFu) | ((v.x >> 8) & 0xFF00u) | ((v.y & 0x7Fu) << 16) | (((v.y >> 16) & 7u) << 23) |
-           (((v.y >> 20) & 0xFu) << 26);
-}
-__device__ __forceinline__ uint2 unpackNode(uint32_t w) {
-    return make_uint2((w & 0xFFu) | ((w & 0xFF00u) << 8),
-                      ((w >> 16) & 0x7Fu) | (((w >> 23) & 7u) << 16) | (((w >> 26) & 0xFu) << 20));
-}
-
 // SHAPE fixes the window and pattern block counts at compile time, so that
 // the task-start copy is straight-line code with no per-block conditions (the
 // generic form, SHAPE 0, keeps ~30 block masks in spilled SGPRs and reloads
@@ -741,7 +713,7 @@ struct TextShape { uint32_t win, pat; bool exact; };
 __host__ __device__ constexpr TextShape textShape(int shape) {
     return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
-template <int SIGMA, bool EDIT, bool COUNT, bool PK, int SHAPE = 0>
+template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     uint2* SC = reinterpret_cast<uint2*>(lds);
@@ -757,12 +729,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint32_t* W = slot + threadIdx.x;
     uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
     uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
-    uint32_t* S1 = slot + 3u * (winBlocks + patBlocks) * 256u + threadIdx.x;
-    auto stackGet = [&](uint32_t d) -> uint2 { return PK ? unpackNode(S1[d * 256u]) : S[d * 256u]; };
-    auto stackPut = [&](uint32_t d, const uint2& v) {
-        if (PK) S1[d * 256u] = packNode(v);
-        else S[d * 256u] = v;
-    };
+    auto stackGet = [&](uint32_t d) -> uint2 { return S[d * 256u]; };
+    auto stackPut = [&](uint32_t d, const uint2& v) { S[d * 256u] = v; };
     const uint32_t winLen = winBlocks * 32u;
     const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
     const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
@@ -782,11 +750,10 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
     uint32_t nBase = 0, nEnd = 0, qBase = 0;
     bool haveNext = false;
-    // resolveRows: the prefetched chunk's records still hold SA rows. Their
-    // text positions are read at the next refill, beside its window loads (one
-    // round trip for both), or at the latest when the chunk becomes current.
+    // The prefetched chunk's records still hold SA rows. Their text positions
+    // are read at the next refill, beside its window loads (one round trip for
+    // both), or at the latest when the chunk becomes current.
     bool nextRaw = false;
-    const bool resolve = a.resolveRows != 0u;
     auto resolveNext = [&]() {
         if (nextRaw) {  // wave-uniform
             if (nBase + lane < nEnd) nextRec.x = a.sa[nextRec.x];
@@ -801,7 +768,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             nEnd = e;
             if (b + lane < e) nextRec = tasks[b + lane];
             haveNext = true;
-            nextRaw = resolve;
+            nextRaw = true;
         } else {
             qDone = true;
         }
@@ -842,7 +809,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                         nEnd = e;
                         if (b + lane < e) nextRec = tasks[b + lane];
                         haveNext = true;
-                        nextRaw = resolve;
+                        nextRaw = true;
                     }
                 }
                 if (qNext >= qEnd) continue;
@@ -912,8 +879,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     const uint32_t* src = slot + dTid;
                     uint32_t* dst = slot + threadIdx.x;
                     for (uint32_t k = 0; k < 3u * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
-                    const uint2 node = PK ? unpackNode(slot[3u * (winBlocks + patBlocks) * 256u + dTid])
-                                          : reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
+                    const uint2 node = reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
                     cur = node;
                     pid = dPid;
                     wb = dWb;
@@ -1013,7 +979,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 Im &= R7EI;
                 Sx = Sx && ((R7E0 >> (L + 1u)) & 1u);
             }
-            if (a.prune && EDIT && node && e + 2u == ub0) {
+            if (EDIT && node && e + 2u == ub0) {
                 // A node expanded alone whose error children are chain nodes:
                 // keep only the children whose subtree outlives their own first
                 // step. A child does if its match chain leaves the run or the
@@ -1636,9 +1602,8 @@ void launchFMT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds
     }
 }
 
-// the compile-time shape matching a launch (SAHARA_TEXT_GENERIC=1: always the generic kernel)
+// the compile-time shape matching a launch (0: the generic kernel)
 int textShapeOf(const TextArgs& a) {
-    if (std::getenv("SAHARA_TEXT_GENERIC")) return 0;
     for (int shape = 1; shape <= 2; ++shape) {
         const TextShape t = textShape(shape);
         if (a.winBlocks == t.win && a.patBlocks == t.pat && (a.exactWindow != 0u) == t.exact) return shape;
@@ -1649,37 +1614,20 @@ int textShapeOf(const TextArgs& a) {
 template <int SIGMA, int SHAPE>
 void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     if (edit) {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, false, SHAPE>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, false, SHAPE>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, SHAPE>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, SHAPE>), grid, dim3(256), lds, st, a);
     } else {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, false, SHAPE>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, false, SHAPE>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, SHAPE>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, SHAPE>), grid, dim3(256), lds, st, a);
     }
 }
 
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
-    if (a.packedStack) {
-        if (edit) {
-            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, true>), grid, dim3(256), lds, st, a);
-            else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, true>), grid, dim3(256), lds, st, a);
-        } else {
-            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, true>), grid, dim3(256), lds, st, a);
-            else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, true>), grid, dim3(256), lds, st, a);
-        }
-    } else if (const int shape = textShapeOf(a); shape == 1) {
-        launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
-    } else if (shape == 2) {
-        launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
-    } else {
-        if (edit) {
-            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, false>), grid, dim3(256), lds, st, a);
-            else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, false>), grid, dim3(256), lds, st, a);
-        } else {
-            if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, false>), grid, dim3(256), lds, st, a);
-            else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, false>), grid, dim3(256), lds, st, a);
-        }
-    }
+    const int shape = textShapeOf(a);
+    if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
+    else if (shape == 2) launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
+    else launchTextShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
 }
 
 }  // namespace
@@ -1693,16 +1641,11 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     return b < 1 ? 1 : b;
 }
 
-int textBlocksPerCU(uint32_t sigma, bool edit, bool packedStack, size_t lds) {
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     int b = 0;
     const void* f;
-    if (packedStack) {
-        if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false, true> : (const void*)kSearchText<5, false, false, true>;
-        else            f = edit ? (const void*)kSearchText<6, true, false, true> : (const void*)kSearchText<6, false, false, true>;
-    } else {
-        if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false, false> : (const void*)kSearchText<5, false, false, false>;
-        else            f = edit ? (const void*)kSearchText<6, true, false, false> : (const void*)kSearchText<6, false, false, false>;
-    }
+    if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false> : (const void*)kSearchText<5, false, false>;
+    else            f = edit ? (const void*)kSearchText<6, true, false> : (const void*)kSearchText<6, false, false>;
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b;
 }
@@ -1724,12 +1667,6 @@ void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st) {
     if (sigma == 5) hipLaunchKernelGGL((kSeedItems<5>), dim3(blocks), dim3(256), 0, st, a);
     else            hipLaunchKernelGGL((kSeedItems<6>), dim3(blocks), dim3(256), 0, st, a);
-    SH_HIP(hipGetLastError());
-}
-
-void launchResolveTasks(uint4* tasks, const uint32_t* count, uint32_t cap, const uint32_t* sa, uint32_t blocks,
-                        hipStream_t st) {
-    hipLaunchKernelGGL(kResolveTasks, dim3(blocks), dim3(256), 0, st, tasks, count, cap, sa);
     SH_HIP(hipGetLastError());
 }
 
@@ -1928,36 +1865,6 @@ void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const 
     SH_HIP(hipGetLastError());
 }
 
-// Streamed queries sent two bits per symbol (capi.cpp pack2Avx2: symbol i at
-// bits 2 (i % 4) of byte i / 4) -> one rank per byte through a 4-entry table:
-// A C G T = 1 2 3 4 (dna4) or 1 2 3 5 (dna5, whose N positions kPatchRank
-// writes afterwards). 16 symbols per thread: one 4-B load, one 16-B store.
-__global__ void kUnpack2(const uint8_t* __restrict__ packed, uint8_t* __restrict__ dst, uint64_t n, uint32_t lut) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w * 16 < n; w += stride) {
-        if (w * 16 + 16 <= n) {
-            const uint32_t x = *reinterpret_cast<const uint32_t*>(packed + w * 4);
-            uint32_t o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t b = x >> (8 * q);  // four symbols
-                o[q] = ((lut >> (8 * (b & 3u))) & 0xFFu) | ((lut >> (8 * ((b >> 2) & 3u))) & 0xFFu) << 8 |
-                       ((lut >> (8 * ((b >> 4) & 3u))) & 0xFFu) << 16 | ((lut >> (8 * ((b >> 6) & 3u))) & 0xFFu) << 24;
-            }
-            *reinterpret_cast<uint4*>(dst + w * 16) = make_uint4(o[0], o[1], o[2], o[3]);
-        } else {
-            for (uint64_t i = w * 16; i < n; ++i) dst[i] = (lut >> (8 * ((packed[i >> 2] >> ((i & 3) * 2)) & 3u))) & 0xFFu;
-        }
-    }
-}
-
-void launchUnpack2(const uint8_t* packed, uint8_t* dst, uint64_t n, uint32_t sigma, hipStream_t st) {
-    const uint32_t lut = sigma == 6 ? 0x05030201u : 0x04030201u;
-    const uint64_t blocks = std::min<uint64_t>((n / 16 + 256) / 256, 65536);
-    hipLaunchKernelGGL(kUnpack2, dim3((unsigned)blocks), dim3(256), 0, st, packed, dst, n, lut);
-    SH_HIP(hipGetLastError());
-}
-
 // A streamed 2-bit chunk straight into the search's two pattern forms, with
 // no byte pass: 4-bit words (FM phase) and 3-bit-plane blocks (text phase)
 // of the patterns [p0, p1). Pattern p is row p, or (rc) read p / 2 and, for
@@ -2036,42 +1943,6 @@ void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uin
     const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 65536);
     hipLaunchKernelGGL(kPackFrom2, dim3((unsigned)blocks), dim3(256), 0, st, src, exc, nExc, r0, p0, p1, m,
                        rc ? 1u : 0u, sigma == 6 ? 1u : 0u, patWords, patBlocks, pats, pats3);
-    SH_HIP(hipGetLastError());
-}
-
-// dst[pos[i]] = rank for the listed positions (the N symbols of a 2-bit chunk)
-__global__ void kPatchRank(const uint32_t* __restrict__ pos, uint64_t n, uint8_t* __restrict__ dst, uint32_t rank) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        dst[pos[i]] = (uint8_t)rank;
-}
-
-void launchPatchRank(const uint32_t* pos, uint64_t n, uint8_t* dst, uint32_t rank, hipStream_t st) {
-    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(kPatchRank, dim3((unsigned)blocks), dim3(256), 0, st, pos, n, dst, rank);
-    SH_HIP(hipGetLastError());
-}
-
-// --max_hits' second round (capi.cpp searchExactFirst): the staged patterns
-// of the listed queries (ascending ids) into fresh buffers, both forms.
-__global__ void kGatherPatterns(const uint32_t* __restrict__ pats, const uint4* __restrict__ pats3,
-                                const uint64_t* __restrict__ idx, uint64_t n, uint32_t patWords, uint32_t patBlocks,
-                                uint32_t* __restrict__ opats, uint4* __restrict__ opats3) {
-    const uint32_t per = patWords + patBlocks;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * per; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t q = i / per;
-        const uint32_t k = (uint32_t)(i - q * per);
-        const uint64_t src = idx[q];
-        if (k < patWords) opats[q * patWords + k] = pats[src * patWords + k];
-        else opats3[q * patBlocks + (k - patWords)] = pats3[src * patBlocks + (k - patWords)];
-    }
-}
-
-void launchGatherPatterns(const uint32_t* pats, const uint4* pats3, const uint64_t* idx, uint64_t n, uint32_t patWords,
-                          uint32_t patBlocks, uint32_t* opats, uint4* opats3, hipStream_t st) {
-    if (n == 0) return;
-    const uint64_t blocks = std::min<uint64_t>((n * (patWords + patBlocks) + 255) / 256, 65536);
-    hipLaunchKernelGGL(kGatherPatterns, dim3((unsigned)blocks), dim3(256), 0, st, pats, pats3, idx, n, patWords,
-                       patBlocks, opats, opats3);
     SH_HIP(hipGetLastError());
 }
 

@@ -228,8 +228,8 @@ __attribute__((target("avx2"))) static uint64_t badRanksAvx2(const uint8_t* p, u
 // symbols of `in` -> (count + 3) / 4 bytes of `out`, symbol i at bits
 // 2 (i % 4) of byte i / 4, coded A C G T = 0 1 2 3. dna5's N (rank 4 of
 // sigma 6) is coded 0 and its position (`base` + i) appended to `exc`; the
-// device unpacks through a 4-entry table and patches the listed N positions
-// (kUnpack2, kPatchRank). Returns nonzero if any symbol is no rank in [1, sigma).
+// device turns the codes straight into both pattern forms and sets the listed
+// N positions (kPackFrom2). Returns nonzero if any symbol is no rank in [1, sigma).
 uint64_t pack2Scalar(const uint8_t* in, uint8_t* out, uint64_t count, uint32_t sigma, uint64_t base,
                             std::vector<uint32_t>& exc) {
     uint64_t bad = 0;
@@ -366,11 +366,11 @@ TaskPool& hostPool(Ctx* c) {
     // pool is rebuilt when it changes)
     unsigned cap = 16;
     if (const char* t = std::getenv("SAHARA_PACK_THREADS")) cap = (unsigned)std::max(1, std::min(64, std::atoi(t)));
-    // SAHARA_PACK_BIND: 1 the GPU's node, 2 the node holding the call's
-    // source rows (sampled pages), else unbound
+    // SAHARA_PACK_BIND=1: the GPU's node, else unbound (binding to the node
+    // that holds the call's reads measured slower inside the call: 539M
+    // against 592M reads/s, profiles/r03_pcie_compact_dma.txt)
     const char* e = std::getenv("SAHARA_PACK_BIND");
-    const int mode = e ? std::atoi(e) : 0;
-    const int node = mode == 1 ? c->place.node : mode == 2 ? c->srcNode : -1;
+    const int node = e && std::atoi(e) == 1 ? c->place.node : -1;
     if (!c->pool || c->poolCap != cap || c->poolNode != node) {
         drainPacking(c);
         c->pool.reset();
@@ -451,12 +451,11 @@ void drainPacking(Ctx* c) {
     for (auto& J : c->packJobs) J.group.wait();
 }
 
-// H2D copy of one chunk's staged bytes: on stE, or split into equal parts
-// over stE and c->upStreams - 1 more streams (their parts joined into stE, so
-// that the chunk's ringEv, recorded on stE, covers all of them)
+// H2D copy of one chunk's staged bytes on stE (SAHARA_TIMING=2: timed with
+// events; splitting a chunk over 2-4 streams measured no faster,
+// profiles/r03_pcie_upload_streams.txt)
 static void uploadCopy(Ctx* c, void* dst, const void* src, uint64_t bytes) {
-    const uint32_t ns = std::min<uint32_t>(c->upStreams, 1 + Ctx::kUpStreams);
-    if (c->traceOn) {  // SAHARA_TIMING=2: the DMA's own duration (printed with the marks)
+    if (c->traceOn) {  // the DMA's own duration (printed with the marks)
         if (c->dmaUsed == c->dmaEv.size()) {
             hipEvent_t a, b;
             SH_HIP(hipEventCreate(&a));
@@ -470,22 +469,7 @@ static void uploadCopy(Ctx* c, void* dst, const void* src, uint64_t bytes) {
         SH_HIP(hipEventRecord(d.second.second, c->stE));
         return;
     }
-    if (ns <= 1 || bytes < (16u << 10)) {
-        SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stE));
-        return;
-    }
-    const uint64_t part = ((bytes + ns - 1) / ns + 4095) & ~uint64_t(4095);
-    for (uint32_t i = 0; i < ns; ++i) {
-        const uint64_t lo = std::min<uint64_t>(bytes, i * part), hi = std::min<uint64_t>(bytes, lo + part);
-        if (hi <= lo) break;
-        hipStream_t s = i == 0 ? c->stE : c->stUp[i - 1];
-        SH_HIP(hipMemcpyAsync(static_cast<char*>(dst) + lo, static_cast<const char*>(src) + lo, hi - lo,
-                              hipMemcpyHostToDevice, s));
-        if (i > 0) {
-            SH_HIP(hipEventRecord(c->upPartEv[i - 1], s));
-            SH_HIP(hipStreamWaitEvent(c->stE, c->upPartEv[i - 1], 0));
-        }
-    }
+    SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stE));
 }
 
 // Enqueues the next chunk of the streamed upload (Ctx::Upload): packed on the
@@ -571,17 +555,13 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     if (bits == 4) launchUnpackNibbles(c->nibPats.ptr + b0, raw + s0, s1 - s0, kst);
     U.chunks[bits == 2 ? 0 : bits == 4 ? 1 : 2]++;
     const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
-    if (bits == 2) {  // straight into both pattern forms (no byte pass); SAHARA_UPLOAD_BYTES=1: via bytes
-        if (!std::getenv("SAHARA_UPLOAD_BYTES")) {
-            launchPackFrom2(c->nibPats.ptr + b0, reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff),
-                            (uint32_t)nExc, r0, p0, p1, m, U.rc, sigma, c->patWords, c->patBlocks,
-                            c->pats.ptr + 0, c->pats3.ptr + 0, kst);
-            U.done = r1;
-            c->mark("packed", r0 / U.chunk);
-            return;
-        }
-        launchUnpack2(c->nibPats.ptr + b0, raw + s0, s1 - s0, sigma, kst);
-        if (nExc) launchPatchRank(reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff), nExc, raw + s0, 4, kst);
+    if (bits == 2) {  // straight into both pattern forms (no byte pass)
+        launchPackFrom2(c->nibPats.ptr + b0, reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff),
+                        (uint32_t)nExc, r0, p0, p1, m, U.rc, sigma, c->patWords, c->patBlocks, c->pats.ptr + 0,
+                        c->pats3.ptr + 0, kst);
+        U.done = r1;
+        c->mark("packed", r0 / U.chunk);
+        return;
     }
     if (U.rc) launchInterleaveRC(c->readRaw.ptr, r0, r1, m, sigma, c->npat, c->rawPats.ptr, kst);
     if (p1 > p0) {
@@ -664,19 +644,10 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     Ctx::Upload& U = c->up;
     U = Ctx::Upload{};
     if (const char* e = std::getenv("SAHARA_PACK_AHEAD")) U.ahead = (uint32_t)std::max(0, std::atoi(e));
-    c->upStreams = 1;
     c->dmaUsed = 0;
-    if (const char* e = std::getenv("SAHARA_UPLOAD_STREAMS"))
-        c->upStreams = (uint32_t)std::max(1, std::min(1 + Ctx::kUpStreams, std::atoi(e)));
-    for (uint32_t i = 0; i + 1 < c->upStreams; ++i)
-        if (!c->stUp[i]) {
-            SH_HIP(hipStreamCreateWithFlags(&c->stUp[i], hipStreamNonBlocking));
-            SH_HIP(hipEventCreateWithFlags(&c->upPartEv[i], hipEventDisableTiming));
-        }
     U.src = src;
     U.rc = rc;
     U.rows = rows;
-    if (const char* e = std::getenv("SAHARA_PACK_BIND"); e && std::atoi(e) == 2) c->srcNode = nodeOfBuffer(src, rows * m);
     // symbols cross PCIe at 2 bits (DNA: A C G T codes, N positions listed),
     // 4 bits (any alphabet) or 8 (as given): SAHARA_UPLOAD_BITS, or
     // SAHARA_NIBBLE_UPLOAD=0 for 8
@@ -694,7 +665,7 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     if (U.bits != 8) chunk = std::min<uint64_t>(chunk, Ctx::kRingSlot * 2 / m);
     // chunk * m a multiple of 32 symbols: every chunk's region of the staging
     // buffers (s0 / 2 bytes at 2 or 4 bits, s0 at 8) then starts 16-B aligned
-    // for kPackFrom2's word loads and kUnpack2's 16-B stores (C5: m = 250)
+    // for kPackFrom2's word loads (C5: m = 250)
     uint64_t g = 32;
     while (m % g) g /= 2;
     const uint64_t step = std::max<uint64_t>(2, 32 / g);

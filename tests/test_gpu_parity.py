@@ -250,12 +250,9 @@ def test_decode_over_many_records(gpu_device, nrec):
         assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
 
 
-@pytest.mark.parametrize("wide", [False, True])
-def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch, wide):
+def test_text_phase_at_record_and_text_boundaries(gpu_device, monkeypatch):
     """Occurrences that touch position 0, the last symbol of the text and
-    record delimiters: the text-phase windows are clamped there. Both text
-    stack forms (one-word packed nodes, and the two-word form of m > 127)."""
-    monkeypatch.setenv("SAHARA_PACKED_STACK", "0" if wide else "1")
+    record delimiters: the text-phase windows are clamped there."""
     rng = np.random.default_rng(21)
     recs = random_records(rng, [60, 45, 200, 33, 90], 6)
     m = 24
@@ -319,16 +316,13 @@ def test_sort_decode_tile_holds_every_tier(gpu_device):
         assert np.array_equal(hits_as_rows(sa.search(gpu, pats2, sch)), want2), (verify, locate_sa)
 
 
-@pytest.mark.parametrize("batch,resolve", [("97", "2"), ("97", "1"), ("97", "0"), ("1000000", "2")])
-def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch, resolve):
+@pytest.mark.parametrize("batch", ["97", "1000000"])
+def test_segment_sort_and_multi_batch_pipeline(gpu_device, monkeypatch, batch):
     """Per-query segments of every length: reads from a 40-fold repeated unit
     have > 8 located rows (segmented radix sort), unique reads 1-2 (register
     sort), random reads none. SAHARA_BATCH=97 runs many batches through the
-    three-stream pipeline, with the per-query counters reused between them.
-    SAHARA_RESOLVE: text tasks' SA rows resolved inside the text kernel (2) or
-    by kResolveTasks on the FM stream (1) / the text stream (0)."""
+    three-stream pipeline, with the per-query counters reused between them."""
     monkeypatch.setenv("SAHARA_BATCH", batch)
-    monkeypatch.setenv("SAHARA_RESOLVE", resolve)
     recs, pats, sch, want = _repeat_case()
     per_q = np.bincount(want[:, 0].astype(np.int64), minlength=len(pats))
     assert per_q.max() > 8 and ((per_q >= 1) & (per_q <= 8)).any() and (per_q == 0).any()
@@ -510,15 +504,16 @@ def test_text_phase_work_stealing(gpu_device, monkeypatch, steal):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 2, 5])
-def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
+@pytest.mark.parametrize("n,batch", [(1, "257"), (2, "257"), (5, "257"), (3, "7")])
+def test_max_hits_on_the_device(gpu_device, monkeypatch, n, batch):
     """--max_hits n limited per batch on the device (search.hip limitBatch)
     equals the documented policy (include/sahara_hip.h, test_golden's
     limit_rows) over the oracle's hits: repeat-rich text (queries with many
     positions and several error counts), several batches, reads and
-    patterns calls, and besthits."""
+    patterns calls, and besthits. Batches of 7 patterns: 143 batches, past
+    the 64 whose per-batch host counters fit one page of pinned memory."""
     from test_golden import limit_rows
-    monkeypatch.setenv("SAHARA_BATCH", "257")
+    monkeypatch.setenv("SAHARA_BATCH", batch)
     rng = np.random.default_rng(40 + n)
     recs = random_records(rng, [25000, 8000], 6, repeats=True)
     reads = mutate_reads(rng, recs, 500, 50, 2, 6)
@@ -530,28 +525,19 @@ def test_max_hits_on_the_device(gpu_device, monkeypatch, n):
     gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
     assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme, max_hits=n)), want)
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
-    # two rounds: an exact round first, the full scheme on the rest
-    monkeypatch.setenv("SAHARA_MAXHITS_ROUNDS", "2")
-    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme, max_hits=n)), want)
-    monkeypatch.delenv("SAHARA_MAXHITS_ROUNDS")
     best = [sa.search_scheme("h2-k2", j, j, 50) for j in range(3)]
     bw = O.search_best(ref, pats, best, nthreads=8)
     assert np.array_equal(hits_as_rows(sa.search_best(gpu, pats, best, max_hits=n)), limit_rows(hits_as_rows(bw), n))
 
 
 @pytest.mark.parametrize("n", [1, 3, 40])
-def test_max_hits_exact_round_first(gpu_device, monkeypatch, n):
-    """--max_hits n with SAHARA_MAXHITS_ROUNDS=2 runs an exact round first and
-    the full scheme only on the queries with fewer than n exact positions
-    (capi.cpp searchExactFirst):
-    equal to the policy over the oracle's full hits, with queries of every
-    kind — exact repeats with hundreds of positions (leave after the exact
-    round), exact reads with a few positions, and reads with 1-2 errors (need
-    the full scheme) — over several batches, reads with and without reverse
+def test_max_hits_repeats_and_exact_reads(gpu_device, monkeypatch, n):
+    """--max_hits n equal to the policy over the oracle's full hits, with
+    queries of every kind — exact repeats with hundreds of positions, exact
+    reads with a few positions, and reads with 1-2 errors — over several batches, reads with and without reverse
     complements, and the patterns call."""
     from test_golden import limit_rows
     monkeypatch.setenv("SAHARA_BATCH", "173")
-    monkeypatch.setenv("SAHARA_MAXHITS_ROUNDS", "2")
     rng = np.random.default_rng(90 + n)
     unit = random_records(rng, [60], 6)[0]
     rep = np.tile(unit, 300)

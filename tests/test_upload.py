@@ -72,14 +72,10 @@ def _inputs(with_n, m=60, n_reads=2000):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bits", ["2", "2b", "4", "8"])
+@pytest.mark.parametrize("bits", ["2", "4", "8"])
 @pytest.mark.parametrize("with_n", [False, True])
 def test_streamed_upload_encodings(gpu_device, monkeypatch, bits, with_n):
-    """2 bits: straight into the pattern forms (kPackFrom2), or through bytes
-    (2b: SAHARA_UPLOAD_BYTES=1, kUnpack2 + kPatchRank); 4: nibbles; 8: bytes."""
-    if bits == "2b":
-        monkeypatch.setenv("SAHARA_UPLOAD_BYTES", "1")
-        bits = "2"
+    """2 bits: straight into the pattern forms (kPackFrom2); 4: nibbles; 8: bytes."""
     monkeypatch.setenv("SAHARA_UPLOAD_BITS", bits)
     monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "64")
     monkeypatch.setenv("SAHARA_BATCH", "997")
@@ -154,11 +150,6 @@ def test_2bit_pattern_forms_any_length(gpu_device, monkeypatch, m):
     monkeypatch.setenv("SAHARA_UPLOAD_BITS", "2")
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
     assert gpu.stats()["upload_chunks"][0] > 1
-    # the byte pass (kUnpack2's 16-B stores) over the same chunks: every
-    # chunk's region starts 16-B aligned whatever m (staging.cpp stageStreamed)
-    monkeypatch.setenv("SAHARA_UPLOAD_BYTES", "1")
-    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
-    monkeypatch.delenv("SAHARA_UPLOAD_BYTES")
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
     assert np.array_equal(want, hits_as_rows(ref.search(sa.interleave_rc(reads, 6), sch, nthreads=8)[0]))
