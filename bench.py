@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
 """bench.py — reads/s of sahara's search hot path on MI355X (BASELINE.json metric).
 
-A "step" is one pass of the hot path (search-scheme DFS + locate + canonical
-sort) over the whole batch of synthetic reads of the configured workload,
-with the reads (and their reverse complements, search.cpp:121-123) already
-resident in HBM. Default workload = BASELINE.json configs[2] (C3): k=2
-Levenshtein, 10M x 100 bp reads vs a 3 Gbp, 24-record synthetic reference
-(record lengths proportional to GRCh38 chromosomes), default
-generator h2-k2.
+A "step" is one call of the hot path at the drop-in boundary, SURVEY §8(d)'s
+search wall time: the workload's synthetic reads, in host memory in the form
+`sahara search`'s FASTA ingest produces (two bits per symbol, N positions
+listed: sahara_read_fasta form 2), go through sahara_gpu_search_packed_compact
+— upload, reverse-complement interleave (search.cpp:121-123), search-scheme
+DFS, locate, canonical sort — until every located hit is in host memory.
+`value` = reads / that time. The same pass with the reads already resident in
+HBM and the hits left there is reported as config.device_resident. Default
+workload = BASELINE.json configs[2] (C3): k=2 Levenshtein, 10M x 100 bp reads
+vs a 3 Gbp, 24-record synthetic reference (record lengths proportional to
+GRCh38 chromosomes), default generator h2-k2. The ingest that
+the timed region starts after (FASTA -> 2-bit) is timed beside it, with the
+rank form it replaces (config.ingest).
 
 Multi-GPU (torchrun, one process per GPU): every rank builds the full index
 on its own GPU (replicated, as SURVEY §8(e) prescribes), searches its own
@@ -97,7 +103,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented (untimed) counter run")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive (host buffers) pass")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the secondary PCIe-inclusive calls (rank reads, whole records, host patterns)")
+    ap.add_argument("--no-ingest", action="store_true", help="skip timing the FASTA ingest (both forms)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed RCCL gather of hit records")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the full-size checks (origin recall; GPU suffix array against the text)")
@@ -151,11 +159,14 @@ def main():
                                    substitutions=0 if edit else k, with_origin=True)
     pats = sa.interleave_rc(reads, sigma)
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
-    idx.stage(pats, scheme, edit=edit)
-    log(f"rank {rank}: {nreads} reads (+RC) simulated and staged in HBM ({time.time()-t:.1f}s), "
-        f"{scheme[0].shape[0]} searches")
+    # the reads as `sahara search`'s FASTA ingest hands them over: two bits per
+    # symbol, N positions listed (sahara_read_fasta form 2)
+    packed = sa.pack_reads(reads, sigma)
+    log(f"rank {rank}: {nreads} reads simulated and packed ({time.time()-t:.1f}s), {scheme[0].shape[0]} searches")
+    ingest = None
+    if not args.no_ingest and rank == 0:
+        ingest = time_ingest(sa, reads, packed, sigma)
     if args.execution == "reference":  # profiling aid: the timed steps are the reference's execution model
-        idx.set_mode(verify=False, locate_sa=False)
         args.no_count = args.no_ref_path = True
 
     def barrier():
@@ -163,28 +174,57 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for i in range(args.warmup):
-        t = time.time()
-        idx.run()
-        log(f"rank {rank}: warmup {i} {time.time()-t:.2f}s")
+    # ---- the headline: SURVEY §8(d)'s search wall time per call, host reads
+    # (packed) in, every located hit in host memory out
+    packed_call = lambda: sa.search_packed_compact(idx, packed, scheme, edit=edit)  # noqa: E731
+    step_stats = {"search_ms": 0.0, "text_ms": 0.0, "locate_ms": 0.0, "sort_ms": 0.0, "seed_ms": 0.0,
+                  "stage_ms": 0.0, "output_ms": 0.0, "search_launches": 0, "text_launches": 0}
+    h = None
+    if args.execution != "reference":
+        # two warmup calls whatever --warmup says: the first sizes the hit
+        # sink from its own result, the second pins it into the pool every
+        # later call draws from (capi.cpp allocPinned)
+        for i in range(max(2, args.warmup)):
+            t = time.time()
+            h = packed_call()
+            h.close()
+            log(f"rank {rank}: warmup {i} {time.time()-t:.3f}s")
+        h = None
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            if h is not None:
+                h.close()  # the previous call's records back to the pool (sahara_gpu_free_blocks)
+            h = packed_call()
+            st = idx.stats()
+            for kk in step_stats:
+                step_stats[kk] += st[kk]
+        barrier()
+        elapsed = time.perf_counter() - t0
+        n_packed = len(h)
+        packed_hits = h.to_hits()
+        h.close()
+        del h
 
+    # ---- the same pass device-resident: reads staged in HBM, hits left there
+    idx.stage(pats, scheme, edit=edit)
+    if args.execution == "reference":
+        idx.set_mode(verify=False, locate_sa=False)
+    for i in range(args.warmup):
+        idx.run()
     barrier()
     t0 = time.perf_counter()
-    search_ms = text_ms = locate_ms = sort_ms = seed_ms = 0.0
-    launches = text_launches = 0
+    dr_stats = {"search_ms": 0.0, "text_ms": 0.0, "search_launches": 0, "text_launches": 0}
     for i in range(args.steps):
         nh = idx.run()
         st = idx.stats()
-        search_ms += st["search_ms"]
-        text_ms += st["text_ms"]
-        locate_ms += st["locate_ms"]
-        sort_ms += st["sort_ms"]
-        seed_ms += st["seed_ms"]
-        launches += st["search_launches"]
-        text_launches += st["text_launches"]
+        for kk in dr_stats:
+            dr_stats[kk] += st[kk]
     barrier()
-    elapsed = time.perf_counter() - t0
+    dr_elapsed = time.perf_counter() - t0
     digest = idx.digest()
+    if args.execution == "reference":  # the timed steps are this mode's
+        elapsed, step_stats, n_packed, packed_hits = dr_elapsed, dr_stats, nh, None
 
     gather = None
     per_rank = None
@@ -192,13 +232,18 @@ def main():
         from sahara_amd.dist import max_over_ranks, sum_over_ranks, values_of_ranks
         per_rank = {"index_build_s": [round(v, 2) for v in values_of_ranks(build_s, device="cuda")],
                     "ms_per_step": [round(v * 1e3 / args.steps, 3) for v in values_of_ranks(elapsed, device="cuda")],
+                    "device_resident_ms_per_step": [round(v * 1e3 / args.steps, 3)
+                                                    for v in values_of_ranks(dr_elapsed, device="cuda")],
                     "hits": [int(v) for v in values_of_ranks(nh, device="cuda")]}
         elapsed = max_over_ranks(elapsed, device="cuda")  # RCCL over xGMI
+        dr_elapsed = max_over_ranks(dr_elapsed, device="cuda")
         total_hits = sum_over_ranks(nh, device="cuda")
         if not args.no_gather:
             gather = gather_step(idx, nh, nreads, world, rank, barrier, dist, torch)
     else:
         total_hits = nh
+    same_hits = n_packed == nh and (packed_hits is None or hits_digest(packed_hits) == digest)
+    del packed_hits
 
     # full-size checks that do not lean on the GPU's own index: every read is
     # found where it was sampled (all ranks), and rank 0 checks the whole GPU
@@ -216,6 +261,10 @@ def main():
 
     ms_per_step = elapsed * 1000.0 / args.steps
     reads_per_s = nreads * world * args.steps / elapsed
+    search_ms = step_stats["search_ms"]
+    text_ms = step_stats["text_ms"]
+    launches = step_stats["search_launches"]
+    text_launches = step_stats["text_launches"]
 
     # instrumented run (untimed): deterministic work counters -> algorithmic bytes
     cnt = ref_cnt = None
@@ -235,16 +284,18 @@ def main():
     extra = {}
     if cnt:
         # algorithmic bytes per step: FM = 64-B Occ lines touched
-        # + pattern bytes; text = per task its window, packed pattern, task
-        # record and SA entry; locate = one SA read per FM-located row
-        # (the FM kernel reads each pattern as 4-bit words: patWords u32 per
-        # pattern, capi staging, not one byte per symbol)
+        # + pattern bytes; text = per task its window, task record and SA
+        # entry, plus each pattern once; locate = one SA read per FM-located
+        # row (the FM kernel reads each pattern as 4-bit words: patWords u32
+        # per pattern, not one byte per symbol)
         search_bytes = 64.0 * cnt["ext_lines"] + pats.shape[0] * ((rlen + 7) // 8) * 4.0
-        # per text task: its window and pattern as 16-B blocks of 32 symbols
-        # (3 bit planes; capi.cpp winBlocks / patBlocks), the task record, the SA entry
+        # per text task: the source blocks of its window (16-B blocks of 32
+        # symbols, 3 bit planes: pass.cpp winBlocks, plus the block its
+        # funnel-shifted copy starts in), the task record, the SA entry; per
+        # pattern its blocks once (the tasks of one pattern share them in L2)
         win_blocks = (rlen + 2 * k + 62) // 32
         pat_blocks = (rlen + 31) // 32
-        text_bytes = cnt["conversions"] * (16.0 * (win_blocks + pat_blocks) + 16 + 4)
+        text_bytes = cnt["conversions"] * (16.0 * win_blocks + 16 + 4) + pats.shape[0] * 16.0 * pat_blocks
         locate_bytes = 4.0 * cnt["hits"]
         text_ms_step = text_ms / args.steps
         kern = {"kSearchFM": {"ms": round(search_ms_step, 2), "bytes": search_bytes,
@@ -319,8 +370,10 @@ def main():
                  "text_steps_per_read": round(cnt["text_steps"] / nreads, 1),
                  "cursors": cnt["cursors"], "hits_per_read": round(cnt["hits"] / nreads, 3),
                  "search_ms": round(search_ms_step, 2), "text_ms": round(text_ms / args.steps, 2),
-                 "locate_ms": round(locate_ms / args.steps, 2),
-                 "sort_ms": round(sort_ms / args.steps, 2), "seed_ms": round(seed_ms / args.steps, 2), "search_launches_per_step": launches // args.steps,
+                 "locate_ms": round(step_stats["locate_ms"] / args.steps, 2),
+                 "sort_ms": round(step_stats["sort_ms"] / args.steps, 2),
+                 "seed_ms": round(step_stats["seed_ms"] / args.steps, 2),
+                 "search_launches_per_step": launches // args.steps,
                  "text_launches_per_step": text_launches // args.steps,
                  "search_grid": cnt["search_grid"], "text_grid": cnt["text_grid"],
                  "pipelined": bool(cnt["pipelined"]),
@@ -330,10 +383,27 @@ def main():
                                          "same_hits": ref_cnt["hits"] == cnt["hits"]},
                  }
 
-    # PCIe-inclusive rate (not `value`): SURVEY §8(d)'s search wall time, host
-    # ranks in through located hits in host memory (sahara_gpu_search), timed
-    # like `value`: warmup calls, then --steps calls, each handing its hit
-    # buffer back before the next (sahara_gpu_free)
+    extra["timed_call"] = ("sahara_gpu_search_packed_compact from host reads two bits per symbol (N listed; the "
+                           "form sahara_read_fasta form 2 produces): each chunk copied into a pinned ring and "
+                           "uploaded, RC interleave and pattern packing on the device (kPackFrom2), search, locate, "
+                           "sort, each batch's hits as 8-B records (qid, text position, e; sahara_hit_blocks) copied "
+                           "into pinned host memory recycled through sahara_gpu_free_blocks")
+    extra["same_hits"] = bool(same_hits)
+    extra["device_resident"] = {
+        "reads_per_s": round(nreads * world * args.steps / dr_elapsed, 1),
+        "ms_per_step": round(dr_elapsed * 1e3 / args.steps, 2),
+        "text_ms": round(dr_stats["text_ms"] / args.steps, 2),
+        "text_launches_per_step": dr_stats["text_launches"] // args.steps,
+        "timed_over": "sahara_gpu_run: reads (+RC) staged in HBM before timing, hits left in HBM"}
+    extra["device_resident"]["timed_call_over_device_resident"] = round(
+        reads_per_s / extra["device_resident"]["reads_per_s"], 3)
+    if ingest:
+        extra["ingest"] = ingest
+    # other PCIe-inclusive calls (SURVEY §8(d)'s search wall time, as `value`):
+    # host reads one rank per byte (packed on the host's threads inside the
+    # call), whole 24-B records, host-interleaved patterns; timed like
+    # `value`: warmup calls, then --steps calls, each handing its hit buffer
+    # back before the next
     if not args.no_e2e:
         # two warmup calls whatever --warmup says: the first sizes the hit
         # buffer from its own result, the second pins it into the pool that
@@ -343,13 +413,11 @@ def main():
         # the hits come back as 8-B records (sahara_gpu_search_reads_compact:
         # what `sahara search` calls; single-part indexes)
         if idx.info()["n_parts"] == 1:
-            extra["pcie_inclusive"] = pcie_inclusive(
+            extra["pcie_inclusive_rank_reads"] = pcie_inclusive(
                 lambda: sa.search_reads_compact(idx, reads, scheme, edit=edit), idx, nreads, args.steps, w2, world,
                 barrier, nh, digest,
-                "sahara_gpu_search_reads_compact from host reads: streamed upload (four symbols per byte, N listed) + "
-                "device RC interleave, search, locate, sort, each batch's hits written by the device as 8-B records "
-                "(qid, text position, e; sahara_hit_blocks) into pinned host memory recycled through "
-                "sahara_gpu_free_blocks")
+                "sahara_gpu_search_reads_compact from host reads one rank per byte: packed to two bits per symbol "
+                "(N listed) on the host's threads inside the call, then as `value`")
         # the same with whole 24-B sahara_hit records (sahara_gpu_search_reads)
         extra["pcie_inclusive_full_records"] = pcie_inclusive(
             lambda: sa.search_reads(idx, reads, scheme, edit=edit), idx, nreads, args.steps, w2, world, barrier, nh,
@@ -407,6 +475,61 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def time_ingest(sa, reads, packed, sigma):
+    """The FASTA ingest that the timed region starts after, timed in both
+    forms on the same reads written as a FASTA file (80 columns, one header
+    per read, in /dev/shm when there is one): FASTA -> one rank per byte (the
+    reference's form, search.cpp:111-130) and FASTA -> two bits per symbol +
+    N list (what `sahara search` hands to sahara_gpu_search_packed_compact),
+    on the host threads the CLI uses. Checks that the 2-bit form equals the
+    timed call's input."""
+    import tempfile
+    d = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+    n, m = reads.shape
+    chars = np.frombuffer(b"$ACGNT" if sigma == 6 else b"$ACGT", np.uint8)
+    t = time.time()
+    # ">%09d" header lines, then the read in 80-column lines
+    head = np.empty((n, 11), np.uint8)
+    head[:, 0] = ord(">")
+    head[:, 10] = ord("\n")
+    ids = np.arange(n, dtype=np.int64)
+    for dgt in range(9):
+        head[:, 9 - dgt] = 48 + (ids // 10 ** dgt) % 10
+    lines = [(j, min(m, j + 80)) for j in range(0, m, 80)]
+    body = np.empty((n, m + len(lines)), np.uint8)
+    o = 0
+    for a, b in lines:
+        body[:, o:o + b - a] = chars[reads[:, a:b]]
+        body[:, o + b - a] = ord("\n")
+        o += b - a + 1
+    fd, path = tempfile.mkstemp(suffix=".fa", dir=d)
+    try:
+        with os.fdopen(fd, "wb") as f:
+            f.write(np.concatenate([head, body], axis=1).tobytes())
+        size = os.path.getsize(path)
+        write_s = time.time() - t
+        threads = host_threads()
+        out = {"fasta_bytes": size, "threads": threads, "file": "tmpfs" if d else "tmp"}
+        for form, name in ((1, "ranks"), (2, "two_bit")):
+            best = None
+            for _ in range(2):  # the second read is warm in the page cache
+                t = time.perf_counter()
+                r = sa.read_fasta(path, sigma, form=form, threads=threads)
+                dt = time.perf_counter() - t
+                best = dt if best is None else min(best, dt)
+            out[f"{name}_s"] = round(best, 3)
+            out[f"{name}_reads_per_s"] = round(n / best, 1)
+            if form == 2:
+                out["two_bit_equals_timed_input"] = bool(np.array_equal(r["data"], packed.codes) and
+                                                         np.array_equal(r["n_pos"], packed.n_pos))
+            del r
+        log(f"ingest: {size/1e9:.2f} GB FASTA (written in {write_s:.1f}s): ranks {out['ranks_s']}s, "
+            f"2-bit {out['two_bit_s']}s on {threads} threads")
+        return out
+    finally:
+        os.unlink(path)
 
 
 def gather_step(idx, nh, nreads, world, rank, barrier, dist, torch, device="cuda"):

@@ -184,6 +184,24 @@ int  sahara_gpu_search_reads_compact(void* ctx, const uint8_t* reads, uint64_t n
                                      uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
                                      uint32_t n_searches, int edit, sahara_hit_blocks* out);
 void sahara_gpu_free_blocks(sahara_hit_blocks* blocks);
+/* The same searches from reads already two bits per symbol — the form
+ * `sahara search`'s FASTA ingest produces (sahara_read_fasta form 2;
+ * sahara_pack_2bit's layout): stream symbol s is bits 2 (s % 4) of
+ * codes[s / 4], A C G T coded 0 1 2 3. Read i is the stream symbols
+ * [sym0 + i * len, sym0 + (i + 1) * len) (sym0: a shard of a larger stream
+ * may start inside a byte). dna5's N symbols are listed by stream position in
+ * n_pos, strictly ascending (entries outside the reads are ignored; their
+ * codes are ignored); a dna4 index takes none. The codes cross PCIe as given
+ * (a quarter of the rank bytes) and the host does no per-symbol work; hits,
+ * order, ownership and max_hits as sahara_gpu_search_reads[_compact]. */
+int  sahara_gpu_search_packed(void* ctx, const uint8_t* codes, uint64_t sym0, const uint64_t* n_pos,
+                              uint64_t n_count, uint64_t n_reads, uint32_t len, int reverse, uint64_t limit,
+                              const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,
+                              int edit, uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits);
+int  sahara_gpu_search_packed_compact(void* ctx, const uint8_t* codes, uint64_t sym0, const uint64_t* n_pos,
+                                      uint64_t n_count, uint64_t n_reads, uint32_t len, int reverse, uint64_t limit,
+                                      const uint32_t* pi, const uint32_t* l, const uint32_t* u,
+                                      uint32_t n_searches, int edit, sahara_hit_blocks* out);
 /* --search_mode besthits (search_ng21::search_best[_n], search.cpp:233-241):
  * n_schemes expanded schemes, scheme j covering exactly j errors, stored one
  * after another in pi/l/u (n_searches[j] rows of len entries each). A pattern's
@@ -251,6 +269,30 @@ int  sahara_scheme_parts(const char* generator, int min_k, int max_k, int* parts
 /* Node count / weighted node count of an expanded scheme (search.cpp:197-198). */
 int  sahara_scheme_counts(const uint32_t* l, const uint32_t* u, uint32_t n_searches, uint32_t len, int edit,
                           int sigma, double text_len, double* node_count, double* weighted_node_count);
+
+/* --- query ingest (replaces ivio::fasta::reader + ivs::convert_char_to_rank +
+ * ivs::verify_rank, search.cpp:111-130; index.cpp:53-72) --- */
+/* A FASTA file on `threads` host threads (0: OMP_NUM_THREADS, else all), in
+ * form 1 (one rank per byte of data, 255 = no rank of the alphabet) or form 2
+ * (two bits per symbol as sahara_gpu_search_packed takes them, N positions in
+ * n_pos). Records: symbols [offs[i], offs[i+1]). bad != 0: the first character
+ * that is no rank of the alphabet is character bad_pos of record bad_record
+ * (header bad_id), bad_char. Release with sahara_free_fasta. */
+typedef struct sahara_fasta {
+    uint8_t* data;
+    uint64_t n_symbols;
+    uint64_t* offs;
+    uint64_t n_records;
+    uint64_t* n_pos;
+    uint64_t n_count;
+    int bad;
+    uint32_t bad_char;
+    uint64_t bad_record;
+    uint64_t bad_pos;
+    char* bad_id;
+} sahara_fasta;
+int  sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threads, sahara_fasta* out);
+void sahara_free_fasta(sahara_fasta* f);
 
 /* --- synthetic inputs (host-side generators, BASELINE.md §2 / SURVEY §8(d)) --- */
 /* Uniform i.i.d. ACGT records (ranks 1,2,3 and 4 (dna4) / 5 (dna5) for T),

@@ -20,7 +20,9 @@ import os
 import numpy as np
 
 __all__ = [
-    "BiFMIndex", "HIT_DTYPE", "search", "search_reads", "search_reads_compact", "CompactHits", "search_scheme", "scheme_parts", "scheme_generators",
+    "BiFMIndex", "HIT_DTYPE", "search", "search_reads", "search_reads_compact", "CompactHits", "PackedReads",
+    "pack_reads", "search_packed", "search_packed_compact", "read_fasta", "search_scheme", "scheme_parts",
+    "scheme_generators",
     "scheme_counts", "synth_reference", "synth_reads", "interleave_rc", "load_fasta",
     "library_path", "lib", "SaharaError", "DNA5", "DNA4",
 ]
@@ -47,6 +49,13 @@ class HitBlocks(C.Structure):
     _fields_ = [("recs", C.POINTER(C.c_uint64)), ("n_hits", C.c_uint64), ("block_qid0", C.POINTER(C.c_uint64)),
                 ("block_end", C.POINTER(C.c_uint64)), ("n_blocks", C.c_uint64),
                 ("rec_starts", C.POINTER(C.c_uint64)), ("n_records", C.c_uint64)]
+
+
+class FastaOut(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("n_symbols", C.c_uint64), ("offs", C.POINTER(C.c_uint64)),
+                ("n_records", C.c_uint64), ("n_pos", C.POINTER(C.c_uint64)), ("n_count", C.c_uint64),
+                ("bad", C.c_int), ("bad_char", C.c_uint32), ("bad_record", C.c_uint64), ("bad_pos", C.c_uint64),
+                ("bad_id", C.c_char_p)]
 
 
 class IndexInfo(C.Structure):
@@ -100,6 +109,14 @@ EXPORTED = {
     "sahara_gpu_search_reads_compact": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, C.c_int, C.c_uint64,
                                                   u32p, u32p, u32p, C.c_uint32, C.c_int, C.POINTER(HitBlocks)]),
     "sahara_gpu_free_blocks": (None, [C.POINTER(HitBlocks)]),
+    "sahara_gpu_search_packed": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u64p, C.c_uint64, C.c_uint64, C.c_uint32,
+                                           C.c_int, C.c_uint64, u32p, u32p, u32p, C.c_uint32, C.c_int, C.c_uint32,
+                                           C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "sahara_gpu_search_packed_compact": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u64p, C.c_uint64, C.c_uint64,
+                                                   C.c_uint32, C.c_int, C.c_uint64, u32p, u32p, u32p, C.c_uint32,
+                                                   C.c_int, C.POINTER(HitBlocks)]),
+    "sahara_read_fasta": (C.c_int, [C.c_char_p, C.c_uint32, C.c_int, C.c_uint32, C.POINTER(FastaOut)]),
+    "sahara_free_fasta": (None, [C.POINTER(FastaOut)]),
     "sahara_gpu_search_best": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                          u32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_uint64)]),
@@ -462,6 +479,82 @@ def search_reads_compact(index, reads, scheme, edit=True, reverse=True, limit=0)
                                                  int(limit), _p(pi, u32p), _p(l, u32p), _p(u, u32p), pi.shape[0],
                                                  int(edit), C.byref(b)))
     return CompactHits(b, index)
+
+
+class PackedReads:
+    """Reads two bits per symbol, the form sahara_gpu_search_packed[_compact]
+    take and `sahara search`'s FASTA ingest produces (read_fasta(form=2)):
+    `codes` holds stream symbol s at bits 2 (s % 4) of byte s / 4 (A C G T =
+    0 1 2 3), read i is symbols [sym0 + i * length, sym0 + (i + 1) * length),
+    and `n_pos` lists the stream positions of N (dna5), ascending."""
+
+    def __init__(self, codes, n_reads, length, n_pos=None, sym0=0):
+        self.codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        self.n_reads, self.length, self.sym0 = int(n_reads), int(length), int(sym0)
+        self.n_pos = np.ascontiguousarray(n_pos if n_pos is not None else np.zeros(0), dtype=np.uint64)
+        if self.codes.size * 4 < self.sym0 + self.n_reads * self.length:
+            raise SaharaError("packed codes shorter than the reads they should hold")
+
+    def shard(self, r0, r1):
+        """Reads [r0, r1) over the same buffers (a shard of the stream)."""
+        return PackedReads(self.codes, r1 - r0, self.length, self.n_pos, self.sym0 + r0 * self.length)
+
+
+def pack_reads(reads, sigma=6):
+    """(n_reads, len) ranks -> PackedReads (the library's host packer,
+    sahara_pack_2bit; raises on a byte that is no rank of the alphabet)."""
+    r = np.ascontiguousarray(reads, dtype=np.uint8)
+    codes, pos, bad = pack_2bit(r, sigma)
+    if bad:
+        raise SaharaError("reads hold a byte that is no rank of the alphabet")
+    return PackedReads(codes, r.shape[0], r.shape[1], pos.astype(np.uint64))
+
+
+def _packed_args(packed, scheme):
+    pi, l, u = (np.ascontiguousarray(a, dtype=np.uint32) for a in scheme)
+    if packed.n_reads <= 0:
+        raise SaharaError("no reads")
+    return (_p(packed.codes, u8p), packed.sym0, _p(packed.n_pos, u64p) if packed.n_pos.size else None,
+            packed.n_pos.size, packed.n_reads, packed.length), (pi, l, u)
+
+
+def search_packed(index, packed, scheme, edit=True, reverse=True, limit=0, max_hits=0):
+    """search_reads from PackedReads (sahara_gpu_search_packed)."""
+    a, (pi, l, u) = _packed_args(packed, scheme)
+    out = C.c_void_p()
+    n = C.c_uint64()
+    _check(lib().sahara_gpu_search_packed(index._h, *a, int(reverse), int(limit), _p(pi, u32p), _p(l, u32p),
+                                          _p(u, u32p), pi.shape[0], int(edit), max_hits, C.byref(out), C.byref(n)))
+    return _hits_array(out, n.value)
+
+
+def search_packed_compact(index, packed, scheme, edit=True, reverse=True, limit=0):
+    """search_reads_compact from PackedReads (sahara_gpu_search_packed_compact):
+    `sahara search`'s call at the drop-in boundary."""
+    a, (pi, l, u) = _packed_args(packed, scheme)
+    b = HitBlocks()
+    _check(lib().sahara_gpu_search_packed_compact(index._h, *a, int(reverse), int(limit), _p(pi, u32p), _p(l, u32p),
+                                                  _p(u, u32p), pi.shape[0], int(edit), C.byref(b)))
+    return CompactHits(b, index)
+
+
+def read_fasta(path, sigma=6, form=1, threads=0):
+    """The library's FASTA ingest (sahara_read_fasta; search.cpp:111-130):
+    dict with `data` (form 1: one rank per symbol, 255 = invalid; form 2: two
+    bits per symbol), `offs` (record i = symbols [offs[i], offs[i+1])),
+    `n_pos` (form 2: N positions) and `bad` (None, or (record, position,
+    character, header) of the first invalid character)."""
+    f = FastaOut()
+    _check(lib().sahara_read_fasta(os.fsencode(path), sigma, form, threads, C.byref(f)))
+    try:
+        nb = f.n_symbols if form == 1 else (f.n_symbols + 3) // 4
+        data = np.ctypeslib.as_array(f.data, shape=(nb,)).copy() if nb else np.zeros(0, np.uint8)
+        offs = np.ctypeslib.as_array(f.offs, shape=(f.n_records + 1,)).copy() if f.n_records else np.zeros(0, np.uint64)
+        npos = np.ctypeslib.as_array(f.n_pos, shape=(f.n_count,)).copy() if f.n_count else np.zeros(0, np.uint64)
+        bad = (int(f.bad_record), int(f.bad_pos), chr(f.bad_char), f.bad_id.decode()) if f.bad else None
+        return {"data": data, "offs": offs, "n_pos": npos, "n_symbols": int(f.n_symbols), "bad": bad}
+    finally:
+        lib().sahara_free_fasta(C.byref(f))
 
 
 def search_best(index, queries, schemes, max_hits=0):

@@ -29,10 +29,11 @@
 #include <vector>
 
 #include "../../include/sahara_hip.h"
-#include "fasta.h"
+#include "../csrc/fasta.h"
 #include "shard.h"
 
 using namespace sahara_cli;
+using namespace sahara_io;
 
 namespace sahara_cli {
 struct ReadSimulatorArgs {
@@ -371,12 +372,16 @@ int cmdSearch(int argc, char** argv) {
     std::vector<std::tuple<std::string, double>> timing;
     StopWatch sw;
 
-    // queries (search.cpp:111-130): ranks and verification on the host (parallel
-    // whole-file ingest); the reverse-complement interleave and --limit_queries
-    // cut happen on the device (sahara_gpu_search_reads), so only the reads
-    // cross PCIe. Query numbers in messages count the interleaved list.
+    // queries (search.cpp:111-130): parsed and verified on the host (parallel
+    // whole-file ingest) straight into two bits per symbol with the N
+    // positions listed (besthits: one rank per byte); the reverse-complement
+    // interleave and --limit_queries cut happen on the device
+    // (sahara_gpu_search_packed[_compact]), so only the packed reads cross
+    // PCIe. Query numbers in messages count the interleaved list.
     const unsigned nt = hostThreads();
-    FastaData Q = parseFastaParallel(query.value, (uint32_t)sigma, nt);
+    const bool packedIn = !besthits;
+    FastaData Q = parseFastaParallel(query.value, (uint32_t)sigma, nt, 8u << 20,
+                                     packedIn ? FastaForm::kCodes2 : FastaForm::kRanks);
     const size_t nrec = Q.records();
     const size_t per = noRev.given ? 1 : 2;  // patterns per read
     if (Q.bad) {
@@ -458,7 +463,7 @@ int cmdSearch(int argc, char** argv) {
             throw CliError(fmtStr("query %zu has length %zu, but all queries must have the length of the first "
                                   "(%u): sahara expands one search scheme for queries[0].size()",
                                   per * r, (size_t)(Q.offs[r + 1] - Q.offs[r]), len));
-    const uint8_t* reads = Q.ranks.data();  // nreads x len, back to back
+    const uint8_t* reads = Q.ranks.data();  // nreads x len, back to back (packedIn: 2-bit codes)
 
     std::vector<Scheme> schemes;  // all: [0..k]; besthits: one per exact error count j
     // --dynamic_generator: part sizes by weighted node count (search.cpp:192-195, 202-205)
@@ -526,18 +531,20 @@ int cmdSearch(int argc, char** argv) {
                 int rc;
                 const uint32_t cap = (uint32_t)std::max(0L, mh);
                 HitPart part;
+                // the shard's reads: stream symbols [r0 * len, r1 * len) of the packed codes
+                const uint64_t* npos = Q.nPos.empty() ? nullptr : Q.nPos.data();
                 if (!besthits && compactOut) {  // 8-B records straight into host memory, decoded by writeHits
                     const Scheme& s = schemes[0];
-                    rc = sahara_gpu_search_reads_compact(ctx[g], reads + r0 * len, r1 - r0, len, noRev.given ? 0 : 1,
-                                                         q1 - q0, s.pi.data(), s.l.data(), s.u.data(), s.n,
-                                                         edit ? 1 : 0, &part.blocks);
+                    rc = sahara_gpu_search_packed_compact(ctx[g], reads, (uint64_t)r0 * len, npos, Q.nPos.size(),
+                                                          r1 - r0, len, noRev.given ? 0 : 1, q1 - q0, s.pi.data(),
+                                                          s.l.data(), s.u.data(), s.n, edit ? 1 : 0, &part.blocks);
                     part.compact = rc == 0;
                     nh = part.blocks.n_hits;
                 } else if (!besthits) {
                     const Scheme& s = schemes[0];
-                    rc = sahara_gpu_search_reads(ctx[g], reads + r0 * len, r1 - r0, len, noRev.given ? 0 : 1, q1 - q0,
-                                                 s.pi.data(), s.l.data(), s.u.data(), s.n, edit ? 1 : 0, cap, &hits,
-                                                 &nh);
+                    rc = sahara_gpu_search_packed(ctx[g], reads, (uint64_t)r0 * len, npos, Q.nPos.size(), r1 - r0, len,
+                                                  noRev.given ? 0 : 1, q1 - q0, s.pi.data(), s.l.data(), s.u.data(),
+                                                  s.n, edit ? 1 : 0, cap, &hits, &nh);
                 } else {  // search_best takes the interleaved patterns
                     std::vector<uint8_t> pats((q1 - q0) * len);
                     for (size_t q = q0; q < q1; ++q) {

@@ -23,9 +23,10 @@
 #include <tuple>
 #include <vector>
 
-#include "fasta.h"
+#include "../csrc/fasta.h"
 
 namespace sahara_cli {
+using namespace sahara_io;
 namespace {
 
 std::mt19937_64 g_transcriptEngine;  // the reference's global `generator` (read_simulator.cpp:114)

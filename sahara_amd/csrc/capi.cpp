@@ -640,7 +640,8 @@ static void printDmaTimes(Ctx* c) {
 // to the caller (search.cpp:218-250 from host queries to host hits).
 static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t len,
                            const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit,
-                           uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits) {
+                           uint32_t max_hits, sahara_hit** hits, uint64_t* n_hits,
+                           const PackedReads* packed = nullptr) {
     using clk = std::chrono::steady_clock;
     const auto tA = clk::now();
     {
@@ -649,7 +650,7 @@ static void searchStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, u
         c->traceT0 = tA;
         c->trace.clear();
     }
-    stageStreamed(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit);
+    stageStreamed(c, src, rows, rc, npat, len, pi, l, u, n_searches, edit, packed);
     const auto tB = clk::now();
     c->sink = nullptr;
     c->sinkCap = 0;
@@ -807,7 +808,8 @@ int sahara_gpu_search_reads(void* ctx, const uint8_t* reads, uint64_t n_reads, u
 // finish), handed over as blocks (one per batch).
 static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, uint32_t len, int reverse,
                                uint64_t limit, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
-                               uint32_t n_searches, int edit, sahara_hit_blocks* out) {
+                               uint32_t n_searches, int edit, sahara_hit_blocks* out,
+                               const PackedReads* packed = nullptr) {
     using clk = std::chrono::steady_clock;
     const auto tA = clk::now();
     if (c->I.sigma != 5 && c->I.sigma != 6) throw Error("reverse complements need a dna4 or dna5 index");
@@ -824,7 +826,7 @@ static void searchReadsCompact(Ctx* c, const uint8_t* reads, uint64_t n_reads, u
     }
     for (uint64_t i = 0; i < (uint64_t)n_searches * len; ++i)  // before staging: a refused call stages nothing
         if (u[i] > 15) throw Error("compact hit records hold at most 15 errors");
-    stageStreamed(c, reads, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit);
+    stageStreamed(c, reads, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit, packed);
     c->sink = nullptr;
     c->compactSink = c->sinkPinned = false;
     // the sink, sized from the last call (else 2 hits per pattern), always
@@ -933,6 +935,36 @@ int sahara_gpu_search_reads_compact(void* ctx, const uint8_t* reads, uint64_t n_
         if (!out) throw Error("sahara_gpu_search_reads_compact: null output");
         *out = sahara_hit_blocks{};
         searchReadsCompact(ctxOf(ctx), reads, n_reads, len, reverse, limit, pi, l, u, n_searches, edit, out);
+    });
+}
+
+int sahara_gpu_search_packed(void* ctx, const uint8_t* codes, uint64_t sym0, const uint64_t* n_pos, uint64_t n_count,
+                             uint64_t n_reads, uint32_t len, int reverse, uint64_t limit, const uint32_t* pi,
+                             const uint32_t* l, const uint32_t* u, uint32_t n_searches, int edit, uint32_t max_hits,
+                             sahara_hit** hits, uint64_t* n_hits) {
+    return guarded([&] {
+        Ctx* c = ctxOf(ctx);
+        if (!codes || (n_count && !n_pos)) throw Error("sahara_gpu_search_packed: null input");
+        uint64_t npat = reverse ? 2 * n_reads : n_reads;
+        if (limit && limit < npat) npat = limit;  // --limit_queries cuts the interleaved list (search.cpp:125-127)
+        if (npat == 0) throw Error("no patterns");
+        const uint64_t rows = reverse ? (npat + 1) / 2 : npat;
+        const PackedReads pk{sym0, n_pos, n_count};
+        searchStreamed(c, codes, rows, reverse != 0, npat, len, pi, l, u, n_searches, edit, max_hits, hits, n_hits,
+                       &pk);
+    });
+}
+
+int sahara_gpu_search_packed_compact(void* ctx, const uint8_t* codes, uint64_t sym0, const uint64_t* n_pos,
+                                     uint64_t n_count, uint64_t n_reads, uint32_t len, int reverse, uint64_t limit,
+                                     const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t n_searches,
+                                     int edit, sahara_hit_blocks* out) {
+    return guarded([&] {
+        if (!out) throw Error("sahara_gpu_search_packed_compact: null output");
+        *out = sahara_hit_blocks{};
+        if (!codes || (n_count && !n_pos)) throw Error("sahara_gpu_search_packed_compact: null input");
+        const PackedReads pk{sym0, n_pos, n_count};
+        searchReadsCompact(ctxOf(ctx), codes, n_reads, len, reverse, limit, pi, l, u, n_searches, edit, out, &pk);
     });
 }
 

@@ -397,7 +397,7 @@ struct Ctx {
     // the host waits for it before packing into the slot again. The ring is
     // pinned once per context, in the background while the index loads.
     struct Upload {
-        const uint8_t* src = nullptr;  // host symbols: the patterns, or the reads (rc)
+        const uint8_t* src = nullptr;  // host symbols: the patterns, or the reads (rc); prepacked: 2-bit codes
         bool rc = false;               // reads: reverse complements interleaved on the device
         uint32_t bits = 4;             // 2: ACGT codes + N list, 4: nibbles, 8: bytes as given
         uint64_t rows = 0;             // source rows
@@ -408,7 +408,16 @@ struct Ctx {
         bool bad = false;              // a chunk held a byte that is no rank of this index
         double hostMs = 0;             // host time spent packing and enqueueing
         uint64_t chunks[3] = {0, 0, 0};  // chunks sent at 2 / 4 / 8 bits per symbol
+        // reads that arrive two bits per symbol (sahara_gpu_search_packed):
+        // chunks are copied into the ring, not packed; source symbol s of
+        // the call is stream symbol sym0 + s; the N positions of the call's
+        // reads are on the device (nList, relative to each chunk's first
+        // whole byte), chunk j's from entry nFirst[j]
+        bool prepacked = false;
+        uint64_t sym0 = 0;
+        std::vector<uint64_t> nFirst;
     } up;
+    DevBuf<uint32_t> nList;
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
     // SAHARA_TIMING=2: timing events around each chunk's DMA (bytes, events)
@@ -561,8 +570,15 @@ void uploadChunk(Ctx* c, hipStream_t kst);
 void ensureUploaded(Ctx* c, uint64_t patEnd, hipStream_t kst);
 void stageScheme(Ctx* c, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l, const uint32_t* u,
                  uint32_t ns, int edit);
+// reads given two bits per symbol (sahara_gpu_search_packed[_compact])
+struct PackedReads {
+    uint64_t sym0;          // stream position of the first read's first symbol
+    const uint64_t* nPos;   // stream positions of N, ascending (any outside the reads are ignored)
+    uint64_t nCount;
+};
 void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t m,
-                   const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit);
+                   const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit,
+                   const PackedReads* packed = nullptr);
 void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32_t* pi, const uint32_t* l,
            const uint32_t* u, uint32_t ns, int edit);
 

@@ -1,4 +1,5 @@
-// fasta.h — FASTA reading and rank conversion for the `sahara` CLI.
+// fasta.h — FASTA reading and rank conversion: the library's query ingest
+// (sahara_read_fasta) and the `sahara` CLI's reference reader.
 //
 // Restates what the reference takes from ivio / ivsigma on this path:
 //   ivio::fasta::reader            (search.cpp:115, index.cpp:53)
@@ -25,7 +26,7 @@
 #include <utility>
 #include <vector>
 
-namespace sahara_cli {
+namespace sahara_io {
 
 struct Record {
     std::string id;
@@ -128,11 +129,21 @@ inline std::vector<uint8_t> toRanks(const std::string& s, uint32_t sigma) {
 // The file is mapped and cut into pieces of ~8 MB that start at line starts.
 // A line starting with '>' is a header (a new record), any other line is
 // sequence. Pass 1 counts each piece's sequence characters and notes where
-// its records start; pass 2 converts them into one flat rank array
-// (255 = no rank of the alphabet) at the prefix-summed offsets.
+// its records start; pass 2 converts them at the prefix-summed offsets into
+// one flat array, in one of two forms:
+//   kRanks: one rank per byte (255 = no rank of the alphabet);
+//   kCodes2: two bits per symbol, symbol s at bits 2 (s % 4) of byte s / 4,
+//            A C G T coded 0 1 2 3, and the positions of dna5's N listed in
+//            ascending order (their code is 0) — the packed reads that
+//            sahara_gpu_search_packed[_compact] take, written without an
+//            intermediate rank array (a quarter of the bytes).
+enum class FastaForm { kRanks = 1, kCodes2 = 2 };
+
 struct FastaData {
-    std::vector<uint64_t> offs;     // record i's ranks = ranks[offs[i], offs[i+1])
-    std::vector<uint8_t> ranks;
+    std::vector<uint64_t> offs;     // record i = symbols [offs[i], offs[i+1])
+    std::vector<uint8_t> ranks;     // kRanks: one per symbol; kCodes2: (symbols + 3) / 4 bytes
+    std::vector<uint64_t> nPos;     // kCodes2: symbols that are N (dna5), ascending
+    uint64_t symbols = 0;
     // the first byte that is no rank of the alphabet, if any
     bool bad = false;
     size_t badRecord = 0;
@@ -164,7 +175,7 @@ inline unsigned hostThreads() {
 }
 
 inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, unsigned nt,
-                                    size_t kPiece = 8u << 20) {
+                                    size_t kPiece = 8u << 20, FastaForm form = FastaForm::kRanks) {
     const int fd = ::open(path.c_str(), O_RDONLY);
     if (fd < 0) throw std::runtime_error("can not open file " + path);
     struct stat sb {};
@@ -206,6 +217,8 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
         std::vector<std::pair<uint64_t, uint64_t>> heads;    // (header position, sequence characters before it)
         uint64_t badAt = UINT64_MAX;                         // first invalid rank (piece-local sequence index)
         unsigned char badChar = 0;
+        std::vector<uint64_t> nPos;                          // kCodes2: its N symbols (global positions)
+        uint8_t head = 0, tail = 0;                          // kCodes2: its bits of the bytes it shares
     };
     std::vector<Piece> pc(P);
     // a line's sequence bytes end before its '\n', and before a '\r' right
@@ -246,31 +259,93 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
         }
     if (heads.empty()) return D;
     D.offs.push_back(base[P]);
+    D.symbols = base[P];
     // pass 2: convert
-    D.ranks.resize(base[P]);
     uint8_t table[256];
     for (int c = 0; c < 256; ++c) table[c] = charToRank((char)c, sigma);
+    const bool codes = form == FastaForm::kCodes2;
+    if (!codes) {
+        D.ranks.resize(base[P]);
+    } else {
+        D.ranks.assign((base[P] + 3) / 4, 0);
+    }
+    // rank -> 2-bit code (A C G T = 0 1 2 3; N = 0, listed)
+    uint8_t code2[256];
+    for (int r = 0; r < 256; ++r) code2[r] = 0;
+    code2[1] = 0; code2[2] = 1; code2[3] = 2; code2[sigma == 6 ? 5 : 4] = 3;
+    const uint8_t rankN = sigma == 6 ? 4 : 0;  // (the table never gives 0)
     parallelFor(nt, P, [&](size_t i) {
         Piece& c = pc[i];
-        uint8_t* const o0 = D.ranks.data() + base[i];
-        uint8_t* o = o0;
+        if (!codes) {
+            uint8_t* const o0 = D.ranks.data() + base[i];
+            uint8_t* o = o0;
+            for (size_t p = bound[i], e = bound[i + 1]; p < e;) {
+                const void* nl = std::memchr(b + p, '\n', e - p);
+                const size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : e;
+                if (b[p] != '>') {
+                    for (size_t q = p, qe = lineEnd(p, eol, nl != nullptr); q < qe; ++q) {
+                        const unsigned char ch = (unsigned char)b[q];
+                        const uint8_t v = table[ch];
+                        if (v >= sigma && c.badAt == UINT64_MAX) {
+                            c.badAt = (uint64_t)(o - o0);
+                            c.badChar = ch;
+                        }
+                        *o++ = v;
+                    }
+                }
+                p = eol + 1;
+            }
+            return;
+        }
+        // two bits per symbol: whole bytes inside the piece are stored, the
+        // partial first and last bytes (shared with the neighbours) kept in
+        // head / tail and or-ed in afterwards
+        uint8_t* const out = D.ranks.data();
+        const uint64_t g0 = base[i];
+        uint64_t g = g0;
+        uint32_t acc = 0;
+        auto flush = [&](uint64_t byteIdx, uint8_t v) {
+            if (byteIdx == g0 / 4 && (g0 & 3u)) c.head = v;
+            else out[byteIdx] = v;
+        };
         for (size_t p = bound[i], e = bound[i + 1]; p < e;) {
             const void* nl = std::memchr(b + p, '\n', e - p);
             const size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : e;
             if (b[p] != '>') {
-                for (size_t q = p, qe = lineEnd(p, eol, nl != nullptr); q < qe; ++q) {
+                for (size_t q = p, qe = lineEnd(p, eol, nl != nullptr); q < qe; ++q, ++g) {
                     const unsigned char ch = (unsigned char)b[q];
                     const uint8_t v = table[ch];
                     if (v >= sigma && c.badAt == UINT64_MAX) {
-                        c.badAt = (uint64_t)(o - o0);
+                        c.badAt = g - g0;
                         c.badChar = ch;
                     }
-                    *o++ = v;
+                    if (v == rankN) c.nPos.push_back(g);
+                    acc |= (uint32_t)code2[v] << (2u * (uint32_t)(g & 3u));
+                    if ((g & 3u) == 3u) {
+                        flush(g / 4, (uint8_t)acc);
+                        acc = 0;
+                    }
                 }
             }
             p = eol + 1;
         }
+        if (g & 3u) {  // a partial last byte
+            if (g / 4 == g0 / 4 && (g0 & 3u)) c.head |= (uint8_t)acc;  // the piece lies inside one byte
+            else c.tail = (uint8_t)acc;
+        }
     });
+    if (codes) {
+        uint64_t nN = 0;
+        for (size_t i = 0; i < P; ++i) {
+            const uint64_t g0 = base[i], g1 = base[i + 1];
+            if (g1 == g0) continue;
+            if (g0 & 3u) D.ranks[g0 / 4] |= pc[i].head;
+            if ((g1 & 3u) && !(g1 / 4 == g0 / 4 && (g0 & 3u))) D.ranks[g1 / 4] |= pc[i].tail;
+            nN += pc[i].nPos.size();
+        }
+        D.nPos.reserve(nN);
+        for (size_t i = 0; i < P; ++i) D.nPos.insert(D.nPos.end(), pc[i].nPos.begin(), pc[i].nPos.end());
+    }
     for (size_t i = 0; i < P; ++i)
         if (pc[i].badAt != UINT64_MAX) {
             const uint64_t at = base[i] + pc[i].badAt;
@@ -306,4 +381,4 @@ inline std::vector<uint8_t> reverseComplement(const std::vector<uint8_t>& r, uin
     return o;
 }
 
-}  // namespace sahara_cli
+}  // namespace sahara_io

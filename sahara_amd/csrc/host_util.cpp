@@ -1,10 +1,14 @@
-// host_util.cpp — .idx I/O and the synthetic read generator (host side).
+// host_util.cpp — .idx I/O, the synthetic read generator and the FASTA
+// query ingest (host side).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <thread>
 
+#include "../../include/sahara_hip.h"
 #include "device_index.h"
+#include "fasta.h"
 #include "idx_format.h"
 
 namespace sahara {
@@ -246,3 +250,64 @@ void synthReads(const uint8_t* ranks, const uint64_t* recLens, uint64_t nrec, ui
 }
 
 }  // namespace sahara
+
+namespace sahara {
+extern thread_local std::string g_err;  // sahara_gpu_last_error (capi.cpp)
+}
+
+// ------------------------------------------------------------ FASTA ingest --
+// sahara_read_fasta: search.cpp:111-130's query ingest (ivio::fasta::reader,
+// ivs::convert_char_to_rank, ivs::verify_rank) on the host's threads, in one
+// of the two forms the search calls take (fasta.h parseFastaParallel).
+namespace {
+template <typename T>
+T* copyOut(const std::vector<T>& v) {
+    T* p = static_cast<T*>(std::malloc(std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!p) throw sahara::Error("out of host memory for FASTA data");
+    if (!v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
+    return p;
+}
+}  // namespace
+
+extern "C" {
+
+int sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threads, sahara_fasta* out) {
+    try {
+        if (!out || !path) throw sahara::Error("sahara_read_fasta: null argument");
+        *out = sahara_fasta{};
+        if (sigma != 5 && sigma != 6) throw sahara::Error("sigma must be 5 or 6");
+        if (form != 1 && form != 2) throw sahara::Error("form must be 1 (ranks) or 2 (two bits per symbol)");
+        const unsigned nt = threads ? threads : sahara_io::hostThreads();
+        sahara_io::FastaData D = sahara_io::parseFastaParallel(
+            path, sigma, nt, 8u << 20, form == 2 ? sahara_io::FastaForm::kCodes2 : sahara_io::FastaForm::kRanks);
+        out->data = copyOut(D.ranks);
+        out->offs = copyOut(D.offs);
+        out->n_pos = copyOut(D.nPos);
+        out->n_symbols = D.symbols;
+        out->n_records = D.records();
+        out->n_count = D.nPos.size();
+        out->bad = D.bad ? 1 : 0;
+        out->bad_record = D.badRecord;
+        out->bad_pos = D.badPos;
+        out->bad_char = D.badChar;
+        std::vector<char> id(D.badId.begin(), D.badId.end());
+        id.push_back(0);
+        out->bad_id = copyOut(id);
+        return 0;
+    } catch (const std::exception& e) {
+        if (out) sahara_free_fasta(out);
+        sahara::g_err = e.what();
+    }
+    return -1;
+}
+
+void sahara_free_fasta(sahara_fasta* f) {
+    if (!f) return;
+    std::free(f->data);
+    std::free(f->offs);
+    std::free(f->n_pos);
+    std::free(f->bad_id);
+    *f = sahara_fasta{};
+}
+
+}  // extern "C"

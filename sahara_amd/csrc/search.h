@@ -137,9 +137,11 @@ void sortHitsByQid(const sahara_hit* in, uint64_t n, uint64_t nqid, sahara_hit* 
                    hipStream_t st);
 void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const uint64_t* starts, uint64_t* out,
                        hipStream_t st, uint32_t maxBlocks = 8192);
-void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,
-                     uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks, uint32_t* pats,
-                     uint4* pats3, hipStream_t st);
+// a streamed chunk of 2-bit codes (read r0's first symbol at symbol `so` of
+// src, 0..3) straight into both pattern forms of the patterns [p0, p1)
+void launchPackFrom2(const uint8_t* src, uint32_t so, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0,
+                     uint64_t p1, uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks,
+                     uint32_t* pats, uint4* pats3, hipStream_t st);
 // reads [r0, r1) (m bytes each) -> patterns [2 r0, min(2 r1, pEnd)): read, reverse complement, ...
 void launchInterleaveRC(const uint8_t* reads, uint64_t r0, uint64_t r1, uint32_t m, uint32_t sigma, uint64_t pEnd,
                         uint8_t* pats, hipStream_t st);

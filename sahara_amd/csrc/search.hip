@@ -1869,7 +1869,8 @@ void launchCompactHits(const sahara_hit* h, uint64_t n, uint64_t qidBase, const 
 // no byte pass: 4-bit words (FM phase) and 3-bit-plane blocks (text phase)
 // of the patterns [p0, p1). Pattern p is row p, or (rc) read p / 2 and, for
 // odd p, its reverse complement (search.cpp:121-123: reversed, codes
-// complemented as c ^ 3); read r starts at chunk-local symbol (r - r0) * m.
+// complemented as c ^ 3); read r starts at chunk-local symbol so + (r - r0) * m
+// (so < 4: reads given packed start anywhere in a byte).
 // `exc` lists the chunk's N positions in ascending order (rank 4). One thread
 // per (pattern, 32-symbol block): 64 bits of codes from three word loads,
 // even / odd bits gathered into the code planes c0 / c1, then
@@ -1889,8 +1890,8 @@ __device__ __forceinline__ uint32_t spreadNibbles(uint32_t x) {  // bit j of 8 -
     x = (x | (x << 6)) & 0x03030303u;
     return (x | (x << 3)) & 0x11111111u;
 }
-__global__ void kPackFrom2(const uint8_t* __restrict__ src, const uint32_t* __restrict__ exc, uint32_t nExc,
-                           uint64_t r0, uint64_t p0, uint64_t p1, uint32_t m, uint32_t rc, uint32_t dna5,
+__global__ void kPackFrom2(const uint8_t* __restrict__ src, uint32_t so, const uint32_t* __restrict__ exc,
+                           uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1, uint32_t m, uint32_t rc, uint32_t dna5,
                            uint32_t patWords, uint32_t patBlocks, uint32_t* __restrict__ pats,
                            uint4* __restrict__ pats3) {
     const uint64_t total = (p1 - p0) * patBlocks;
@@ -1900,7 +1901,7 @@ __global__ void kPackFrom2(const uint8_t* __restrict__ src, const uint32_t* __re
         const uint64_t r = rc ? p >> 1 : p;
         const bool rev = rc && (p & 1u);
         const uint32_t nsym = min(32u, m - 32u * b);
-        const uint64_t start = (r - r0) * m + (rev ? m - 32u * b - nsym : 32u * b);  // source symbols [start, start + nsym)
+        const uint64_t start = so + (r - r0) * m + (rev ? m - 32u * b - nsym : 32u * b);  // source symbols [start, start + nsym)
         const uint32_t* w = reinterpret_cast<const uint32_t*>(src + (start >> 4) * 4);
         const uint32_t sh = (uint32_t)(start & 15u) * 2u;
         uint64_t v = ((uint64_t)w[1] << 32) | w[0];
@@ -1935,13 +1936,13 @@ __global__ void kPackFrom2(const uint8_t* __restrict__ src, const uint32_t* __re
     }
 }
 
-void launchPackFrom2(const uint8_t* src, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0, uint64_t p1,
-                     uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks, uint32_t* pats,
-                     uint4* pats3, hipStream_t st) {
+void launchPackFrom2(const uint8_t* src, uint32_t so, const uint32_t* exc, uint32_t nExc, uint64_t r0, uint64_t p0,
+                     uint64_t p1, uint32_t m, bool rc, uint32_t sigma, uint32_t patWords, uint32_t patBlocks,
+                     uint32_t* pats, uint4* pats3, hipStream_t st) {
     const uint64_t total = (p1 - p0) * patBlocks;
     if (total == 0) return;
     const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 65536);
-    hipLaunchKernelGGL(kPackFrom2, dim3((unsigned)blocks), dim3(256), 0, st, src, exc, nExc, r0, p0, p1, m,
+    hipLaunchKernelGGL(kPackFrom2, dim3((unsigned)blocks), dim3(256), 0, st, src, so, exc, nExc, r0, p0, p1, m,
                        rc ? 1u : 0u, sigma == 6 ? 1u : 0u, patWords, patBlocks, pats, pats3);
     SH_HIP(hipGetLastError());
 }

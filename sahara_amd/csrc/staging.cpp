@@ -417,21 +417,35 @@ static void submitPack(Ctx* c, uint64_t j) {
     if (const char* e = std::getenv("SAHARA_PACK_PIECE")) pieceSyms = std::max<uint64_t>(4096, std::atoll(e)) & ~uint64_t(3);
     J.chunk = j;
     J.pieceSyms = pieceSyms;
-    J.pieces = (n + pieceSyms - 1) / pieceSyms;
     J.bad.store(0, std::memory_order_relaxed);
-    if (J.exc.size() < J.pieces) J.exc.resize(J.pieces);
-    for (auto& v : J.exc) v.clear();
-    J.group.begin(J.pieces);
     uint8_t* out = c->ring + slot * Ctx::kRingSlot;
-    const uint8_t* src = U.src + s0;
     std::vector<std::function<void()>> fs;
-    fs.reserve(J.pieces);
-    for (uint64_t k = 0; k < J.pieces; ++k)
-        fs.emplace_back([&J, out, src, n, sigma, k] {
-            const uint64_t lo = k * J.pieceSyms, hi = std::min(n, lo + J.pieceSyms);
-            if (pack2Best(src + lo, out + lo / 4, hi - lo, sigma, lo, J.exc[k])) J.bad.store(1, std::memory_order_relaxed);
-            J.group.oneDone();
-        });
+    if (U.prepacked) {  // codes as given: the chunk's bytes of the caller's buffer, copied in pieces
+        const uint64_t B0 = (U.sym0 + s0) / 4, nb = (U.sym0 + s0 + n + 3) / 4 - B0, pb = pieceSyms / 4;
+        J.pieces = (nb + pb - 1) / pb;
+        J.group.begin(J.pieces);
+        const uint8_t* src = U.src + B0;
+        fs.reserve(J.pieces);
+        for (uint64_t k = 0; k < J.pieces; ++k)
+            fs.emplace_back([&J, out, src, nb, pb, k] {
+                const uint64_t lo = k * pb, hi = std::min(nb, lo + pb);
+                std::memcpy(out + lo, src + lo, hi - lo);
+                J.group.oneDone();
+            });
+    } else {
+        J.pieces = (n + pieceSyms - 1) / pieceSyms;
+        if (J.exc.size() < J.pieces) J.exc.resize(J.pieces);
+        for (auto& v : J.exc) v.clear();
+        J.group.begin(J.pieces);
+        const uint8_t* src = U.src + s0;
+        fs.reserve(J.pieces);
+        for (uint64_t k = 0; k < J.pieces; ++k)
+            fs.emplace_back([&J, out, src, n, sigma, k] {
+                const uint64_t lo = k * J.pieceSyms, hi = std::min(n, lo + J.pieceSyms);
+                if (pack2Best(src + lo, out + lo / 4, hi - lo, sigma, lo, J.exc[k])) J.bad.store(1, std::memory_order_relaxed);
+                J.group.oneDone();
+            });
+    }
     hostPool(c).postMany(fs);
     U.submitted = j + 1;
     c->mark("pack posted", j);
@@ -497,8 +511,20 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     const uint64_t b0 = s0 / 2, b1 = (s1 + 1) / 2;
     uint32_t bits = U.bits;
     uint64_t nExc = 0, excOff = 0;  // 2 bits: the N list, at byte excOff of the chunk's region
+    const uint32_t* excDev = nullptr;  // ... on the device
+    uint32_t so = 0;                   // read r0's first symbol in the chunk's first byte (prepacked)
     uint8_t* out = c->ring + slot * Ctx::kRingSlot;
-    if (bits == 2) {
+    if (bits == 2 && U.prepacked) {
+        if (U.submitted <= j) submitPack(c, j);
+        c->packJobs[slot].group.wait();
+        c->mark("slot free", j);
+        const uint64_t S0 = U.sym0 + s0, S1 = U.sym0 + s1;
+        so = (uint32_t)(S0 & 3u);
+        nExc = U.nFirst[j + 1] - U.nFirst[j];
+        excDev = c->nList.ptr + U.nFirst[j];
+        uploadCopy(c, c->nibPats.ptr + b0, out, (S1 + 3) / 4 - S0 / 4);
+        c->mark("dma enqueued", j);
+    } else if (bits == 2) {
         if (U.submitted <= j) submitPack(c, j);  // (U.submitted == j: chunks post in order)
         Ctx::PackJob& J = c->packJobs[slot];
         J.group.wait();
@@ -519,6 +545,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
                 e += v.size() * 4;
             }
             uploadCopy(c, c->nibPats.ptr + b0, out, excOff + 4 * nExc);
+            excDev = reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff);
             c->mark("dma enqueued", j);
         }
     } else {
@@ -556,9 +583,8 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
     U.chunks[bits == 2 ? 0 : bits == 4 ? 1 : 2]++;
     const uint64_t p0 = U.rc ? 2 * r0 : r0, p1 = U.rc ? std::min(2 * r1, c->npat) : r1;
     if (bits == 2) {  // straight into both pattern forms (no byte pass)
-        launchPackFrom2(c->nibPats.ptr + b0, reinterpret_cast<const uint32_t*>(c->nibPats.ptr + b0 + excOff),
-                        (uint32_t)nExc, r0, p0, p1, m, U.rc, sigma, c->patWords, c->patBlocks, c->pats.ptr + 0,
-                        c->pats3.ptr + 0, kst);
+        launchPackFrom2(c->nibPats.ptr + b0, so, excDev, (uint32_t)nExc, r0, p0, p1, m, U.rc, sigma, c->patWords,
+                        c->patBlocks, c->pats.ptr + 0, c->pats3.ptr + 0, kst);
         U.done = r1;
         c->mark("packed", r0 / U.chunk);
         return;
@@ -626,10 +652,45 @@ void stageScheme(Ctx* c, uint64_t npat, uint32_t m, const uint32_t* pi, const ui
 // during the pass (uploadChunk). src holds `rows` rows of m symbols: the
 // patterns, or (rc) the reads whose interleave with their reverse
 // complements, cut to npat, is the query list.
+// Reads given two bits per symbol: their N positions (stream positions,
+// ascending) checked and uploaded once per call, each relative to the first
+// whole byte of its chunk, chunk j's from entry U.nFirst[j] (kPackFrom2 sets
+// them). Every 2-bit code is an A, C, G or T: nothing else to check.
+static void stagePackedN(Ctx* c, const PackedReads& P, uint64_t rows, uint32_t m) {
+    Ctx::Upload& U = c->up;
+    U.prepacked = true;
+    U.sym0 = P.sym0;
+    const uint64_t lo = P.sym0, hi = P.sym0 + rows * m;
+    const uint64_t* all = P.nCount ? P.nPos : nullptr;
+    const uint64_t* b = all ? std::lower_bound(all, all + P.nCount, lo) : nullptr;
+    const uint64_t* e = all ? std::lower_bound(b, all + P.nCount, hi) : nullptr;
+    const uint64_t nN = all ? (uint64_t)(e - b) : 0;
+    for (uint64_t i = 1; i < nN; ++i)
+        if (b[i] <= b[i - 1]) throw Error("N positions of packed reads must be strictly ascending");
+    if (nN && c->I.sigma == 5) throw Error("pattern rank out of range for this index");  // N is no dna4 rank
+    const uint64_t nch = chunkCount(U);
+    U.nFirst.assign(nch + 1, nN);
+    std::vector<uint32_t> rel(nN);
+    uint64_t i = 0;
+    for (uint64_t j = 0; j < nch; ++j) {
+        const uint64_t S0 = lo + j * U.chunk * m, S1 = lo + std::min(rows, (j + 1) * U.chunk) * m;
+        U.nFirst[j] = i;
+        for (; i < nN && b[i] < S1; ++i) rel[i] = (uint32_t)(b[i] - (S0 & ~uint64_t(3)));
+    }
+    c->nList.reserve(std::max<uint64_t>(nN, 1));
+    if (nN) SH_HIP(hipMemcpy(c->nList.ptr, rel.data(), nN * 4, hipMemcpyHostToDevice));
+}
+
+// src holds `rows` rows of m symbols: the patterns, or (rc) the reads whose
+// interleave with their reverse complements, cut to npat, is the query list;
+// one rank per byte, or (packed) two bits per symbol with the N positions
+// listed (the reads of sahara_gpu_search_packed[_compact]).
 void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t npat, uint32_t m,
-                   const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit) {
+                   const uint32_t* pi, const uint32_t* l, const uint32_t* u, uint32_t ns, int edit,
+                   const PackedReads* packed) {
     c->staged = c->streaming = false;
     if (m == 0 || m > kMaxPatternLen) throw Error("pattern length out of range");
+    if (packed && c->I.sigma != 5 && c->I.sigma != 6) throw Error("reads two bits per symbol need a dna4 or dna5 index");
     stageScheme(c, npat, m, pi, l, u, ns, edit);
     c->m = m;
     c->npat = npat;
@@ -658,6 +719,7 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
         if (b == 2 || b == 4 || b == 8) U.bits = (uint32_t)b;
     }
     if (U.bits == 2 && c->I.sigma != 5 && c->I.sigma != 6) U.bits = 4;
+    if (packed) U.bits = 2;
     // 1M patterns per chunk (SAHARA_UPLOAD_CHUNK), at most one ring slot of nibbles
     uint64_t chunkPats = 1u << 20;
     if (const char* e = std::getenv("SAHARA_UPLOAD_CHUNK")) chunkPats = std::max<uint64_t>(2, std::atoll(e));
@@ -670,6 +732,7 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     while (m % g) g /= 2;
     const uint64_t step = std::max<uint64_t>(2, 32 / g);
     U.chunk = std::max<uint64_t>(step, chunk - chunk % step);
+    if (packed) stagePackedN(c, *packed, rows, m);
     if (c->ringInit.joinable()) c->ringInit.join();
     if (U.bits != 8 && !c->ring) throw Error("could not pin the upload ring buffer");
     for (hipEvent_t e : c->ringEv) SH_HIP(hipEventSynchronize(e));  // the last call's DMAs

@@ -7,9 +7,9 @@
 #include <random>
 #include <string>
 
-#include "../sahara_amd/cli/fasta.h"
+#include "../sahara_amd/csrc/fasta.h"
 
-using namespace sahara_cli;
+using namespace sahara_io;
 
 int main(int argc, char** argv) {
     const std::string path = argc > 1 ? argv[1] : "/tmp/fasta_fuzz.fa";
@@ -71,6 +71,22 @@ int main(int argc, char** argv) {
                     ok = ok && D.bad == (badRec >= 0);
                     if (ok && D.bad)
                         ok = (long)D.badRecord == badRec && (long)D.badPos == badPos && D.badId == ids[(size_t)badRec];
+                    // the 2-bit form: the same records, codes of the valid
+                    // symbols (A C G T = 0 1 2 3, N = 0), N listed, same first
+                    // invalid character
+                    FastaData E = parseFastaParallel(path, sigma, nt, piece, FastaForm::kCodes2);
+                    ok = ok && E.offs == D.offs && E.bad == D.bad && E.badRecord == D.badRecord &&
+                         E.badPos == D.badPos && E.badId == D.badId && E.ranks.size() == (D.ranks.size() + 3) / 4;
+                    std::vector<uint64_t> wantN;
+                    for (uint64_t q = 0; ok && q < D.ranks.size(); ++q) {
+                        const uint8_t r = D.ranks[q];
+                        if (r >= sigma) continue;  // invalid: code unspecified
+                        const uint32_t code = (E.ranks[q / 4] >> (2 * (q % 4))) & 3u;
+                        const uint32_t want2 = r == 1 ? 0 : r == 2 ? 1 : r == 3 ? 2 : (sigma == 6 && r == 4) ? 0 : 3;
+                        ok = code == want2;
+                        if (sigma == 6 && r == 4) wantN.push_back(q);
+                    }
+                    ok = ok && E.nPos == wantN && E.symbols == D.ranks.size();
                 }
                 if (!ok) {
                     std::printf("mismatch: iteration %d piece %zu threads %u (%s | %s)\n", it, piece, nt, werr.c_str(),
