@@ -299,8 +299,87 @@ static PScheme fromTable(std::initializer_list<TableRow> rows, int minK) {
     return out;
 }
 
+// PEX hierarchical partition (Navarro and Raffinot 2002; Kärkkäinen and Na
+// 2007) as a search scheme, restated with parent links: nodes over leaf
+// ranges [lo, hi) with budget hi - lo - 1; top-down splits a node of budget e
+// after floor(e / 2) + 1 leaves, bottom-up pairs neighbours level by level
+// (an odd last node moves up as it is). Search of leaf j: leaf j exact, then
+// for each ancestor, from the leaf's parent up, the parts of the ancestor not
+// yet covered (the side the other child lies on, outward), cumulative errors
+// <= the ancestor's budget; with lower bounds, a leaf under the right child
+// requires the ancestor to hold more errors than the left child's budget.
+static PScheme genPex(int K, int minK, bool bottomUp, bool lower) {
+    struct N { int lo, hi, parent, leftChild; };
+    std::vector<N> nd;
+    std::vector<int> leafNode(K + 1, -1);
+    if (!bottomUp) {
+        std::vector<int> todo{0};
+        nd.push_back({0, K + 1, -1, -1});
+        while (!todo.empty()) {
+            const int id = todo.back();
+            todo.pop_back();
+            const int lo = nd[id].lo, hi = nd[id].hi;
+            if (hi - lo == 1) { leafNode[lo] = id; continue; }
+            const int cut = lo + (hi - lo - 1) / 2 + 1;
+            const int a = (int)nd.size();
+            nd.push_back({lo, cut, id, -1});
+            nd.push_back({cut, hi, id, -1});
+            nd[id].leftChild = a;
+            todo.push_back(a);
+            todo.push_back(a + 1);
+        }
+    } else {
+        std::vector<int> cur;
+        for (int j = 0; j <= K; ++j) { leafNode[j] = (int)nd.size(); cur.push_back((int)nd.size()); nd.push_back({j, j + 1, -1, -1}); }
+        while (cur.size() > 1) {
+            std::vector<int> nxt;
+            size_t i = 0;
+            for (; i + 1 < cur.size(); i += 2) {
+                const int id = (int)nd.size();
+                nd.push_back({nd[cur[i]].lo, nd[cur[i + 1]].hi, -1, cur[i]});
+                nd[cur[i]].parent = nd[cur[i + 1]].parent = id;
+                nxt.push_back(id);
+            }
+            if (i < cur.size()) nxt.push_back(cur[i]);
+            cur = nxt;
+        }
+    }
+    PScheme out;
+    for (int j = 0; j <= K; ++j) {
+        PSearch s{{j}, {0}, {0}};
+        int child = leafNode[j];
+        for (int a = nd[child].parent; a >= 0; child = a, a = nd[a].parent) {
+            const int budget = nd[a].hi - nd[a].lo - 1;
+            const int last = s.l.back();
+            if (nd[child].hi < nd[a].hi)
+                for (int t = nd[child].hi; t < nd[a].hi; ++t) { s.pi.push_back(t); s.l.push_back(last); s.u.push_back(budget); }
+            else
+                for (int t = nd[child].lo - 1; t >= nd[a].lo; --t) { s.pi.push_back(t); s.l.push_back(last); s.u.push_back(budget); }
+            const bool underRight = nd[a].leftChild != child;
+            if (lower && underRight) {
+                const N& L = nd[nd[a].leftChild];
+                s.l.back() = std::max(s.l.back(), L.hi - L.lo);
+            }
+        }
+        s.l.back() = std::max(s.l.back(), minK);
+        out.push_back(s);
+    }
+    return out;
+}
+
 static bool makeScheme(const std::string& name, int minK, int maxK, PScheme& out) {
     if (minK < 0 || maxK < minK) return false;
+    if (name == "pex-td" || name == "pex-td-l" || name == "pex-bu" || name == "pex-bu-l") {
+        out = genPex(maxK, minK, name[4] == 'b', name.size() == 8);
+        return true;
+    }
+    if (name == "kianfar") {  // Kianfar et al. 2018, the paper's optimum schemes for K <= 2
+        if (maxK > 2) return false;
+        if (maxK == 0) out = {PSearch{{0}, {0}, {0}}};
+        else if (maxK == 1) out = fromTable({{"12", "00", "01"}, {"21", "01", "01"}}, minK);
+        else out = fromTable({{"1234", "0011", "0022"}, {"3214", "0000", "1122"}, {"4321", "0002", "0122"}}, minK);
+        return true;
+    }
     const bool tableFamily = name == "lam" || name == "kucherov-k1" || name == "kucherov-k2";
     if (tableFamily && maxK > 2) return false;  // tables for k <= 2 only
     if (tableFamily && maxK == 0) {             // one exact search over the family's parts

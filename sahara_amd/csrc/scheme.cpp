@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <initializer_list>
 #include <string>
 #include <vector>
@@ -129,6 +130,105 @@ std::vector<int> rightThenLeft(int P, int j) {
 // K = 0 for a table family: one exact search over its P parts
 std::vector<Part> exactOnly(int P) { return {Part{connected(P, 0, true), std::vector<int>(P, 0), std::vector<int>(P, 0)}}; }
 
+// PEX: the hierarchical partition of Navarro and Baeza-Yates' filter (as
+// Navarro and Raffinot, "Flexible Pattern Matching in Strings", 2002, and
+// Kärkkäinen and Na state it), written as a search scheme. The K + 1 parts
+// are the leaves of a binary tree; a node over leaves [a, b) may hold
+// e = b - a - 1 errors, and its two children e1 and e2 with e1 + e2 + 1 = e,
+// so one child of a node within its budget is within its own: some leaf is
+// error-free and every node above it is within its budget. One search per
+// leaf: the leaf exactly, then each ancestor's other child, nearest part
+// first, bounded by that ancestor's budget. The tree is built top-down
+// (a node of budget e splits into floor(e / 2) + 1 leaves on the left and the
+// rest on the right) or bottom-up (leaves merged pairwise from the left,
+// level by level, an odd last node carried up). With lower bounds (the -l
+// names), ties go to the left child: a search whose leaf lies in the right
+// child of a node sees the left child over its budget, so the node holds
+// at least e1 + 1 errors once the search has covered it.
+struct PexNode {
+    int a, b;           // leaves [a, b)
+    int left, right;    // children (-1: a leaf)
+};
+
+int pexTopDown(std::vector<PexNode>& t, int a, int b) {
+    const int id = (int)t.size();
+    t.push_back({a, b, -1, -1});
+    if (b - a > 1) {
+        const int e = b - a - 1, mid = a + e / 2 + 1;
+        const int l = pexTopDown(t, a, mid);
+        const int r = pexTopDown(t, mid, b);
+        t[id].left = l;
+        t[id].right = r;
+    }
+    return id;
+}
+
+int pexBottomUp(std::vector<PexNode>& t, int P) {
+    std::vector<int> level;
+    for (int j = 0; j < P; ++j) {
+        level.push_back((int)t.size());
+        t.push_back({j, j + 1, -1, -1});
+    }
+    while (level.size() > 1) {
+        std::vector<int> up;
+        for (size_t i = 0; i + 1 < level.size(); i += 2) {
+            up.push_back((int)t.size());
+            t.push_back({t[level[i]].a, t[level[i + 1]].b, level[i], level[i + 1]});
+        }
+        if (level.size() % 2) up.push_back(level.back());
+        level.swap(up);
+    }
+    return level[0];
+}
+
+std::vector<Part> pexScheme(int maxK, int minK, bool bottomUp, bool lower) {
+    const int P = maxK + 1;
+    std::vector<PexNode> t;
+    const int root = bottomUp ? pexBottomUp(t, P) : pexTopDown(t, 0, P);
+    std::vector<Part> out;
+    // depth-first over the tree with the path of (node, came from the right child)
+    std::vector<std::pair<int, bool>> path;
+    auto leafSearch = [&](int j) {
+        Part p;
+        p.pi = {j};
+        p.l = {0};
+        p.u = {0};
+        int lo = j, hi = j + 1;  // parts covered
+        for (size_t k = path.size(); k-- > 0;) {
+            const PexNode& A = t[path[k].first];
+            const int e = A.b - A.a - 1;
+            const bool fromRight = path[k].second;
+            const int before = (int)p.pi.size();
+            for (; hi < A.b; ++hi) p.pi.push_back(hi);
+            for (; lo > A.a; --lo) p.pi.push_back(lo - 1);
+            for (int i = before; i < (int)p.pi.size(); ++i) {
+                p.l.push_back(p.l.back());
+                p.u.push_back(e);
+            }
+            if (lower && fromRight) {
+                const PexNode& L = t[A.left];
+                p.l.back() = std::max(p.l.back(), L.b - L.a);  // left child's budget + 1
+            }
+        }
+        p.l.back() = std::max(p.l.back(), minK);
+        out.push_back(p);
+    };
+    std::function<void(int)> walk = [&](int id) {
+        const PexNode& n = t[id];
+        if (n.left < 0) {
+            leafSearch(n.a);
+            return;
+        }
+        path.push_back({id, false});
+        walk(n.left);
+        path.back().second = true;
+        walk(n.right);
+        path.pop_back();
+    };
+    walk(root);
+    return out;
+}
+
 bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& out) {
     if (minK < 0 || maxK < minK || maxK > 15) return false;
     // Lam et al. 2009 (bidirectional BWT, k <= 2), as Kucherov, Salikhov and
@@ -140,9 +240,13 @@ bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& ou
         else return false;
         return true;
     }
-    // Kucherov, Salikhov, Tsur 2016, K + 1 parts (k1) and K + 2 parts (k2),
-    // K <= 2; the K + 2 tables are this build's tightest bounds for KST's
-    // three search shapes (forward, backward, bidirectional from part 2)
+    // Kucherov, Salikhov and Tsur's search shapes (2016), K + 1 parts (k1) and
+    // K + 2 parts (k2), K <= 2, with this build's bounds: k1 at K = 1 is
+    // their non-redundant scheme, k1 at K = 2 is Lam's table as they print
+    // it, and the K + 2 tables are this build's tightest bounds for their
+    // three shapes (forward, backward, bidirectional from part 2). Upstream's
+    // kucherov tables are not in the container: hits and node counts of these
+    // names are unpinned against it
     if (name == "kucherov-k1") {
         if (maxK == 0) out = exactOnly(1);
         else if (maxK == 1) out = table({"12,00,01", "21,01,01"}, minK);
@@ -218,6 +322,20 @@ bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& ou
             }
         return true;
     }
+    // Kianfar et al. 2018's optimum search schemes (ILP optimum for K = 1,
+    // 2), as the paper tabulates them (1-based): K + 1 and K + 2 parts.
+    // Restated for K <= 2 only (unpinned against upstream's table)
+    if (name == "kianfar") {
+        if (maxK == 0) out = exactOnly(1);
+        else if (maxK == 1) out = table({"12,00,01", "21,01,01"}, minK);
+        else if (maxK == 2) out = table({"1234,0011,0022", "3214,0000,1122", "4321,0002,0122"}, minK);
+        else return false;
+        return true;
+    }
+    if (name == "pex-td" || name == "pex-td-l" || name == "pex-bu" || name == "pex-bu-l") {
+        out = pexScheme(maxK, minK, name.compare(0, 6, "pex-bu") == 0, name.size() == 8);
+        return true;
+    }
     if (name == "backtracking") {
         out = {Part{{0}, {minK}, {maxK}}};
         return true;
@@ -243,22 +361,31 @@ bool generate(const std::string& name, int minK, int maxK, std::vector<Part>& ou
     return false;
 }
 
-// in the reference's listing order (search_scheme.cpp:192); the names it lists
-// beyond these (optimum, 01*0_opt, kianfar, hato, pex-*) have no construction
-// restatable offline and stay unknown (search.cpp:181's error)
+// in the reference's listing order (search_scheme.cpp:192). Every table here
+// is this build's restatement of a published construction; upstream's tables
+// are not in the container, so each is unpinned against upstream (hits under
+// P-set are not: a complete scheme finds the same positions, tests/
+// test_scheme.py). The names it lists beyond these (optimum, 01*0_opt, hato)
+// have no published construction restatable offline and stay unknown
+// (search.cpp:181's error).
 const char* kNames[] = {"backtracking", "01*0", "pigeon", "pigeon_opt", "suffix", "h2-k1", "h2-k2", "h2-k3",
-                        "kucherov-k1", "kucherov-k2", "lam"};
+                        "kianfar", "kucherov-k1", "kucherov-k2", "lam", "pex-td", "pex-td-l", "pex-bu", "pex-bu-l"};
 const char* kDescs[] = {"single part, errors anywhere",
-                        "k+2 parts, one search per 0 1* 0 seed (Vroland et al.)",
+                        "k+2 parts, one search per 0 1* 0 seed (Vroland et al.; this build's bounds)",
                         "k+1 parts, one exact part per search (pigeonhole)",
-                        "k+1 parts, pigeonhole with tightened bounds",
-                        "k+1 parts, suffix filter (Karkkainen and Na)",
-                        "k+1 parts, greedy-box optimum-style scheme",
-                        "k+2 parts, greedy-box optimum-style scheme (default)",
-                        "k+3 parts, greedy-box optimum-style scheme",
-                        "k+1 parts, Kucherov, Salikhov and Tsur (k <= 2)",
-                        "k+2 parts, Kucherov, Salikhov and Tsur shapes (k <= 2)",
-                        "Lam et al. bidirectional scheme (k <= 2)"};
+                        "k+1 parts, pigeonhole with this build's tightened bounds",
+                        "k+1 parts, suffix filter (Karkkainen and Na; this build's bounds)",
+                        "k+1 parts, this build's greedy-box scheme",
+                        "k+2 parts, this build's greedy-box scheme (default)",
+                        "k+3 parts, this build's greedy-box scheme",
+                        "Kianfar et al. optimum search schemes (k <= 2, the paper's table)",
+                        "k+1 parts, Kucherov, Salikhov and Tsur shapes, this build's bounds (k <= 2)",
+                        "k+2 parts, Kucherov, Salikhov and Tsur shapes, this build's bounds (k <= 2)",
+                        "Lam et al. bidirectional scheme (k <= 2)",
+                        "k+1 parts, PEX hierarchical partition, tree built top-down",
+                        "k+1 parts, PEX top-down with lower bounds (left child preferred)",
+                        "k+1 parts, PEX hierarchical partition, tree built bottom-up",
+                        "k+1 parts, PEX bottom-up with lower bounds (left child preferred)"};
 
 // expand(oss, len) with explicit part sizes: inside a part the order follows
 // the search direction; upper bounds hold for the whole part, lower bounds

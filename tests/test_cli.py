@@ -220,6 +220,26 @@ def test_cli_errors_after_index_load(tmp_path, gpu_device):
     rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
                      "-g", "nope")
     assert rc == 1 and 'unknown search scheme generetaror "nope"' in err
+    # names the reference lists whose tables are not restated here keep its error
+    for name in ("optimum", "01*0_opt", "hato"):
+        rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                         "-g", name)
+        assert rc == 1 and f'unknown search scheme generetaror "{name}"' in err and "pex-bu-l" in err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gen", ["kianfar", "pex-td", "pex-td-l", "pex-bu", "pex-bu-l"])
+def test_cli_new_generators_find_the_golden_positions(tmp_path, gpu_device, gen):
+    """-g with the PEX and Kianfar schemes: the same (qid, seqId, pos) set as
+    the golden file of the default generator (a complete scheme finds every
+    position; duplicates and e follow the scheme)."""
+    out = tmp_path / "h.txt"
+    rc, _, err = run("search", "-q", os.path.join(GOLD, "reads_a.fa"), "-i", os.path.join(GOLD, IDX["a"]),
+                     "-e", 2, "-g", gen, "-o", out)
+    assert rc == 0, err
+    got = {tuple(r) for r in read_hits(out, 3).tolist()}
+    want = {tuple(r[:3]) for r in expected("a_lev_k2").tolist()}
+    assert got == want
 
 
 # ------------------------------------------------------- read_simulator ----

@@ -60,7 +60,9 @@ MODES = [(True, True), (False, False), (True, False), (False, True)]  # (verify,
 @pytest.mark.gpu
 @pytest.mark.parametrize("gen,k,edit", [("lam", 2, True), ("kucherov-k1", 1, True), ("kucherov-k2", 2, True),
                                         ("pigeon_opt", 3, True), ("suffix", 2, True), ("01*0", 2, True),
-                                        ("01*0", 3, False), ("suffix", 3, False)])
+                                        ("01*0", 3, False), ("suffix", 3, False), ("kianfar", 2, True),
+                                        ("kianfar", 1, False), ("pex-td", 3, True), ("pex-td-l", 2, True),
+                                        ("pex-bu", 4, True), ("pex-bu-l", 3, False)])
 def test_gpu_equals_oracle_published_generators(gpu_device, gen, k, edit):
     """Each of the published generators (search_scheme.cpp:192 names): GPU ==
     oracle multiset in every execution mode, seeds from the k-mer table and

@@ -85,9 +85,10 @@ CASES = [  # (sigma, edit, k, m, with_n, repeats)
 
 @pytest.mark.parametrize("sigma,edit,k,m,with_n,repeats", CASES)
 @pytest.mark.parametrize("gen", ["backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3", "lam", "kucherov-k1",
-                                 "kucherov-k2", "pigeon_opt", "suffix", "01*0"])
+                                 "kucherov-k2", "pigeon_opt", "suffix", "01*0", "kianfar", "pex-td", "pex-td-l",
+                                 "pex-bu", "pex-bu-l"])
 def test_pset_equals_bruteforce(sigma, edit, k, m, with_n, repeats, gen):
-    if gen in ("lam", "kucherov-k1", "kucherov-k2") and k > 2:
+    if gen in ("lam", "kucherov-k1", "kucherov-k2", "kianfar") and k > 2:
         return  # tables for k <= 2
     rng = np.random.default_rng(1000 * k + m + sigma + (7 if edit else 0))
     recs = random_records(rng, [600, 250, 400], sigma, with_n=with_n, repeats=repeats)

@@ -7,10 +7,10 @@ import oracle as O
 import sahara_amd as sa
 
 GENS = ["backtracking", "pigeon", "h2-k1", "h2-k2", "h2-k3", "lam", "kucherov-k1", "kucherov-k2", "pigeon_opt",
-        "suffix", "01*0"]
+        "suffix", "01*0", "kianfar", "pex-td", "pex-td-l", "pex-bu", "pex-bu-l"]
 # published tables for k <= 2 only (unknown generator beyond, like upstream's
 # generators outside their tables)
-KMAX = {"lam": 2, "kucherov-k1": 2, "kucherov-k2": 2}
+KMAX = {"lam": 2, "kucherov-k1": 2, "kucherov-k2": 2, "kianfar": 2}
 # the reference's listing (search_scheme.cpp:192); the rest stay unknown here
 REFERENCE_ORDER = ["backtracking", "optimum", "01*0", "01*0_opt", "pigeon", "pigeon_opt", "suffix", "h2-k1", "h2-k2",
                    "h2-k3", "kianfar", "kucherov-k1", "kucherov-k2", "lam", "hato", "pex-td", "pex-td-l", "pex-bu",
@@ -41,7 +41,7 @@ def dists(P, lo, hi):
 
 
 @pytest.mark.parametrize("gen", GENS)
-@pytest.mark.parametrize("k", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("k", [0, 1, 2, 3, 4, 5, 6])
 def test_complete_and_valid(gen, k):
     if k > KMAX.get(gen, 99):
         with pytest.raises(sa.SaharaError):
@@ -164,3 +164,43 @@ def test_redundancy_where_published_schemes_differ():
         assert min(opt) == 1 and all(a <= b for a, b in zip(opt, plain)) and sum(opt) < sum(plain)
     assert set(multiplicity("kucherov-k1", 1)) == {1}
     assert max(multiplicity("lam", 1)) == 2
+
+
+@pytest.mark.parametrize("gen,k,want", [
+    ("pex-td", 2, [([0, 1, 2], [0, 0, 0], [0, 1, 2]), ([1, 0, 2], [0, 0, 0], [0, 1, 2]), ([2, 1, 0], [0, 0, 0], [0, 2, 2])]),
+    ("pex-td-l", 2, [([0, 1, 2], [0, 0, 0], [0, 1, 2]), ([1, 0, 2], [0, 1, 1], [0, 1, 2]),
+                     ([2, 1, 0], [0, 0, 2], [0, 2, 2])]),
+    # K = 4: bottom-up pairs (0 1)(2 3) then merges them, leaf 4 joins last;
+    # top-down splits 3 + 2 leaves at the root
+    ("pex-bu", 4, [([0, 1, 2, 3, 4], [0] * 5, [0, 1, 3, 3, 4]), ([1, 0, 2, 3, 4], [0] * 5, [0, 1, 3, 3, 4]),
+                   ([2, 3, 1, 0, 4], [0] * 5, [0, 1, 3, 3, 4]), ([3, 2, 1, 0, 4], [0] * 5, [0, 1, 3, 3, 4]),
+                   ([4, 3, 2, 1, 0], [0] * 5, [0, 4, 4, 4, 4])]),
+    ("pex-td", 4, [([0, 1, 2, 3, 4], [0] * 5, [0, 1, 2, 4, 4]), ([1, 0, 2, 3, 4], [0] * 5, [0, 1, 2, 4, 4]),
+                   ([2, 1, 0, 3, 4], [0] * 5, [0, 2, 2, 4, 4]), ([3, 4, 2, 1, 0], [0] * 5, [0, 1, 4, 4, 4]),
+                   ([4, 3, 2, 1, 0], [0] * 5, [0, 1, 4, 4, 4])]),
+    ("kianfar", 2, [([0, 1, 2, 3], [0, 0, 1, 1], [0, 0, 2, 2]), ([2, 1, 0, 3], [0, 0, 0, 0], [1, 1, 2, 2]),
+                    ([3, 2, 1, 0], [0, 0, 0, 2], [0, 1, 2, 2])]),
+])
+def test_pex_and_kianfar_shapes(gen, k, want):
+    """The PEX trees (top-down: a node of budget e keeps floor(e / 2) + 1
+    leaves on the left; bottom-up: neighbours paired level by level) and
+    Kianfar et al.'s K = 2 optimum table, as part-level schemes."""
+    pi, l, u = sa.scheme_parts(gen, 0, k)
+    got = [(pi[s].tolist(), l[s].tolist(), u[s].tolist()) for s in range(pi.shape[0])]
+    assert got == want
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5])
+def test_pex_lower_bounds_cut_redundancy(k):
+    """With lower bounds (ties to the left child) a PEX scheme covers every
+    error distribution at most as often as without, and in total less often;
+    for k <= 2 exactly once. (Beyond, cumulative bounds cannot say "the left
+    child alone is over its budget", so some overlap stays.)"""
+    def mult(gen):
+        pi, l, u = sa.scheme_parts(gen, 0, k)
+        return [sum(covers(pi[s], l[s], u[s], d) for s in range(pi.shape[0])) for d in dists(pi.shape[1], 0, k)]
+    for tree in ("td", "bu"):
+        low, plain = mult(f"pex-{tree}-l"), mult(f"pex-{tree}")
+        assert min(low) == 1 and all(a <= b for a, b in zip(low, plain)) and sum(low) < sum(plain)
+        if k <= 2:
+            assert set(low) == {1}
