@@ -106,6 +106,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the secondary PCIe-inclusive calls (rank reads, whole records, host patterns)")
     ap.add_argument("--no-ingest", action="store_true", help="skip timing the FASTA ingest (both forms)")
+    ap.add_argument("--no-device-resident", action="store_true",
+                    help="skip the device-resident pass (profiling: every search launch then has the timed call's "
+                         "shape); implies --no-count --no-verify --no-e2e --no-ref-path --no-cpu")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed RCCL gather of hit records")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the full-size checks (origin recall; GPU suffix array against the text)")
@@ -118,6 +121,8 @@ def main():
                          "default profiles/traffic_<config>.json when it exists")
     args = ap.parse_args()
 
+    if args.no_device_resident:
+        args.no_count = args.no_verify = args.no_e2e = args.no_ref_path = args.no_cpu = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -207,22 +212,25 @@ def main():
         del h
 
     # ---- the same pass device-resident: reads staged in HBM, hits left there
-    idx.stage(pats, scheme, edit=edit)
-    if args.execution == "reference":
-        idx.set_mode(verify=False, locate_sa=False)
-    for i in range(args.warmup):
-        idx.run()
-    barrier()
-    t0 = time.perf_counter()
     dr_stats = {"search_ms": 0.0, "text_ms": 0.0, "search_launches": 0, "text_launches": 0}
-    for i in range(args.steps):
-        nh = idx.run()
-        st = idx.stats()
-        for kk in dr_stats:
-            dr_stats[kk] += st[kk]
-    barrier()
-    dr_elapsed = time.perf_counter() - t0
-    digest = idx.digest()
+    if args.no_device_resident:
+        dr_elapsed, nh, digest = None, n_packed, None
+    else:
+        idx.stage(pats, scheme, edit=edit)
+        if args.execution == "reference":
+            idx.set_mode(verify=False, locate_sa=False)
+        for i in range(args.warmup):
+            idx.run()
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            nh = idx.run()
+            st = idx.stats()
+            for kk in dr_stats:
+                dr_stats[kk] += st[kk]
+        barrier()
+        dr_elapsed = time.perf_counter() - t0
+        digest = idx.digest()
     if args.execution == "reference":  # the timed steps are this mode's
         elapsed, step_stats, n_packed, packed_hits = dr_elapsed, dr_stats, nh, None
 
@@ -233,16 +241,17 @@ def main():
         per_rank = {"index_build_s": [round(v, 2) for v in values_of_ranks(build_s, device="cuda")],
                     "ms_per_step": [round(v * 1e3 / args.steps, 3) for v in values_of_ranks(elapsed, device="cuda")],
                     "device_resident_ms_per_step": [round(v * 1e3 / args.steps, 3)
-                                                    for v in values_of_ranks(dr_elapsed, device="cuda")],
+                                                    for v in values_of_ranks(dr_elapsed or 0.0, device="cuda")],
                     "hits": [int(v) for v in values_of_ranks(nh, device="cuda")]}
         elapsed = max_over_ranks(elapsed, device="cuda")  # RCCL over xGMI
-        dr_elapsed = max_over_ranks(dr_elapsed, device="cuda")
+        dr_elapsed = max_over_ranks(dr_elapsed, device="cuda") if dr_elapsed else None
         total_hits = sum_over_ranks(nh, device="cuda")
         if not args.no_gather:
             gather = gather_step(idx, nh, nreads, world, rank, barrier, dist, torch)
     else:
         total_hits = nh
-    same_hits = n_packed == nh and (packed_hits is None or hits_digest(packed_hits) == digest)
+    same_hits = None if digest is None else (n_packed == nh and (packed_hits is None or
+                                                                  hits_digest(packed_hits) == digest))
     del packed_hits
 
     # full-size checks that do not lean on the GPU's own index: every read is
@@ -388,15 +397,16 @@ def main():
                            "uploaded, RC interleave and pattern packing on the device (kPackFrom2), search, locate, "
                            "sort, each batch's hits as 8-B records (qid, text position, e; sahara_hit_blocks) copied "
                            "into pinned host memory recycled through sahara_gpu_free_blocks")
-    extra["same_hits"] = bool(same_hits)
-    extra["device_resident"] = {
-        "reads_per_s": round(nreads * world * args.steps / dr_elapsed, 1),
-        "ms_per_step": round(dr_elapsed * 1e3 / args.steps, 2),
-        "text_ms": round(dr_stats["text_ms"] / args.steps, 2),
-        "text_launches_per_step": dr_stats["text_launches"] // args.steps,
-        "timed_over": "sahara_gpu_run: reads (+RC) staged in HBM before timing, hits left in HBM"}
-    extra["device_resident"]["timed_call_over_device_resident"] = round(
-        reads_per_s / extra["device_resident"]["reads_per_s"], 3)
+    extra["same_hits"] = same_hits
+    if dr_elapsed:
+        extra["device_resident"] = {
+            "reads_per_s": round(nreads * world * args.steps / dr_elapsed, 1),
+            "ms_per_step": round(dr_elapsed * 1e3 / args.steps, 2),
+            "text_ms": round(dr_stats["text_ms"] / args.steps, 2),
+            "text_launches_per_step": dr_stats["text_launches"] // args.steps,
+            "timed_over": "sahara_gpu_run: reads (+RC) staged in HBM before timing, hits left in HBM"}
+        extra["device_resident"]["timed_call_over_device_resident"] = round(
+            reads_per_s / extra["device_resident"]["reads_per_s"], 3)
     if ingest:
         extra["ingest"] = ingest
     # other PCIe-inclusive calls (SURVEY §8(d)'s search wall time, as `value`):

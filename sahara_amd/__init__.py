@@ -402,11 +402,31 @@ def search_reads(index, reads, scheme, edit=True, reverse=True, limit=0, max_hit
     return _hits_array(out, n.value)
 
 
+class _Blocks:
+    """Owner of one sahara_hit_blocks: frees it when released or when the last
+    reference goes (the CompactHits, or an array made over its records)."""
+
+    def __init__(self, blocks):
+        self.b = blocks
+
+    def free(self):
+        if self.b is not None:
+            lib().sahara_gpu_free_blocks(C.byref(self.b))
+            self.b = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class _OwnedRecords:
-    """numpy array interface over library-owned records that keeps their owner
+    """numpy array interface over the records of a _Blocks that keeps it
     alive: an array made from it (CompactHits.recs, and every view of that)
-    holds the CompactHits, so its memory cannot go back to the library's pool
-    while any of them exists."""
+    holds the owner, so the memory cannot go back to the library's pool while
+    any of them exists. (The owner is not the CompactHits itself: no cycle,
+    so a dropped result frees its memory at once.)"""
 
     def __init__(self, owner, addr, n):
         self._owner = owner
@@ -416,18 +436,18 @@ class _OwnedRecords:
 class CompactHits:
     """Hits of sahara_gpu_search_reads_compact (include/sahara_hip.h
     sahara_hit_blocks): 8-B records in page-locked host memory, one block per
-    batch. `recs` is a read-only zero-copy view that keeps this object (and so
-    the memory) alive; close() releases the memory at once, after which views
-    taken earlier must not be read (copy them first). to_hits() expands the
-    records to HIT_DTYPE."""
+    batch. `recs` is a read-only zero-copy view that keeps the memory alive;
+    close() releases the memory at once, after which views taken earlier must
+    not be read (copy them first). to_hits() expands the records to HIT_DTYPE."""
 
     def __init__(self, blocks, index):
+        self._own = _Blocks(blocks)
         self._b = blocks
         self._index = index  # rec_starts belongs to the context
         n = blocks.n_hits
         if n:
             addr = C.cast(blocks.recs, C.c_void_p).value
-            self.recs = np.asarray(_OwnedRecords(self, addr, n))
+            self.recs = np.asarray(_OwnedRecords(self._own, addr, n))
         else:
             self.recs = np.zeros(0, np.uint64)
         nb = blocks.n_blocks
@@ -457,14 +477,8 @@ class CompactHits:
     def close(self):
         if self._b is not None:
             self.recs = None
-            lib().sahara_gpu_free_blocks(C.byref(self._b))
+            self._own.free()
             self._b = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def search_reads_compact(index, reads, scheme, edit=True, reverse=True, limit=0):

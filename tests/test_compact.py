@@ -121,7 +121,13 @@ def test_compact_records_view_outlives_its_call(gpu_device, monkeypatch):
     assert not recs.flags.writeable
     assert np.array_equal(recs, saved)
     del recs
-    gc.collect()
+    # a result dropped without close() frees its memory at once (no cycle
+    # keeps it for the garbage collector): the next call reuses the pool
+    import weakref
+    r = sa.search_reads_compact(gpu, reads, sch)
+    owner = weakref.ref(r._own)
+    del r
+    assert owner() is None
 
 
 @pytest.mark.gpu

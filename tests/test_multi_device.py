@@ -40,7 +40,7 @@ def device_lines(so):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpus", [2, 3])
+@pytest.mark.parametrize("gpus", [2, 3, 8])
 @pytest.mark.parametrize("name", ["a_lev_k2", "a_ham_k2", "a_best_k2", "a_lev_k2_pigeon_norev", "b_lev_k3"])
 def test_cli_gpus_n_equals_golden(gpus, name, tmp_path, gpu_device):
     c = CASES[name]
@@ -99,50 +99,104 @@ def test_cli_device_map_without_entry_is_loud(tmp_path, gpu_device):
     assert rc == 1 and "SAHARA_DEVICE_MAP has no entry for device 1" in err
 
 
+def _proc_status():
+    got = {}
+    for line in open("/proc/self/status"):
+        k, _, v = line.partition(":")
+        if k in ("Threads", "VmLck", "VmPin", "VmRSS"):
+            got[k] = v.strip()
+    return got
+
+
 @pytest.mark.gpu
-def test_concurrent_contexts_on_shards(gpu_device, monkeypatch):
-    """Two contexts searched from two host threads at once (ctypes drops the
-    GIL in the calls), each on its own shard of the reads, several rounds
-    (the second and later draw their hit sinks from the shared pinned pool):
-    the concatenation equals the golden multiset, every round."""
-    monkeypatch.setenv("SAHARA_DEVICE_MAP", "0,0")
+@pytest.mark.parametrize("n", [2, 8])
+def test_concurrent_contexts_on_shards(gpu_device, monkeypatch, n):
+    """n contexts searched from n host threads at once (ctypes drops the GIL
+    in the calls), each on its own shard of the reads, several rounds (the
+    second and later draw their hit sinks from the shared pinned pool), half
+    of them through the packed-reads compact call: the concatenation equals
+    the golden multiset, every round. At n = 8 (C4's host side: eight packing
+    pools, eight pinned rings, one shared hit pool under contention) the
+    process's thread count and locked memory are printed."""
+    monkeypatch.setenv("SAHARA_DEVICE_MAP", ",".join(["0"] * n))
     monkeypatch.setenv("SAHARA_PIN_MIN", "0")  # every hit buffer pinned and pooled
     monkeypatch.setenv("SAHARA_BATCH", "17")   # several batches per call: the pipeline's threads
     c = CASES["a_lev_k2"]
     reads = np.array(read_fasta(os.path.join(GOLD, "reads_a.fa"), SIGMA["a"]))
     m = reads.shape[1]
     scheme = sa.search_scheme("h2-k2", 0, c["k"], m)
-    ctx = [sa.BiFMIndex.load(os.path.join(GOLD, IDX["a"]), device=g) for g in (0, 1)]
+    before = _proc_status()
+    ctx = [sa.BiFMIndex.load(os.path.join(GOLD, IDX["a"]), device=g) for g in range(n)]
     for g in ctx:
         pl = g.placement()
         assert pl["device"] == 0
         assert pl["numa_node"] >= -1 and pl["n_cpus"] >= 0
         assert pl["n_cpus"] == 0 or pl["numa_node"] >= 0
-    half = len(reads) // 2 + 3
-    shards = [(0, half), (half, len(reads))]
+    bounds = [len(reads) * g // n + (3 if 0 < g < n else 0) for g in range(n)] + [len(reads)]
+    shards = [(bounds[g], bounds[g + 1]) for g in range(n)]
+    packed = sa.pack_reads(reads, SIGMA["a"])
     want = expected("a_lev_k2")
-    for _ in range(4):
-        out, errs = [None, None], []
+    peak = {}
+    for rnd in range(4):
+        out, errs = [None] * n, []
 
         def work(g):
             try:
                 r0, r1 = shards[g]
-                h = sa.search_reads(ctx[g], reads[r0:r1], scheme, edit=True)
-                rows = hits_as_rows(h).copy()
+                if (g + rnd) % 2:
+                    h = sa.search_packed_compact(ctx[g], packed.shard(r0, r1), scheme, edit=True)
+                    rows = hits_as_rows(h.to_hits()).copy()
+                    h.close()
+                else:
+                    rows = hits_as_rows(sa.search_reads(ctx[g], reads[r0:r1], scheme, edit=True)).copy()
                 rows[:, 0] += 2 * r0
                 out[g] = rows
             except Exception as e:  # surfaced below
                 errs.append(e)
 
-        th = [threading.Thread(target=work, args=(g,)) for g in (0, 1)]
+        th = [threading.Thread(target=work, args=(g,)) for g in range(n)]
         for t in th:
             t.start()
         for t in th:
             t.join()
         assert not errs, errs
         assert np.array_equal(np.concatenate(out), want)
+        peak = _proc_status()
+    print(f"\n[{n} contexts] before: {before} after the searches: {peak}")
     for g in ctx:
         g.close()
+
+
+@pytest.mark.gpu
+def test_cli_gpus_8_medium_equals_one(tmp_path, gpu_device):
+    """`sahara search --gpus 8` on a medium case (2 Mbp in 24 records, 20k
+    reads of 101 bp with 2 errors, so device shards start inside a byte of
+    the packed reads) writes the file `--gpus 1` writes, and both equal the
+    oracle's multiset."""
+    import oracle as O
+    from test_packed import _write_fasta
+    lens = np.full(24, 2_000_000 // 24, np.uint64)
+    flat, lens = sa.synth_reference(lens, sigma=6, seed=5)
+    reads = sa.synth_reads(flat, lens, 20_000, 101, 2, sigma=6, seed=6)
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    recs = [flat[offs[i]:offs[i + 1]] for i in range(len(lens))]
+    ref = tmp_path / "ref.fa"
+    _write_fasta(ref, recs, width=80)
+    q = tmp_path / "reads.fa"
+    _write_fasta(q, reads, width=80)
+    rc, _, err = run("index", ref)
+    assert rc == 0, err
+    one, many = tmp_path / "one.txt", tmp_path / "many.txt"
+    rc, so1, err = run("search", "-q", q, "-i", f"{ref}.idx", "-e", 2, "--emit-errors", "-o", one)
+    assert rc == 0, err
+    rc, so, err = run_env(_env(8), "search", "-q", q, "-i", f"{ref}.idx", "-e", 2, "--emit-errors", "-o", many,
+                          "--gpus", 8)
+    assert rc == 0, err
+    assert open(one).read() == open(many).read()
+    assert len(device_lines(so)) == 8
+    pats = sa.interleave_rc(reads, 6)
+    want, _ = O.Index.build(recs, 6, 16).search(pats, sa.search_scheme("h2-k2", 0, 2, 101), edit=True, nthreads=8)
+    assert np.array_equal(hits_as_rows(read_hits(many, 4)), hits_as_rows(want))
 
 
 @pytest.mark.gpu

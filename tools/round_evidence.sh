@@ -18,6 +18,6 @@ done
 cd /tmp && export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=8
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python3 "$R/bench.py" --no-cpu --no-count --no-verify --no-e2e --no-ref-path --steps 5 > "$OUT/trace/b.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
+    python3 "$R/bench.py" --no-device-resident --no-ingest --steps 5 > "$OUT/trace/b.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
 cd "$R" && python3 tools/timeline.py "$OUT/trace/run_kernel_trace.csv" 5 > "$OUT/c3_timeline.txt" && cp "$OUT/trace/run_kernel_stats.csv" "$OUT/c3_kernel_stats.csv" && rm -f "$OUT/trace/run_kernel_trace.csv"
 for f in "$OUT"/*_bench.json; do python3 -c "import json,sys; d=json.load(open('$f')); c=d['config']; print('$f', d['value'], d['ms_per_step'], (d.get('cpu_baseline') or {}).get('parity_on_sample'), c.get('origin_recall'), c.get('sa_probe_ok'), (c.get('pcie_inclusive') or {}).get('reads_per_s'))"; done

@@ -8,9 +8,9 @@ OUT=$(realpath -m "$1"); shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python3 "$R/bench.py" --no-cpu --no-count --no-verify --no-e2e --no-ref-path "$@" > "$OUT/trace.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
+    python3 "$R/bench.py" --no-device-resident --no-ingest "$@" > "$OUT/trace.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "kSearch|kSeed|kResolve|kLocate" -d "$OUT/pmc_fetch" -o run \
-    --output-format csv -- python3 "$R/bench.py" --no-cpu --no-count --no-verify --no-e2e --no-ref-path "$@" > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" || { echo "pmc failed"; exit 1; }
+    --output-format csv -- python3 "$R/bench.py" --no-device-resident --no-ingest "$@" > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err" || { echo "pmc failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "kGroup" -d "$OUT/calib" -o run \
     --output-format csv -- "$R/tools/gather_bench" > "$OUT/calib.txt" 2> "$OUT/calib.err" || { echo "calib failed"; exit 1; }
 echo done

@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$(realpath -m "$1"); shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--execution reference --no-cpu --no-verify --no-e2e --warmup 0 --steps 2"
+ARGS="--execution reference --no-cpu --no-verify --no-e2e --no-ingest --warmup 0 --steps 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 "$R/bench.py" $ARGS "$@" > "$OUT/trace.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "kSearch|kSeed|kLocate" -d "$OUT/pmc_fetch" -o run \
