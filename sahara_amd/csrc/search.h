@@ -96,6 +96,12 @@ struct TextArgs {
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
+    uint32_t planes;         // LDS planes per block: 3 (any symbol) or 2 (A C G T codes; window / pattern with
+                             // '$' or N diverted to excTasks for a three-plane launch)
+    uint4* excTasks;         // planes 2: tasks diverted (text position in x), excCap entries, *excCount of them
+    uint32_t excCap;
+    uint32_t* excCount;
+    uint32_t resolved;       // 1: the task records hold text positions (the diverted tasks), not SA rows
 };
 
 struct LocateArgs {
@@ -115,7 +121,9 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds, uint32_t planes = 3, const TextArgs* shapeOf = nullptr);
+// whether the two-plane kernel exists for this launch's shape
+bool textTwoPlanes(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);

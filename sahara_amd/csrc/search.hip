@@ -620,12 +620,13 @@ __device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
 __device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
 __device__ __forceinline__ Planes shr2(const Planes& p) { return {p.b0 >> 2, p.b1 >> 2, p.b2 >> 2}; }
 // 32 symbols from offset o of a lane's interleaved plane array (block i, plane
-// b at word (3i + b) * 256). o may be negative (down to -32): reads may run
-// past either end of the array into the lane's neighbouring LDS regions; callers
-// mask.
+// b at word (PL i + b) * 256; PL = 3 rank planes, or 2 code planes). o may be
+// negative (down to -32): reads may run past either end of the array into the
+// lane's neighbouring LDS regions; callers mask.
+template <int PL>
 __device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b) {
     const int i = o >> 5;
-    return __builtin_amdgcn_alignbit(A[(3 * i + 3 + (int)b) * 256], A[(3 * i + (int)b) * 256], (uint32_t)o & 31u);
+    return __builtin_amdgcn_alignbit(A[(PL * i + PL + (int)b) * 256], A[(PL * i + (int)b) * 256], (uint32_t)o & 31u);
 }
 // 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
 // reversed (back: bit j = symbol o - 1 - j). Symbols outside the array are
@@ -633,17 +634,31 @@ __device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b)
 // kTextTableMin words, the pattern's is the window): the window's are masked
 // by its `avail`, the pattern's lie beyond the pattern, which the chain logic
 // never uses (tests/text_model.py reads arbitrary symbols there).
+// (PL = 2: b2 is 0 on both sides, and the compiler drops it.)
+template <int PL>
 __device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
     const int off = (int)o - (fwd ? 0 : 32);
     Planes r;
-    uint32_t v[3];
+    uint32_t v[3] = {0u, 0u, 0u};
 #pragma unroll
-    for (uint32_t b = 0; b < 3; ++b) {
-        const uint32_t w = read32(A, off, b);
+    for (uint32_t b = 0; b < (uint32_t)PL; ++b) {
+        const uint32_t w = read32<PL>(A, off, b);
         v[b] = fwd ? w : __builtin_bitreverse32(w);
     }
     r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
     return r;
+}
+
+// Two code planes (PL = 2) for the symbols A C G T, from the three rank
+// planes: c0 = b0 (dna4: A 001, C 010, G 011, T 100) or b0 ^ b2 (dna5: T is
+// 101), c1 = b1 — four distinct codes, so symbol equality is code equality.
+// '$' (000) and dna5's N (100) have no code: a task whose window or pattern
+// holds one runs in the three-plane kernel instead (odd3 flags them).
+template <int SIGMA>
+__device__ __forceinline__ uint32_t code0(uint32_t b0, uint32_t b2) { return SIGMA == 6 ? b0 ^ b2 : b0; }
+template <int SIGMA>
+__device__ __forceinline__ uint32_t odd3(uint32_t b0, uint32_t b1, uint32_t b2) {
+    return ~(b0 | b1 | b2) | (SIGMA == 6 ? (b2 & ~b0) : 0u);
 }
 
 // Raw buffer resource over [base, base + bytes) (gfx9 dword3): loads at an
@@ -658,8 +673,12 @@ constexpr uint32_t kBufOOB = 0xFFFFFFFFu;  // offset of a load that returns 0
 // interleaved LDS slots (3 words per block): all loads of up to 8 blocks of
 // each array are issued before the first store, so a task start costs one
 // memory round trip for m <~ 190.
+// PL = 2: stored as code planes, and `odd` collects the symbols that have no
+// code (the window's '$' / N, the pattern's N).
+template <int SIGMA, int PL>
 __device__ __forceinline__ void copyBlocks(uint32_t* DA, __amdgpu_buffer_rsrc_t RA, uint32_t offA, uint32_t na,
-                                           uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB, uint32_t nb) {
+                                           uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB, uint32_t nb,
+                                           uint32_t& odd) {
     const uint32_t n = max(na, nb);
     for (uint32_t c = 0; c < n; c += 8) {
         decltype(__builtin_amdgcn_raw_buffer_load_b128(RA, 0u, 0, 0)) va[8], vb[8];
@@ -672,17 +691,33 @@ __device__ __forceinline__ void copyBlocks(uint32_t* DA, __amdgpu_buffer_rsrc_t 
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
             const uint32_t j = c + i;
-            if (j < na) { uint32_t* D = DA + 3u * j * 256u; D[0] = va[i][0]; D[256] = va[i][1]; D[512] = va[i][2]; }
-            if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[i][0]; D[256] = vb[i][1]; D[512] = vb[i][2]; }
+            if (PL == 3) {
+                if (j < na) { uint32_t* D = DA + 3u * j * 256u; D[0] = va[i][0]; D[256] = va[i][1]; D[512] = va[i][2]; }
+                if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[i][0]; D[256] = vb[i][1]; D[512] = vb[i][2]; }
+            } else {
+                if (j < na) {
+                    uint32_t* D = DA + 2u * j * 256u;
+                    D[0] = code0<SIGMA>(va[i][0], va[i][2]);
+                    D[256] = va[i][1];
+                    odd |= odd3<SIGMA>(va[i][0], va[i][1], va[i][2]);
+                }
+                if (j < nb) {
+                    uint32_t* D = DB + 2u * j * 256u;
+                    D[0] = code0<SIGMA>(vb[i][0], vb[i][2]);
+                    D[256] = vb[i][1];
+                    if (SIGMA == 6) odd |= vb[i][2] & ~vb[i][0];  // N (the padding past m is 000: not odd here)
+                }
+            }
         }
     }
 }
 
 // Same, but the window starts at any symbol: na blocks come from na + 1
 // source blocks funnel-shifted by sh symbols (na + 1 <= 8, nb <= 8).
+template <int SIGMA, int PL>
 __device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_rsrc_t RA, uint32_t offA, uint32_t sh,
                                                   uint32_t na, uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB,
-                                                  uint32_t nb) {
+                                                  uint32_t nb, uint32_t& odd) {
     decltype(__builtin_amdgcn_raw_buffer_load_b128(RA, 0u, 0, 0)) va[8], vb[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
@@ -692,14 +727,32 @@ __device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_
 #pragma unroll
     for (uint32_t j = 0; j < 7; ++j)
         if (j < na) {
-            uint32_t* D = DA + 3u * j * 256u;
-            D[0] = __builtin_amdgcn_alignbit(va[j + 1][0], va[j][0], sh);
-            D[256] = __builtin_amdgcn_alignbit(va[j + 1][1], va[j][1], sh);
-            D[512] = __builtin_amdgcn_alignbit(va[j + 1][2], va[j][2], sh);
+            const uint32_t b0 = __builtin_amdgcn_alignbit(va[j + 1][0], va[j][0], sh);
+            const uint32_t b1 = __builtin_amdgcn_alignbit(va[j + 1][1], va[j][1], sh);
+            const uint32_t b2 = __builtin_amdgcn_alignbit(va[j + 1][2], va[j][2], sh);
+            if (PL == 3) {
+                uint32_t* D = DA + 3u * j * 256u;
+                D[0] = b0; D[256] = b1; D[512] = b2;
+            } else {
+                uint32_t* D = DA + 2u * j * 256u;
+                D[0] = code0<SIGMA>(b0, b2);
+                D[256] = b1;
+                odd |= odd3<SIGMA>(b0, b1, b2);
+            }
         }
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j)
-        if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[j][0]; D[256] = vb[j][1]; D[512] = vb[j][2]; }
+        if (j < nb) {
+            if (PL == 3) {
+                uint32_t* D = DB + 3u * j * 256u;
+                D[0] = vb[j][0]; D[256] = vb[j][1]; D[512] = vb[j][2];
+            } else {
+                uint32_t* D = DB + 2u * j * 256u;
+                D[0] = code0<SIGMA>(vb[j][0], vb[j][2]);
+                D[256] = vb[j][1];
+                if (SIGMA == 6) odd |= vb[j][2] & ~vb[j][0];
+            }
+        }
 }
 
 // SHAPE fixes the window and pattern block counts at compile time, so that
@@ -713,7 +766,12 @@ struct TextShape { uint32_t win, pat; bool exact; };
 __host__ __device__ constexpr TextShape textShape(int shape) {
     return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
-template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
+// PL: LDS planes per block. 3 = the rank planes of device_index.h, any
+// symbol; 2 = the code planes of code0 (a quarter less LDS per lane and
+// fewer instructions per compare), with the tasks whose window or pattern
+// holds a '$' or N appended to a.excTasks (text positions resolved) for a
+// three-plane launch over them after this one.
+template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0, int PL = 3>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     uint2* SC = reinterpret_cast<uint2*>(lds);
@@ -727,8 +785,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     const uint32_t winBlocks = SHAPE ? kShape.win : a.winBlocks, patBlocks = SHAPE ? kShape.pat : a.patBlocks;
     const bool exactWindow = SHAPE ? kShape.exact : a.exactWindow != 0u;
     uint32_t* W = slot + threadIdx.x;
-    uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
-    uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
+    uint32_t* P = slot + (uint32_t)PL * winBlocks * 256u + threadIdx.x;
+    uint2* S = reinterpret_cast<uint2*>(slot + (uint32_t)PL * (winBlocks + patBlocks) * 256u) + threadIdx.x;
     auto stackGet = [&](uint32_t d) -> uint2 { return S[d * 256u]; };
     auto stackPut = [&](uint32_t d, const uint2& v) { S[d * 256u] = v; };
     const uint32_t winLen = winBlocks * 32u;
@@ -768,7 +826,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             nEnd = e;
             if (b + lane < e) nextRec = tasks[b + lane];
             haveNext = true;
-            nextRaw = true;
+            nextRaw = a.resolved == 0u;
         } else {
             qDone = true;
         }
@@ -809,7 +867,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                         nEnd = e;
                         if (b + lane < e) nextRec = tasks[b + lane];
                         haveNext = true;
-                        nextRaw = true;
+                        nextRaw = a.resolved == 0u;
                     }
                 }
                 if (qNext >= qEnd) continue;
@@ -821,6 +879,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t srcLane = (qNext - qBase + rank) & 63u;
             const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
                                        __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
+            bool divert = false;
             if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
                 // ---- start a task (x = its text position): copy the pattern
                 // and the text window its subtree can reach
@@ -833,15 +892,33 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
                 wb = x > left ? x - left : 0u;  // window start
+                uint32_t odd = 0u;
                 if (exactWindow) {              // at wb: m + 2k symbols fit in winBlocks blocks
-                    copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
-                                      pid * patBlocks * 16u, patBlocks);
+                    copyBlocksShifted<SIGMA, PL>(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
+                                                 pid * patBlocks * 16u, patBlocks, odd);
                 } else {                        // at the block start below wb (31 more symbols)
                     wb &= ~31u;
-                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
+                    copyBlocks<SIGMA, PL>(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u,
+                                          patBlocks, odd);
                 }
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
-                have = true;
+                divert = PL == 2 && odd != 0u;
+                have = !divert;
+            }
+            if (PL == 2) {
+                // tasks with a '$' or N go to the three-plane launch (wave-uniform:
+                // one atomic per wave and refill round that has any)
+                const uint64_t dm = __ballot(divert);
+                if (dm) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(a.excCount, (uint32_t)__popcll(dm));
+                    base = __shfl(base, 0);
+                    if (divert) {
+                        const uint32_t s = base + (uint32_t)__popcll(dm & ltMask);
+                        if (s < a.excCap) a.excTasks[s] = t;  // t.x is the text position already
+                        else atomicOr(a.flags, 8u);
+                    }
+                }
             }
             pending &= ~__ballot(mine);
             qNext += take;
@@ -878,8 +955,9 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 if (takes) {
                     const uint32_t* src = slot + dTid;
                     uint32_t* dst = slot + threadIdx.x;
-                    for (uint32_t k = 0; k < 3u * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
-                    const uint2 node = reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
+                    for (uint32_t k = 0; k < (uint32_t)PL * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
+                    const uint2 node =
+                        reinterpret_cast<const uint2*>(slot + (uint32_t)PL * (winBlocks + patBlocks) * 256u)[dTid];
                     cur = node;
                     pid = dPid;
                     wb = dWb;
@@ -932,14 +1010,15 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             // edge or before the text start reads as 0 and never matches.
             // One read each at a side-dependent offset (a left run ends at the
             // position and is bit-reversed), so the lanes of both sides share it
-            const Planes P16 = chain32(P, r0 ? q0 : q0 + 1u, r0);
-            const Planes T16 = chain32(W, r0 ? yo : xo, r0);
+            const Planes P16 = chain32<PL>(P, r0 ? q0 : q0 + 1u, r0);
+            const Planes T16 = chain32<PL>(W, r0 ? yo : xo, r0);
             const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
             const uint32_t VT = onesR(avail);
             const uint32_t E0 = eqm(P16, T16) & VT;                 // p_j == t_j     (M chain, S runs)
             const uint32_t ED = eqm(P16, shr1(T16)) & (VT >> 1);    // p_j == t_{j+1} (D runs)
             const uint32_t EI = eqm(shr1(P16), T16) & VT;           // p_{j+1} == t_j (I runs)
-            const uint32_t TZ = (T16.b0 | T16.b1 | T16.b2) & VT;    // t_j is a symbol (not '$' / edge)
+            // t_j is a symbol (not '$' / edge); a two-plane window holds no '$'
+            const uint32_t TZ = PL == 3 ? (T16.b0 | T16.b1 | T16.b2) & VT : VT;
 
             const bool atLeaf = live && pos == m;
             const bool node = live && pos < m;
@@ -1611,23 +1690,28 @@ int textShapeOf(const TextArgs& a) {
     return 0;
 }
 
-template <int SIGMA, int SHAPE>
+template <int SIGMA, int SHAPE, int PL>
 void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     if (edit) {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, SHAPE>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, SHAPE>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, SHAPE, PL>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, SHAPE, PL>), grid, dim3(256), lds, st, a);
     } else {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, SHAPE>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, SHAPE>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, SHAPE, PL>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, SHAPE, PL>), grid, dim3(256), lds, st, a);
     }
 }
 
+// two-plane kernels: the compile-time shapes (C2 / C3, C5); the generic
+// shape keeps three planes
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     const int shape = textShapeOf(a);
-    if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
-    else if (shape == 2) launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
-    else launchTextShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
+    const bool two = a.planes == 2;
+    if (shape == 1 && two) launchTextShaped<SIGMA, 1, 2>(a, edit, count, grid, lds, st);
+    else if (shape == 1) launchTextShaped<SIGMA, 1, 3>(a, edit, count, grid, lds, st);
+    else if (shape == 2 && two) launchTextShaped<SIGMA, 2, 2>(a, edit, count, grid, lds, st);
+    else if (shape == 2) launchTextShaped<SIGMA, 2, 3>(a, edit, count, grid, lds, st);
+    else launchTextShaped<SIGMA, 0, 3>(a, edit, count, grid, lds, st);
 }
 
 }  // namespace
@@ -1641,13 +1725,32 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     return b < 1 ? 1 : b;
 }
 
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
+// occupancy of the kernel a launch of this shape uses (shapeOf: its args;
+// nullptr: the generic kernel)
+template <int SIGMA, bool EDIT>
+const void* textKernelFor(uint32_t planes, int shape) {
+    if (shape == 1) return planes == 2 ? (const void*)kSearchText<SIGMA, EDIT, false, 1, 2>
+                                       : (const void*)kSearchText<SIGMA, EDIT, false, 1, 3>;
+    if (shape == 2) return planes == 2 ? (const void*)kSearchText<SIGMA, EDIT, false, 2, 2>
+                                       : (const void*)kSearchText<SIGMA, EDIT, false, 2, 3>;
+    return (const void*)kSearchText<SIGMA, EDIT, false, 0, 3>;
+}
+
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds, uint32_t planes, const TextArgs* shapeOf) {
+    const int shape = shapeOf ? textShapeOf(*shapeOf) : 0;
+    const void* f = sigma == 5 ? (edit ? textKernelFor<5, true>(planes, shape) : textKernelFor<5, false>(planes, shape))
+                               : (edit ? textKernelFor<6, true>(planes, shape) : textKernelFor<6, false>(planes, shape));
     int b = 0;
-    const void* f;
-    if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false> : (const void*)kSearchText<5, false, false>;
-    else            f = edit ? (const void*)kSearchText<6, true, false> : (const void*)kSearchText<6, false, false>;
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b;
+}
+
+bool textTwoPlanes(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow) {
+    TextArgs a{};
+    a.winBlocks = winBlocks;
+    a.patBlocks = patBlocks;
+    a.exactWindow = exactWindow ? 1u : 0u;
+    return textShapeOf(a) != 0;
 }
 
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,

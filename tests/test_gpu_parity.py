@@ -592,3 +592,35 @@ def test_long_and_huge_segments(gpu_device, monkeypatch, batch):
     for verify, locate_sa in MODES:
         gpu.set_mode(verify, locate_sa)
         assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k", [(100, 2), (250, 3), (100, 1)])
+def test_two_plane_text_phase_diverts_dollar_and_n(gpu_device, monkeypatch, m, k):
+    """The compile-time text shapes (m = 100: C2 / C3, m = 250 with k = 3: C5)
+    keep window and pattern in two code planes; a task whose window holds a
+    record delimiter '$' (short records), an N of the text or whose pattern
+    holds an N runs in a three-plane launch after the batch's. Same multiset
+    as the oracle and as three planes everywhere (SAHARA_TEXT_PLANES=3), in
+    one batch and many, with tasks diverted and tasks not."""
+    rng = np.random.default_rng(m + k)
+    lens = [int(x) for x in rng.integers(m // 2, 3 * m, 60)] + [20000, 9000]
+    recs = random_records(rng, lens, 6, with_n=True, repeats=True)
+    reads = mutate_reads(rng, recs, 300, m, k, 6)
+    reads[rng.random(reads.shape) < 0.002] = 4
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme("h2-k2", 0, k, m)
+    want, _ = O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)
+    want = hits_as_rows(want)
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    for batch in (None, "131"):
+        if batch:
+            monkeypatch.setenv("SAHARA_BATCH", batch)
+        monkeypatch.delenv("SAHARA_TEXT_PLANES", raising=False)
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), batch
+        st = gpu.stats()
+        assert st["text_exc_tasks"] > 0
+        assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme)), want), batch
+        monkeypatch.setenv("SAHARA_TEXT_PLANES", "3")
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), batch
+        assert gpu.stats()["text_exc_tasks"] == 0

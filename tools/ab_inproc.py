@@ -2,7 +2,10 @@
 (bench.py CONFIGS) is built and staged once, then each setting's timed steps
 run in alternating rounds (the library reads its variables per pass).
 
-usage: python tools/ab_inproc.py [--config c3] [--rounds 3] [--steps 10] [--count] NAME=VAR=VAL[,VAR=VAL] ...
+usage: python tools/ab_inproc.py [--config c3] [--rounds 3] [--steps 10] [--count] [--packed] NAME=VAR=VAL[,VAR=VAL] ...
+
+--packed times the bench's headline call instead (sahara_gpu_search_packed_compact
+from host reads two bits per symbol, hits into host memory).
 """
 import argparse
 import os
@@ -22,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--count", action="store_true", help="one instrumented run per setting (lane utilisation)")
+    ap.add_argument("--packed", action="store_true", help="time the packed-reads compact call (bench value)")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     import bench
@@ -34,6 +38,15 @@ def main():
     del flat
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
     idx.stage(sa.interleave_rc(reads, 6), scheme, edit=edit)
+    packed = sa.pack_reads(reads, 6) if a.packed else None
+
+    def one():
+        if packed is None:
+            return idx.run()
+        h = sa.search_packed_compact(idx, packed, scheme, edit=edit)
+        n = len(h)
+        h.close()
+        return n
     sets = []
     for s in a.settings:
         name, _, kv = s.partition("=")
@@ -46,11 +59,12 @@ def main():
             for v in known:
                 os.environ.pop(v, None)
             os.environ.update(env)
-            idx.run()
+            one()
+            one()
             t = time.perf_counter()
             tm = 0.0
             for _ in range(a.steps):
-                nh = idx.run()
+                nh = one()
                 tm += idx.stats()["text_ms"]
             el = time.perf_counter() - t
             res[name].append(nreads * a.steps / el)
