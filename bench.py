@@ -164,13 +164,17 @@ def main():
                                    substitutions=0 if edit else k, with_origin=True)
     pats = sa.interleave_rc(reads, sigma)
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
-    # the reads as `sahara search`'s FASTA ingest hands them over: two bits per
-    # symbol, N positions listed (sahara_read_fasta form 2)
-    packed = sa.pack_reads(reads, sigma)
-    log(f"rank {rank}: {nreads} reads simulated and packed ({time.time()-t:.1f}s), {scheme[0].shape[0]} searches")
+    log(f"rank {rank}: {nreads} reads simulated ({time.time()-t:.1f}s), {scheme[0].shape[0]} searches")
+    # the timed call's input: the reads as `sahara search`'s FASTA ingest hands
+    # them over — two bits per symbol in page-locked memory, N positions
+    # listed (sahara_read_fasta form 2) — from the reads written as a FASTA
+    # file and read back, the ingest timed in both forms (--no-ingest: the
+    # library's packer fills the same form)
     ingest = None
-    if not args.no_ingest and rank == 0:
-        ingest = time_ingest(sa, reads, packed, sigma)
+    if not args.no_ingest:
+        ingest, packed = time_ingest(sa, reads, sigma)
+    else:
+        packed = sa.pack_reads(reads, sigma, pinned=True)
     if args.execution == "reference":  # profiling aid: the timed steps are the reference's execution model
         args.no_count = args.no_ref_path = True
 
@@ -487,14 +491,15 @@ def main():
         dist.destroy_process_group()
 
 
-def time_ingest(sa, reads, packed, sigma):
+def time_ingest(sa, reads, sigma):
     """The FASTA ingest that the timed region starts after, timed in both
     forms on the same reads written as a FASTA file (80 columns, one header
     per read, in /dev/shm when there is one): FASTA -> one rank per byte (the
     reference's form, search.cpp:111-130) and FASTA -> two bits per symbol +
-    N list (what `sahara search` hands to sahara_gpu_search_packed_compact),
-    on the host threads the CLI uses. Checks that the 2-bit form equals the
-    timed call's input."""
+    N list in page-locked memory (what `sahara search` hands to
+    sahara_gpu_search_packed_compact), on the host threads the CLI uses.
+    Returns the timings and the 2-bit form as PackedReads (checked against
+    the library's packer over the reads)."""
     import tempfile
     d = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
     n, m = reads.shape
@@ -525,19 +530,20 @@ def time_ingest(sa, reads, packed, sigma):
         for form, name in ((1, "ranks"), (2, "two_bit")):
             best = None
             for _ in range(2):  # the second read is warm in the page cache
+                r = None
                 t = time.perf_counter()
                 r = sa.read_fasta(path, sigma, form=form, threads=threads)
                 dt = time.perf_counter() - t
                 best = dt if best is None else min(best, dt)
             out[f"{name}_s"] = round(best, 3)
             out[f"{name}_reads_per_s"] = round(n / best, 1)
-            if form == 2:
-                out["two_bit_equals_timed_input"] = bool(np.array_equal(r["data"], packed.codes) and
-                                                         np.array_equal(r["n_pos"], packed.n_pos))
-            del r
+        codes, pos, _ = sa.pack_2bit(reads, sigma)
+        out["two_bit_equals_packer"] = bool(np.array_equal(r["data"], codes) and
+                                            np.array_equal(r["n_pos"], pos.astype(np.uint64)))
+        del codes, pos
         log(f"ingest: {size/1e9:.2f} GB FASTA (written in {write_s:.1f}s): ranks {out['ranks_s']}s, "
             f"2-bit {out['two_bit_s']}s on {threads} threads")
-        return out
+        return out, sa.PackedReads(r["data"], n, m, r["n_pos"])
     finally:
         os.unlink(path)
 

@@ -246,6 +246,13 @@ int  sahara_gpu_placement(void* ctx, int* device, int* numa_node, int* n_cpus);
  * writes into memory that is already pinned and faulted in. */
 void sahara_gpu_free(void* p);
 void sahara_gpu_close(void* ctx);
+/* Page-locked host memory any context's DMA can read (NULL on failure, see
+ * sahara_gpu_last_error). Packed reads kept in it (sahara_read_fasta's form 2
+ * is) go up straight from there in sahara_gpu_search_packed[_compact],
+ * without being copied through the library's staging ring: a quarter of the
+ * host memory traffic of a rank-per-byte call. */
+void* sahara_host_alloc(size_t bytes);
+void sahara_host_free(void* p);
 
 /* --- search schemes (replaces generator::all / expand / limitToHamming,
  * search.cpp:174-212, :226) --- */
@@ -278,7 +285,7 @@ int  sahara_scheme_counts(const uint32_t* l, const uint32_t* u, uint32_t n_searc
 /* A FASTA file on `threads` host threads (0: OMP_NUM_THREADS, else all), in
  * form 1 (one rank per byte of data, 255 = no rank of the alphabet) or form 2
  * (two bits per symbol as sahara_gpu_search_packed takes them, N positions in
- * n_pos). Records: symbols [offs[i], offs[i+1]). bad != 0: the first character
+ * n_pos; data in page-locked memory, so the search calls DMA it directly). Records: symbols [offs[i], offs[i+1]). bad != 0: the first character
  * that is no rank of the alphabet is character bad_pos of record bad_record
  * (header bad_id), bad_char. Release with sahara_free_fasta. */
 typedef struct sahara_fasta {

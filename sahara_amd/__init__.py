@@ -117,6 +117,8 @@ EXPORTED = {
                                                    C.c_int, C.POINTER(HitBlocks)]),
     "sahara_read_fasta": (C.c_int, [C.c_char_p, C.c_uint32, C.c_int, C.c_uint32, C.POINTER(FastaOut)]),
     "sahara_free_fasta": (None, [C.POINTER(FastaOut)]),
+    "sahara_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "sahara_host_free": (None, [C.c_void_p]),
     "sahara_gpu_search_best": (C.c_int, [C.c_void_p, u8p, C.c_uint64, C.c_uint32, u32p, u32p, u32p,
                                          u32p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_uint64)]),
@@ -514,11 +516,35 @@ class PackedReads:
         return PackedReads(self.codes, r1 - r0, self.length, self.n_pos, self.sym0 + r0 * self.length)
 
 
-def pack_reads(reads, sigma=6):
+class _Pinned:
+    """Owner of page-locked host memory (sahara_host_alloc), freed with the
+    last array over it."""
+
+    def __init__(self, nbytes):
+        self.p = lib().sahara_host_alloc(max(1, nbytes))
+        if not self.p:
+            raise SaharaError(lib().sahara_gpu_last_error().decode())
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.p, False), "version": 3}
+
+    def __del__(self):
+        try:
+            lib().sahara_host_free(self.p)
+        except Exception:
+            pass
+
+
+def host_array(nbytes):
+    """uint8 array of nbytes in page-locked host memory (sahara_host_alloc):
+    the packed search calls DMA reads kept there without copying them."""
+    return np.asarray(_Pinned(int(nbytes)))
+
+
+def pack_reads(reads, sigma=6, pinned=False):
     """(n_reads, len) ranks -> PackedReads (the library's host packer,
-    sahara_pack_2bit; raises on a byte that is no rank of the alphabet)."""
+    sahara_pack_2bit; raises on a byte that is no rank of the alphabet);
+    pinned: the codes in page-locked memory (host_array)."""
     r = np.ascontiguousarray(reads, dtype=np.uint8)
-    codes, pos, bad = pack_2bit(r, sigma)
+    codes, pos, bad = pack_2bit(r, sigma, out=host_array((r.size + 3) // 4) if pinned else None)
     if bad:
         raise SaharaError("reads hold a byte that is no rank of the alphabet")
     return PackedReads(codes, r.shape[0], r.shape[1], pos.astype(np.uint64))
@@ -558,17 +584,37 @@ def read_fasta(path, sigma=6, form=1, threads=0):
     bits per symbol), `offs` (record i = symbols [offs[i], offs[i+1])),
     `n_pos` (form 2: N positions) and `bad` (None, or (record, position,
     character, header) of the first invalid character)."""
-    f = FastaOut()
+    own = _FastaOwner()
+    f = own.f
     _check(lib().sahara_read_fasta(os.fsencode(path), sigma, form, threads, C.byref(f)))
-    try:
-        nb = f.n_symbols if form == 1 else (f.n_symbols + 3) // 4
+    nb = f.n_symbols if form == 1 else (f.n_symbols + 3) // 4
+    # form 2: a zero-copy view of the library's page-locked buffer (kept alive
+    # by the array); form 1 and the small arrays: copies
+    if nb and form == 2:
+        data = np.asarray(_FastaData(own, C.cast(f.data, C.c_void_p).value, nb))
+    else:
         data = np.ctypeslib.as_array(f.data, shape=(nb,)).copy() if nb else np.zeros(0, np.uint8)
-        offs = np.ctypeslib.as_array(f.offs, shape=(f.n_records + 1,)).copy() if f.n_records else np.zeros(0, np.uint64)
-        npos = np.ctypeslib.as_array(f.n_pos, shape=(f.n_count,)).copy() if f.n_count else np.zeros(0, np.uint64)
-        bad = (int(f.bad_record), int(f.bad_pos), chr(f.bad_char), f.bad_id.decode()) if f.bad else None
-        return {"data": data, "offs": offs, "n_pos": npos, "n_symbols": int(f.n_symbols), "bad": bad}
-    finally:
-        lib().sahara_free_fasta(C.byref(f))
+    offs = np.ctypeslib.as_array(f.offs, shape=(f.n_records + 1,)).copy() if f.n_records else np.zeros(0, np.uint64)
+    npos = np.ctypeslib.as_array(f.n_pos, shape=(f.n_count,)).copy() if f.n_count else np.zeros(0, np.uint64)
+    bad = (int(f.bad_record), int(f.bad_pos), chr(f.bad_char), f.bad_id.decode()) if f.bad else None
+    return {"data": data, "offs": offs, "n_pos": npos, "n_symbols": int(f.n_symbols), "bad": bad}
+
+
+class _FastaOwner:
+    def __init__(self):
+        self.f = FastaOut()
+
+    def __del__(self):
+        try:
+            lib().sahara_free_fasta(C.byref(self.f))
+        except Exception:
+            pass
+
+
+class _FastaData:
+    def __init__(self, owner, addr, n):
+        self._owner = owner
+        self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (addr, False), "version": 3}
 
 
 def search_best(index, queries, schemes, max_hits=0):
@@ -681,12 +727,15 @@ def synth_reads(flat, rec_lens, n_reads, length, errors, sigma=6, seed=7, with_o
     return (out, origin) if with_origin else out
 
 
-def pack_2bit(ranks, sigma=6, scalar=False):
+def pack_2bit(ranks, sigma=6, scalar=False, out=None):
     """Host half of the streamed upload at two bits per symbol (staging.cpp
     pack2Avx512 / pack2Avx2 / pack2Scalar): (packed bytes, N positions,
-    bad-rank flag). scalar: False = widest SIMD, True = scalar, 2 = AVX2 at most."""
+    bad-rank flag). scalar: False = widest SIMD, True = scalar, 2 = AVX2 at most.
+    out: a uint8 array of (n + 3) // 4 bytes to pack into."""
     r = np.ascontiguousarray(ranks, dtype=np.uint8).ravel()
-    out = np.zeros((r.size + 3) // 4, np.uint8)
+    if out is None:
+        out = np.zeros((r.size + 3) // 4, np.uint8)
+    assert out.dtype == np.uint8 and out.size == (r.size + 3) // 4 and out.flags.c_contiguous
     cnt = C.c_uint64(0)
     rc = lib().sahara_pack_2bit(_p(r, u8p), r.size, sigma, int(scalar), _p(out, u8p), None, 0, C.byref(cnt))
     if rc < 0:

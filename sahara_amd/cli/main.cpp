@@ -378,16 +378,22 @@ int cmdSearch(int argc, char** argv) {
     // interleave and --limit_queries cut happen on the device
     // (sahara_gpu_search_packed[_compact]), so only the packed reads cross
     // PCIe. Query numbers in messages count the interleaved list.
+    // (the library's ingest, sahara_read_fasta: the 2-bit form lands in
+    // page-locked memory, which the search calls DMA without a copy)
     const unsigned nt = hostThreads();
     const bool packedIn = !besthits;
-    FastaData Q = parseFastaParallel(query.value, (uint32_t)sigma, nt, 8u << 20,
-                                     packedIn ? FastaForm::kCodes2 : FastaForm::kRanks);
+    struct Queries {
+        sahara_fasta f{};
+        ~Queries() { sahara_free_fasta(&f); }
+        size_t records() const { return f.n_records; }
+    } Q;
+    check(sahara_read_fasta(query.value.c_str(), (uint32_t)sigma, packedIn ? 2 : 1, nt, &Q.f), "reading queries");
     const size_t nrec = Q.records();
     const size_t per = noRev.given ? 1 : 2;  // patterns per read
-    if (Q.bad) {
-        const unsigned char ch = Q.badChar;
-        throw CliError(fmtStr("query '%s' (%zu) has invalid character at position %ld '%c'(%x)", Q.badId.c_str(),
-                              per * Q.badRecord + 1, (long)Q.badPos, ch, ch));
+    if (Q.f.bad) {
+        const unsigned char ch = (unsigned char)Q.f.bad_char;
+        throw CliError(fmtStr("query '%s' (%zu) has invalid character at position %ld '%c'(%x)", Q.f.bad_id,
+                              per * (size_t)Q.f.bad_record + 1, (long)Q.f.bad_pos, ch, ch));
     }
     size_t nq = per * nrec;  // the interleaved query list, cut by --limit_queries
     if (limit.given) nq = std::min<size_t>(toU64(limit.value, "--limit_queries"), nq);
@@ -457,13 +463,14 @@ int cmdSearch(int argc, char** argv) {
         if (!known)
             throw CliError("unknown search scheme generetaror \"" + gen.value + "\", valid generators are: " + all);
     }
-    const uint32_t len = (uint32_t)(Q.offs[1] - Q.offs[0]);
+    const uint64_t* qoffs = Q.f.offs;
+    const uint32_t len = (uint32_t)(qoffs[1] - qoffs[0]);
     for (size_t r = 0; r < nreads; ++r)
-        if (Q.offs[r + 1] - Q.offs[r] != len)
+        if (qoffs[r + 1] - qoffs[r] != len)
             throw CliError(fmtStr("query %zu has length %zu, but all queries must have the length of the first "
                                   "(%u): sahara expands one search scheme for queries[0].size()",
-                                  per * r, (size_t)(Q.offs[r + 1] - Q.offs[r]), len));
-    const uint8_t* reads = Q.ranks.data();  // nreads x len, back to back (packedIn: 2-bit codes)
+                                  per * r, (size_t)(qoffs[r + 1] - qoffs[r]), len));
+    const uint8_t* reads = Q.f.data;  // nreads x len, back to back (packedIn: 2-bit codes)
 
     std::vector<Scheme> schemes;  // all: [0..k]; besthits: one per exact error count j
     // --dynamic_generator: part sizes by weighted node count (search.cpp:192-195, 202-205)
@@ -532,17 +539,18 @@ int cmdSearch(int argc, char** argv) {
                 const uint32_t cap = (uint32_t)std::max(0L, mh);
                 HitPart part;
                 // the shard's reads: stream symbols [r0 * len, r1 * len) of the packed codes
-                const uint64_t* npos = Q.nPos.empty() ? nullptr : Q.nPos.data();
+                const uint64_t* npos = Q.f.n_count ? Q.f.n_pos : nullptr;
+                const uint64_t ncount = Q.f.n_count;
                 if (!besthits && compactOut) {  // 8-B records straight into host memory, decoded by writeHits
                     const Scheme& s = schemes[0];
-                    rc = sahara_gpu_search_packed_compact(ctx[g], reads, (uint64_t)r0 * len, npos, Q.nPos.size(),
+                    rc = sahara_gpu_search_packed_compact(ctx[g], reads, (uint64_t)r0 * len, npos, ncount,
                                                           r1 - r0, len, noRev.given ? 0 : 1, q1 - q0, s.pi.data(),
                                                           s.l.data(), s.u.data(), s.n, edit ? 1 : 0, &part.blocks);
                     part.compact = rc == 0;
                     nh = part.blocks.n_hits;
                 } else if (!besthits) {
                     const Scheme& s = schemes[0];
-                    rc = sahara_gpu_search_packed(ctx[g], reads, (uint64_t)r0 * len, npos, Q.nPos.size(), r1 - r0, len,
+                    rc = sahara_gpu_search_packed(ctx[g], reads, (uint64_t)r0 * len, npos, ncount, r1 - r0, len,
                                                   noRev.given ? 0 : 1, q1 - q0, s.pi.data(), s.l.data(), s.u.data(),
                                                   s.n, edit ? 1 : 0, cap, &hits, &nh);
                 } else {  // search_best takes the interleaved patterns

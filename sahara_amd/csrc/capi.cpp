@@ -1037,6 +1037,20 @@ int sahara_gpu_search_best(void* ctx, const uint8_t* ranks, uint64_t n_patterns,
 
 void sahara_gpu_free(void* p) { freeHits(p); }
 
+void* sahara_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        g_err = "could not allocate " + std::to_string(bytes) + " bytes of page-locked host memory";
+        return nullptr;
+    }
+    return p;
+}
+
+void sahara_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 void sahara_gpu_close(void* ctx) {
     if (!ctx) return;
     Ctx* c = static_cast<Ctx*>(ctx);

@@ -417,6 +417,7 @@ struct Ctx {
         // reads are on the device (nList, relative to each chunk's first
         // whole byte), chunk j's from entry nFirst[j]
         bool prepacked = false;
+        bool srcPinned = false;        // prepacked codes in page-locked memory: DMA'd from there, no copy
         uint64_t sym0 = 0;
         std::vector<uint64_t> nFirst;
     } up;

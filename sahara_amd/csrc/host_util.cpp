@@ -6,6 +6,8 @@
 #include <fstream>
 #include <thread>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/sahara_hip.h"
 #include "device_index.h"
 #include "fasta.h"
@@ -280,7 +282,18 @@ int sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threa
         const unsigned nt = threads ? threads : sahara_io::hostThreads();
         sahara_io::FastaData D = sahara_io::parseFastaParallel(
             path, sigma, nt, 8u << 20, form == 2 ? sahara_io::FastaForm::kCodes2 : sahara_io::FastaForm::kRanks);
-        out->data = copyOut(D.ranks);
+        if (form == 2) {  // page-locked: the packed search calls DMA it as it is
+            void* p = nullptr;
+            if (hipHostMalloc(&p, std::max<size_t>(D.ranks.size(), 1), hipHostMallocPortable) != hipSuccess || !p) {
+                (void)hipGetLastError();
+                out->data = copyOut(D.ranks);  // pageable: the calls copy it through their staging ring
+            } else {
+                out->data = static_cast<uint8_t*>(p);
+                if (!D.ranks.empty()) std::memcpy(p, D.ranks.data(), D.ranks.size());
+            }
+        } else {
+            out->data = copyOut(D.ranks);
+        }
         out->offs = copyOut(D.offs);
         out->n_pos = copyOut(D.nPos);
         out->n_symbols = D.symbols;
@@ -303,7 +316,14 @@ int sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threa
 
 void sahara_free_fasta(sahara_fasta* f) {
     if (!f) return;
-    std::free(f->data);
+    hipPointerAttribute_t at{};
+    if (f->data && hipPointerGetAttributes(&at, f->data) == hipSuccess && at.type == hipMemoryTypeHost &&
+        at.hostPointer) {
+        (void)hipHostFree(f->data);
+    } else {
+        (void)hipGetLastError();
+        std::free(f->data);
+    }
     std::free(f->offs);
     std::free(f->n_pos);
     std::free(f->bad_id);

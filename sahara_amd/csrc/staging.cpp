@@ -422,7 +422,7 @@ static void submitPack(Ctx* c, uint64_t j) {
     std::vector<std::function<void()>> fs;
     if (U.prepacked) {  // codes as given: the chunk's bytes of the caller's buffer, copied in pieces
         const uint64_t B0 = (U.sym0 + s0) / 4, nb = (U.sym0 + s0 + n + 3) / 4 - B0, pb = pieceSyms / 4;
-        J.pieces = (nb + pb - 1) / pb;
+        J.pieces = U.srcPinned ? 0 : (nb + pb - 1) / pb;  // pinned: the DMA reads the caller's buffer
         J.group.begin(J.pieces);
         const uint8_t* src = U.src + B0;
         fs.reserve(J.pieces);
@@ -522,7 +522,7 @@ void uploadChunk(Ctx* c, hipStream_t kst) {
         so = (uint32_t)(S0 & 3u);
         nExc = U.nFirst[j + 1] - U.nFirst[j];
         excDev = c->nList.ptr + U.nFirst[j];
-        uploadCopy(c, c->nibPats.ptr + b0, out, (S1 + 3) / 4 - S0 / 4);
+        uploadCopy(c, c->nibPats.ptr + b0, U.srcPinned ? U.src + S0 / 4 : out, (S1 + 3) / 4 - S0 / 4);
         c->mark("dma enqueued", j);
     } else if (bits == 2) {
         if (U.submitted <= j) submitPack(c, j);  // (U.submitted == j: chunks post in order)
@@ -660,6 +660,18 @@ static void stagePackedN(Ctx* c, const PackedReads& P, uint64_t rows, uint32_t m
     Ctx::Upload& U = c->up;
     U.prepacked = true;
     U.sym0 = P.sym0;
+    // codes in page-locked memory (sahara_host_alloc, sahara_read_fasta's
+    // form 2, or the caller's own) go up by DMA straight from there
+    auto pinned = [](const void* p) {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return at.type == hipMemoryTypeHost && at.hostPointer != nullptr;
+    };
+    const uint64_t b0 = P.sym0 / 4, b1 = (P.sym0 + rows * m + 3) / 4;
+    U.srcPinned = pinned(U.src + b0) && pinned(U.src + b1 - 1);
     const uint64_t lo = P.sym0, hi = P.sym0 + rows * m;
     const uint64_t* all = P.nCount ? P.nPos : nullptr;
     const uint64_t* b = all ? std::lower_bound(all, all + P.nCount, lo) : nullptr;

@@ -38,7 +38,7 @@ def main():
     del flat
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
     idx.stage(sa.interleave_rc(reads, 6), scheme, edit=edit)
-    packed = sa.pack_reads(reads, 6) if a.packed else None
+    packed = sa.pack_reads(reads, 6, pinned=True) if a.packed else None
 
     def one():
         if packed is None:
