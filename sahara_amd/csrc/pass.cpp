@@ -238,9 +238,32 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
     }
-    // batch boundaries: equal batches of <= maxBatch patterns
+    // batch boundaries: equal batches of <= maxBatch patterns, or (pipelined,
+    // SAHARA_RAMP / SAHARA_RAMP_END: lists of pattern counts, ',' or ':') given
+    // first and last batches around equal middle ones
     std::vector<uint64_t> bstart{0};
-    for (uint64_t i = 1; i <= batchesHere; ++i) bstart.push_back(c->npat * i / batchesHere);
+    {
+        auto list = [](const char* e) {
+            std::vector<uint64_t> v;
+            for (const char* p = e; p && *p;) {
+                char* end = nullptr;
+                const unsigned long long x = std::strtoull(p, &end, 10);
+                if (end == p) break;
+                if (x) v.push_back(x);
+                p = (*end == ',' || *end == ':') ? end + 1 : end;
+            }
+            return v;
+        };
+        std::vector<uint64_t> head = list(std::getenv("SAHARA_RAMP")), tail = list(std::getenv("SAHARA_RAMP_END"));
+        uint64_t edges = 0;
+        for (auto& x : head) edges += x = std::min(x, maxBatch);
+        for (auto& x : tail) edges += x = std::min(x, maxBatch);
+        if (serial || c->npat < edges + maxBatch) head.clear(), tail.clear(), edges = 0;
+        for (uint64_t x : head) bstart.push_back(bstart.back() + x);
+        const uint64_t mid = c->npat - edges, q0 = bstart.back(), nmid = (mid + maxBatch - 1) / maxBatch;
+        for (uint64_t i = 1; i <= nmid; ++i) bstart.push_back(q0 + mid * i / nmid);
+        for (uint64_t x : tail) bstart.push_back(bstart.back() + x);
+    }
     const uint64_t nbatch = bstart.size() - 1;
     // per batch, 16 words of pinned host memory: the slot's counters (0-6),
     // the locate flags (7), the row total (8-9), the long / huge segment
