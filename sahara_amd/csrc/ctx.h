@@ -329,6 +329,7 @@ struct Ctx {
     uint64_t npat = 0;
     uint32_t m = 0, patWords = 0, patBlocks = 0;
     DevBuf<uint32_t> scheme, cover, kmerStart;        // FM scheme table; text table (textTable)
+    DevBuf<uint32_t> seedRun;                         // per search: forced run after the k-mer seed (kSeedItems)
     uint32_t nsearch = 0;
     uint32_t maxErr = 0;
     bool edit = true;

@@ -361,6 +361,17 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sd.taskCount = sl.small.ptr + 4;
         sd.flags = sl.small.ptr + 2;
         sd.counters = count ? c->counters.ptr : nullptr;
+        // single-row seeds checked against the text (SAHARA_SEED_CHECK=0: not)
+        const char* checkEnv = std::getenv("SAHARA_SEED_CHECK");
+        if (sd.toText && sd.kmer && !(checkEnv && std::atoi(checkEnv) == 0)) {
+            sd.seedRun = c->seedRun.ptr;
+            sd.sa = c->I.saFull.ptr;
+            sd.text3 = c->I.text3.ptr;
+            sd.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
+            sd.pats3 = c->pats3.ptr + q0 * c->patBlocks;
+            sd.pats3Bytes = (uint32_t)std::min<uint64_t>((c->npat - q0) * c->patBlocks * 16, 0xFFFFFF00ull);
+            sd.patBlocks = c->patBlocks;
+        }
         a.seeds = sl.seeds.ptr;
         a.seedItem = sl.seedItem.ptr;
         a.seedCount = sl.small.ptr + 6;
@@ -425,7 +436,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.excTasks = sl.exc.ptr;
             t.excCap = c->taskCap;
             t.excCount = sl.small.ptr + 7;
-            t.resolved = 0;
             if (split0) {
                 // the first batch's seed tasks while its FM phase runs, then the
                 // tasks the FM phase appended after them
@@ -449,7 +459,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                 e.taskCount = sl.small.ptr + 7;
                 e.taskBegin = nullptr;
                 e.work = sl.queues.ptr + 768;
-                e.resolved = 1;
                 e.excTasks = nullptr;
                 e.excCap = 0;
                 launchText(e, sigma, c->edit, count, (uint32_t)c->numCU, textLds3, sB);

@@ -60,7 +60,23 @@ struct SeedArgs {
     uint32_t* taskCount;
     uint32_t* flags;            // 8: task buffer too small
     unsigned long long* counters;  // count mode: text tasks (+6), else nullptr
+    // Single-row seeds: the forced matches that follow depth kmerK (u == 0
+    // there), checked against the text before the seed becomes a task.
+    // seedRun[s] = R | right << 8 (R <= 32 positions in one direction; 0: no
+    // check); a seed that passes goes to the text phase with its text position
+    // (kTaskResolved), one that fails ends here.
+    const uint32_t* seedRun;    // nullptr: no check
+    const uint32_t* sa;         // full SA
+    const uint4* text3;         // text, 3-bit-plane blocks
+    uint32_t text3Bytes;
+    const uint4* pats3;         // the batch's patterns, 3-bit-plane blocks
+    uint32_t pats3Bytes;
+    uint32_t patBlocks;
 };
+
+// Text task record flag (y, the matched length's high bit): x holds the text
+// position already, not an SA row.
+constexpr uint32_t kTaskResolved = 1u << 31;
 
 // Text phase LDS: the scheme table comes first and takes at least one block of
 // lane words (3 planes x 256 lanes), so that a read of a lane's window block -1
@@ -101,7 +117,6 @@ struct TextArgs {
     uint4* excTasks;         // planes 2: tasks diverted (text position in x), excCap entries, *excCount of them
     uint32_t excCap;
     uint32_t* excCount;
-    uint32_t resolved;       // 1: the task records hold text positions (the diverted tasks), not SA rows
 };
 
 struct LocateArgs {

@@ -223,6 +223,80 @@ __device__ __forceinline__ uint32_t childMeta(uint32_t pos, uint32_t e, uint32_t
     return npos | (ne << 16) | (nl << 20) | (nr << 22) | (nd << 25);
 }
 
+// ---- runs of symbols as bit masks: bit j = chain symbol j. Symbols come as
+// 3 bit planes (device_index.h), so the per-symbol equality of 32 symbols is
+// three word xors; the chain logic uses the low 16 bits.
+constexpr uint32_t kRun = 32;              // symbols per micro-step run (a forced node's match budget)
+constexpr uint32_t kRunMask = 0xFFFFFFFFu;
+// chain positions per micro-step of a node whose error children are forced:
+// the forced-run check of an error child at chain node i reads symbols
+// i .. i + 7 of the 32 (kChain + 7 <= kRun)
+constexpr uint32_t kChain = 25;
+__device__ __forceinline__ uint32_t onesR(uint32_t n) {  // symbols [0, n), capped at kRun
+    return n >= kRun ? kRunMask : (1u << n) - 1u;
+}
+__device__ __forceinline__ uint32_t beyondR(uint32_t n) { return kRunMask & ~onesR(n); }  // symbols >= n
+// bit j set iff bits j .. j+6 are all set (7 consecutive matches from j)
+__device__ __forceinline__ uint32_t run7(uint32_t m) {
+    const uint32_t m2 = m & (m >> 1), m4 = m2 & (m2 >> 2);
+    return m4 & (m2 >> 4) & (m >> 6);
+}
+struct Planes { uint32_t b0, b1, b2; };
+__device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
+    return ~((p.b0 ^ t.b0) | (p.b1 ^ t.b1) | (p.b2 ^ t.b2));
+}
+__device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
+__device__ __forceinline__ Planes shr2(const Planes& p) { return {p.b0 >> 2, p.b1 >> 2, p.b2 >> 2}; }
+// 32 symbols from offset o of a lane's interleaved plane array (block i, plane
+// b at word (PL i + b) * 256; PL = 3 rank planes, or 2 code planes). o may be
+// negative (down to -32): reads may run past either end of the array into the
+// lane's neighbouring LDS regions; callers mask.
+template <int PL>
+__device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b) {
+    const int i = o >> 5;
+    return __builtin_amdgcn_alignbit(A[(PL * i + PL + (int)b) * 256], A[(PL * i + (int)b) * 256], (uint32_t)o & 31u);
+}
+// 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
+// reversed (back: bit j = symbol o - 1 - j). Symbols outside the array are
+// whatever the LDS holds there (the window's block -1 is the table region,
+// kTextTableMin words, the pattern's is the window): the window's are masked
+// by its `avail`, the pattern's lie beyond the pattern, which the chain logic
+// never uses (tests/text_model.py reads arbitrary symbols there).
+// (PL = 2: b2 is 0 on both sides, and the compiler drops it.)
+template <int PL>
+__device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
+    const int off = (int)o - (fwd ? 0 : 32);
+    Planes r;
+    uint32_t v[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t b = 0; b < (uint32_t)PL; ++b) {
+        const uint32_t w = read32<PL>(A, off, b);
+        v[b] = fwd ? w : __builtin_bitreverse32(w);
+    }
+    r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
+    return r;
+}
+
+// Two code planes (PL = 2) for the symbols A C G T, from the three rank
+// planes: c0 = b0 (dna4: A 001, C 010, G 011, T 100) or b0 ^ b2 (dna5: T is
+// 101), c1 = b1 — four distinct codes, so symbol equality is code equality.
+// '$' (000) and dna5's N (100) have no code: a task whose window or pattern
+// holds one runs in the three-plane kernel instead (odd3 flags them).
+template <int SIGMA>
+__device__ __forceinline__ uint32_t code0(uint32_t b0, uint32_t b2) { return SIGMA == 6 ? b0 ^ b2 : b0; }
+template <int SIGMA>
+__device__ __forceinline__ uint32_t odd3(uint32_t b0, uint32_t b1, uint32_t b2) {
+    return ~(b0 | b1 | b2) | (SIGMA == 6 ? (b2 & ~b0) : 0u);
+}
+
+// Raw buffer resource over [base, base + bytes) (gfx9 dword3): loads at an
+// offset past the end return 0 without a memory request, so guarded loads
+// need no branch (and no wait at a branch join).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bufferOf(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+constexpr uint32_t kBufOOB = 0xFFFFFFFFu;  // offset of a load that returns 0
+
 // ========================================================= seeds ====
 // One thread per work item (pattern, search): its starting cursor. A search
 // whose first kmerK steps admit no error starts at depth kmerK from the k-mer
@@ -294,14 +368,71 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t ltMask = (1ull << lane) - 1ull;
     uint64_t cTasks = 0;
+    const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
+    const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
     for (uint32_t base = blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
         uint4 cur[4];
         bool keep[4], task[4];
+        uint32_t resolved[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k]);
             task[k] = keep[k] && a.toText && cur[k].z == 1u && (cur[k].w & 0xFFFFu) < a.m;
             keep[k] = keep[k] && !task[k];
+        }
+        if (a.seedRun) {
+            // single-row seeds: their forced run checked against the text (the
+            // text phase's first micro-step, done where the SA and text reads of
+            // four items per lane are in flight together). A seed of a random
+            // occurrence — most of the reverse complements' — fails within a few
+            // symbols and ends here instead of costing the text phase a task start
+            uint32_t run[4], pos[4], sIdx[4], pid[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t item = base + k * 256u + threadIdx.x;
+                pid[k] = item / a.nsearch;
+                sIdx[k] = item - pid[k] * a.nsearch;
+                run[k] = task[k] ? a.seedRun[sIdx[k]] : 0u;
+                pos[k] = (run[k] & 0xFFu) ? a.sa[cur[k].x] : 0u;
+            }
+            uint4 tb[4][2], pb[4][2];
+            uint32_t tsh[4], psh[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t R = run[k] & 0xFFu;
+                const bool right = (run[k] >> 8) & 1u;
+                const uint32_t ks = R ? a.kmerStart[sIdx[k]] : 0u;
+                // text symbols [tq, tq + R) against pattern symbols [pq, pq + R)
+                const uint32_t tq = right ? pos[k] + a.kmerK : pos[k] - R, pq = right ? ks + a.kmerK : ks - R;
+                const bool live = R && (right || pos[k] >= R);
+                if (R && !live) task[k] = false;  // would run left of the text's first symbol
+                tsh[k] = tq & 31u;
+                psh[k] = pq & 31u;
+                const uint32_t to = live ? (tq >> 5) * 16u : kBufOOB;
+                const uint32_t po = live ? (pid[k] * a.patBlocks + (pq >> 5)) * 16u : kBufOOB;
+                tb[k][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(textBuf, to, 0, 0));
+                tb[k][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(textBuf, live ? to + 16u : kBufOOB, 0, 0));
+                pb[k][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(patBuf, po, 0, 0));
+                pb[k][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(patBuf, live ? po + 16u : kBufOOB, 0, 0));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t R = run[k] & 0xFFu;
+                if (!task[k] || !R) continue;
+                const Planes T = {__builtin_amdgcn_alignbit(tb[k][1].x, tb[k][0].x, tsh[k]),
+                                  __builtin_amdgcn_alignbit(tb[k][1].y, tb[k][0].y, tsh[k]),
+                                  __builtin_amdgcn_alignbit(tb[k][1].z, tb[k][0].z, tsh[k])};
+                const Planes Pp = {__builtin_amdgcn_alignbit(pb[k][1].x, pb[k][0].x, psh[k]),
+                                   __builtin_amdgcn_alignbit(pb[k][1].y, pb[k][0].y, psh[k]),
+                                   __builtin_amdgcn_alignbit(pb[k][1].z, pb[k][0].z, psh[k])};
+                const uint32_t want = onesR(R);
+                if ((eqm(Pp, T) & want) != want) {
+                    task[k] = false;  // the forced run breaks: the seed's subtree is empty
+                } else {
+                    cur[k].x = pos[k];  // the text position: the text phase needs no SA read
+                    resolved[k] = kTaskResolved;
+                }
+            }
         }
         uint64_t m[4], mt[4];
         uint32_t wsum = 0, wtask = 0;
@@ -334,7 +465,8 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
                 const uint32_t at = tslot + (uint32_t)__popcll(mt[k] & ltMask);
                 const uint32_t pid = item / a.nsearch, sIdx = item - pid * a.nsearch;
                 if (at < a.taskCap)
-                    a.tasks[at] = make_uint4(cur[k].x, cur[k].w & 0xFFFFu, pid, (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
+                    a.tasks[at] = make_uint4(cur[k].x, (cur[k].w & 0xFFFFu) | resolved[k], pid,
+                                             (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
                 else
                     atomicOr(a.flags, 8u);
                 ++cTasks;
@@ -595,79 +727,6 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 
 
 
-// ---- runs of symbols as bit masks: bit j = chain symbol j. Symbols come as
-// 3 bit planes (device_index.h), so the per-symbol equality of 32 symbols is
-// three word xors; the chain logic uses the low 16 bits.
-constexpr uint32_t kRun = 32;              // symbols per micro-step run (a forced node's match budget)
-constexpr uint32_t kRunMask = 0xFFFFFFFFu;
-// chain positions per micro-step of a node whose error children are forced:
-// the forced-run check of an error child at chain node i reads symbols
-// i .. i + 7 of the 32 (kChain + 7 <= kRun)
-constexpr uint32_t kChain = 25;
-__device__ __forceinline__ uint32_t onesR(uint32_t n) {  // symbols [0, n), capped at kRun
-    return n >= kRun ? kRunMask : (1u << n) - 1u;
-}
-__device__ __forceinline__ uint32_t beyondR(uint32_t n) { return kRunMask & ~onesR(n); }  // symbols >= n
-// bit j set iff bits j .. j+6 are all set (7 consecutive matches from j)
-__device__ __forceinline__ uint32_t run7(uint32_t m) {
-    const uint32_t m2 = m & (m >> 1), m4 = m2 & (m2 >> 2);
-    return m4 & (m2 >> 4) & (m >> 6);
-}
-struct Planes { uint32_t b0, b1, b2; };
-__device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
-    return ~((p.b0 ^ t.b0) | (p.b1 ^ t.b1) | (p.b2 ^ t.b2));
-}
-__device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
-__device__ __forceinline__ Planes shr2(const Planes& p) { return {p.b0 >> 2, p.b1 >> 2, p.b2 >> 2}; }
-// 32 symbols from offset o of a lane's interleaved plane array (block i, plane
-// b at word (PL i + b) * 256; PL = 3 rank planes, or 2 code planes). o may be
-// negative (down to -32): reads may run past either end of the array into the
-// lane's neighbouring LDS regions; callers mask.
-template <int PL>
-__device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b) {
-    const int i = o >> 5;
-    return __builtin_amdgcn_alignbit(A[(PL * i + PL + (int)b) * 256], A[(PL * i + (int)b) * 256], (uint32_t)o & 31u);
-}
-// 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
-// reversed (back: bit j = symbol o - 1 - j). Symbols outside the array are
-// whatever the LDS holds there (the window's block -1 is the table region,
-// kTextTableMin words, the pattern's is the window): the window's are masked
-// by its `avail`, the pattern's lie beyond the pattern, which the chain logic
-// never uses (tests/text_model.py reads arbitrary symbols there).
-// (PL = 2: b2 is 0 on both sides, and the compiler drops it.)
-template <int PL>
-__device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
-    const int off = (int)o - (fwd ? 0 : 32);
-    Planes r;
-    uint32_t v[3] = {0u, 0u, 0u};
-#pragma unroll
-    for (uint32_t b = 0; b < (uint32_t)PL; ++b) {
-        const uint32_t w = read32<PL>(A, off, b);
-        v[b] = fwd ? w : __builtin_bitreverse32(w);
-    }
-    r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
-    return r;
-}
-
-// Two code planes (PL = 2) for the symbols A C G T, from the three rank
-// planes: c0 = b0 (dna4: A 001, C 010, G 011, T 100) or b0 ^ b2 (dna5: T is
-// 101), c1 = b1 — four distinct codes, so symbol equality is code equality.
-// '$' (000) and dna5's N (100) have no code: a task whose window or pattern
-// holds one runs in the three-plane kernel instead (odd3 flags them).
-template <int SIGMA>
-__device__ __forceinline__ uint32_t code0(uint32_t b0, uint32_t b2) { return SIGMA == 6 ? b0 ^ b2 : b0; }
-template <int SIGMA>
-__device__ __forceinline__ uint32_t odd3(uint32_t b0, uint32_t b1, uint32_t b2) {
-    return ~(b0 | b1 | b2) | (SIGMA == 6 ? (b2 & ~b0) : 0u);
-}
-
-// Raw buffer resource over [base, base + bytes) (gfx9 dword3): loads at an
-// offset past the end return 0 without a memory request, so guarded loads
-// need no branch (and no wait at a branch join).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t bufferOf(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-constexpr uint32_t kBufOOB = 0xFFFFFFFFu;  // offset of a load that returns 0
 
 // Copy two block arrays (window, pattern) from global memory into this lane's
 // interleaved LDS slots (3 words per block): all loads of up to 8 blocks of
@@ -808,13 +867,16 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
     uint32_t nBase = 0, nEnd = 0, qBase = 0;
     bool haveNext = false;
-    // The prefetched chunk's records still hold SA rows. Their text positions
-    // are read at the next refill, beside its window loads (one round trip for
-    // both), or at the latest when the chunk becomes current.
+    // The prefetched chunk's records hold SA rows (FM-phase tasks) or text
+    // positions (kTaskResolved: seeds checked by kSeedItems, diverted tasks).
+    // The rows' text positions are read at the next refill, beside its window
+    // loads (one round trip for both), or at the latest when the chunk becomes
+    // current.
     bool nextRaw = false;
     auto resolveNext = [&]() {
         if (nextRaw) {  // wave-uniform
-            if (nBase + lane < nEnd) nextRec.x = a.sa[nextRec.x];
+            if (nBase + lane < nEnd && !(nextRec.y & kTaskResolved)) nextRec.x = a.sa[nextRec.x];
+            nextRec.y &= ~kTaskResolved;
             nextRaw = false;
         }
     };
@@ -826,7 +888,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             nEnd = e;
             if (b + lane < e) nextRec = tasks[b + lane];
             haveNext = true;
-            nextRaw = a.resolved == 0u;
+            nextRaw = true;
         } else {
             qDone = true;
         }
@@ -867,7 +929,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                         nEnd = e;
                         if (b + lane < e) nextRec = tasks[b + lane];
                         haveNext = true;
-                        nextRaw = a.resolved == 0u;
+                        nextRaw = true;
                     }
                 }
                 if (qNext >= qEnd) continue;
@@ -915,7 +977,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     base = __shfl(base, 0);
                     if (divert) {
                         const uint32_t s = base + (uint32_t)__popcll(dm & ltMask);
-                        if (s < a.excCap) a.excTasks[s] = t;  // t.x is the text position already
+                        if (s < a.excCap) a.excTasks[s] = make_uint4(t.x, t.y | kTaskResolved, t.z, t.w);
                         else atomicOr(a.flags, 8u);
                     }
                 }

@@ -629,20 +629,33 @@ void stageScheme(Ctx* c, uint64_t npat, uint32_t m, const uint32_t* pi, const ui
     SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
     c->cover.reserve(cover.size());
     SH_HIP(hipMemcpyAsync(c->cover.ptr, cover.data(), cover.size() * 4, hipMemcpyHostToDevice, c->st));
-    // searches whose first kmerK steps admit no error start from the k-mer table
-    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu);
+    // searches whose first kmerK steps admit no error start from the k-mer
+    // table; seedRun: the forced run that follows in one direction (u == 0),
+    // which kSeedItems checks for single-row seeds (R | right << 8, R <= 32)
+    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu), run(ns, 0u);
     const uint32_t K = c->I.kmerK;
     for (uint32_t s = 0; K && K <= m && s < ns; ++s) {
+        const uint32_t* P = pi + (size_t)s * m;
+        const uint32_t* U = u + (size_t)s * m;
         bool exact = true;
-        uint32_t lo = pi[(size_t)s * m];
+        uint32_t lo = P[0];
         for (uint32_t p = 0; p < K; ++p) {
-            exact = exact && u[(size_t)s * m + p] == 0;
-            lo = std::min(lo, pi[(size_t)s * m + p]);
+            exact = exact && U[p] == 0;
+            lo = std::min(lo, P[p]);
         }
-        if (exact) kst[s] = lo;
+        if (!exact) continue;
+        kst[s] = lo;
+        if (K < m) {
+            const bool right = P[K] == lo + K;  // else P[K] == lo - 1 (a connected order)
+            uint32_t R = 0;
+            for (uint32_t p = K; p < m && R < 32 && U[p] == 0 && P[p] == (right ? lo + K + R : lo - 1 - R); ++p) ++R;
+            run[s] = R | (right ? 1u << 8 : 0u);
+        }
     }
     c->kmerStart.reserve(ns);
     SH_HIP(hipMemcpyAsync(c->kmerStart.ptr, kst.data(), ns * 4, hipMemcpyHostToDevice, c->st));
+    c->seedRun.reserve(ns);
+    SH_HIP(hipMemcpyAsync(c->seedRun.ptr, run.data(), ns * 4, hipMemcpyHostToDevice, c->st));
     SH_HIP(hipStreamSynchronize(c->st));
     c->nsearch = ns;
     c->edit = edit != 0;
@@ -758,12 +771,11 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
            const uint32_t* u, uint32_t ns, int edit) {
     if (npat == 0) throw Error("no patterns");
     c->staged = c->streaming = false;
-    std::vector<uint32_t> packed, cover;
-    packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);
+    std::vector<uint32_t> packed;
+    packSchemeTable(pi, l, u, ns, m, packed, c->maxErr);  // a bad scheme fails before the upload
     if ((size_t)ns * m * 4 > 60 * 1024) throw Error("scheme too large for LDS (searches * len > 15360)");
     if (ns > 255) throw Error("at most 255 searches per scheme");
     const auto t0 = std::chrono::steady_clock::now();
-    textTable(pi, l, u, ns, m, packed, cover);
     c->patWords = (m + 7) / 8;
     {
         DevBuf<uint8_t>& raw = c->rawPats;  // kept: no 2 GB allocate / free per call at C3
@@ -786,29 +798,9 @@ void stage(Ctx* c, const uint8_t* ranks, uint64_t npat, uint32_t m, const uint32
             throw Error("pattern rank out of range for this index");
         }
     }
-    c->scheme.reserve(packed.size());
-    SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
-    c->cover.reserve(cover.size());
-    SH_HIP(hipMemcpyAsync(c->cover.ptr, cover.data(), cover.size() * 4, hipMemcpyHostToDevice, c->st));
-    // searches whose first kmerK steps admit no error start from the k-mer table
-    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu);
-    const uint32_t K = c->I.kmerK;
-    for (uint32_t s = 0; K && K <= m && s < ns; ++s) {
-        bool exact = true;
-        uint32_t lo = pi[(size_t)s * m];
-        for (uint32_t p = 0; p < K; ++p) {
-            exact = exact && u[(size_t)s * m + p] == 0;
-            lo = std::min(lo, pi[(size_t)s * m + p]);
-        }
-        if (exact) kst[s] = lo;
-    }
-    c->kmerStart.reserve(ns);
-    SH_HIP(hipMemcpyAsync(c->kmerStart.ptr, kst.data(), ns * 4, hipMemcpyHostToDevice, c->st));
-    SH_HIP(hipStreamSynchronize(c->st));
+    stageScheme(c, npat, m, pi, l, u, ns, edit);
     c->npat = npat;
     c->m = m;
-    c->nsearch = ns;
-    c->edit = edit != 0;
     c->staged = true;
     c->stageMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
