@@ -624,3 +624,28 @@ def test_two_plane_text_phase_diverts_dollar_and_n(gpu_device, monkeypatch, m, k
         monkeypatch.setenv("SAHARA_TEXT_PLANES", "3")
         assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), batch
         assert gpu.stats()["text_exc_tasks"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,gen", [(100, 2, "h2-k2"), (60, 3, "h2-k3"), (50, 1, "pigeon"), (80, 2, "pex-bu")])
+def test_seed_forced_run_check(gpu_device, monkeypatch, m, k, gen):
+    """kSeedItems checks the forced run after a single-row seed against the
+    text: the same multiset as the oracle with and without the check
+    (SAHARA_SEED_CHECK=0), on reads and their reverse complements (mostly
+    random occurrences), text ends included; with it fewer text tasks."""
+    rng = np.random.default_rng(m * 10 + k)
+    recs = random_records(rng, [60000, 30000, 700, 150], 6, with_n=True, repeats=True)
+    reads = np.vstack([mutate_reads(rng, recs, 300, m, k, 6), random_records(rng, [m] * 60, 6)])
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme(gen, 0, k, m)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    tasks = {}
+    for check in ("1", "0"):
+        monkeypatch.setenv("SAHARA_SEED_CHECK", check)
+        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), check
+        gpu.stage(pats, scheme)
+        gpu.run(count=True)
+        tasks[check] = gpu.stats()["conversions"]
+        assert np.array_equal(hits_as_rows(gpu.fetch()), want), check
+    assert tasks["1"] < tasks["0"], tasks
