@@ -393,6 +393,8 @@ def main():
                  "reference_algorithm": {"ext_lines_per_read": round(ref_cnt["ext_lines"] / nreads, 1),
                                          "lf_steps_per_read": round(ref_cnt["lf_steps"] / nreads, 2),
                                          "rows_per_read": round(ref_cnt["hits"] / nreads, 3),
+                                         "nodes_per_read": round(ref_cnt["nodes"] / nreads, 1),
+                                         "fm_lane_util": round(ref_cnt["nodes"] / max(1, 64 * ref_cnt["fm_iterations"]), 3),
                                          "same_hits": ref_cnt["hits"] == cnt["hits"]},
                  }
 

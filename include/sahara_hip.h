@@ -94,9 +94,6 @@ typedef struct sahara_stats {
     double   output_ms;          /* sahara_gpu_search: wall time of handing the hits to the host */
     uint64_t text_launches;      /* text-phase kernel launches in the pass */
     uint64_t upload_chunks[3];   /* streamed upload chunks sent at 2 / 4 / 8 bits per symbol */
-    double   text_exc_ms;        /* device time of the three-plane launches over tasks whose window or
-                                    pattern holds a '$' or N (two-plane text phase) */
-    uint64_t text_exc_tasks;     /* those tasks */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

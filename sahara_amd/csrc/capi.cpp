@@ -203,10 +203,10 @@ Ctx* newCtx(int device) {
     });
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmBegin, &sl.fmDone, &sl.textStart, &sl.textMid0,
-                              &sl.textMid1, &sl.textMain, &sl.textDone, &sl.free})
+                              &sl.textMid1, &sl.textDone, &sl.free})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);
-        sl.queues.reserve(1024);
+        sl.queues.reserve(768);
     }
     for (void*& p : c->outStage) SH_HIP(hipHostMalloc(&p, Ctx::kOutChunk));
     c->small.reserve(8);

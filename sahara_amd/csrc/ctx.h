@@ -329,7 +329,6 @@ struct Ctx {
     uint64_t npat = 0;
     uint32_t m = 0, patWords = 0, patBlocks = 0;
     DevBuf<uint32_t> scheme, cover, kmerStart;        // FM scheme table; text table (textTable)
-    DevBuf<uint32_t> seedRun;                         // per search: forced run after the k-mer seed (kSeedItems)
     uint32_t nsearch = 0;
     uint32_t maxErr = 0;
     bool edit = true;
@@ -346,18 +345,16 @@ struct Ctx {
     static constexpr int kSlots = 5;
     struct Slot {
         DevBuf<uint4> hits, tasks, seeds;  // seeds: starting cursors (kSeedItems -> kSearchFM)
-        DevBuf<uint4> exc;                // text tasks with a '$' or N (two-plane text phase -> three-plane launch)
         DevBuf<uint32_t> seedItem;
-        DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount, excCount
+        DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
         DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512),
-                                          // [512, 768) (batch 0's second launch), diverted tasks [768, 1024)
+                                          // [512, 768) (batch 0's second launch)
         // kernel spans, each recorded on the kernel's own stream right around
         // its launch(es): seeds fmStart..seedDone (sD), FM fmBegin..fmDone
         // (sA), text textStart..textDone, or for the first batch's two text
         // launches textStart..textMid0 and textMid1..textDone (sB)
-        // textMain..textDone: the three-plane launch over the diverted tasks
         hipEvent_t fmStart = nullptr, seedDone = nullptr, fmBegin = nullptr, fmDone = nullptr, textStart = nullptr,
-                   textMid0 = nullptr, textMid1 = nullptr, textMain = nullptr, textDone = nullptr, free = nullptr;
+                   textMid0 = nullptr, textMid1 = nullptr, textDone = nullptr, free = nullptr;
         bool twoText = false;
     } slot[kSlots];
     hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
@@ -518,7 +515,7 @@ struct Ctx {
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
             for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
-                                 sl.textMid1, sl.textMain, sl.textDone, sl.free})
+                                 sl.textMid1, sl.textDone, sl.free})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
         if (nibHost) (void)hipHostFree(nibHost);

@@ -78,10 +78,10 @@ void run(Ctx* c, bool count) {
                   &sahara_stats::conversions, &sahara_stats::fm_iterations, &sahara_stats::text_iterations,
                   &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
                   &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
-                  &sahara_stats::text_steps, &sahara_stats::text_launches, &sahara_stats::text_exc_tasks})
+                  &sahara_stats::text_steps, &sahara_stats::text_launches})
                 T.*f += S.*f;
             for (double sahara_stats::*f : {&sahara_stats::search_ms, &sahara_stats::locate_ms, &sahara_stats::sort_ms,
-                                            &sahara_stats::text_ms, &sahara_stats::seed_ms, &sahara_stats::text_exc_ms})
+                                            &sahara_stats::text_ms, &sahara_stats::seed_ms})
                 T.*f += S.*f;
             T.search_launches += S.search_launches;
         }
@@ -187,19 +187,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const uint32_t winBlocks = exactWindow ? exactBlocks : (c->m + 2 * c->maxErr + 31 + 31) / 32;
     const uint32_t textStack = 2 * c->maxErr + 2;
     const uint32_t tableWords = std::max<uint32_t>(2 * c->nsearch * c->m, kTextTableMin);
-    // LDS planes per block: two code planes (A C G T) where a compile-time
-    // shape exists, the tasks with a '$' or N in window or pattern diverted
-    // to a three-plane launch after each batch's; three elsewhere
-    // (SAHARA_TEXT_PLANES=3: three everywhere)
-    const char* plEnv = std::getenv("SAHARA_TEXT_PLANES");
-    const uint32_t planes = textTwoPlanes(winBlocks, c->patBlocks, exactWindow) && (c->I.sigma == 5 || c->I.sigma == 6) &&
-                                    !(plEnv && std::atoi(plEnv) == 3)
-                                ? 2u
-                                : 3u;
-    auto ldsFor = [&](uint32_t pl) {
-        return (size_t)tableWords * 4 + (size_t)256 * (pl * (winBlocks + c->patBlocks) + 2 * textStack) * 4;
-    };
-    const size_t textLds = ldsFor(planes), textLds3 = ldsFor(3);
+    const size_t textLds = (size_t)tableWords * 4 + (size_t)256 * (3 * (winBlocks + c->patBlocks) + 2 * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
     if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
@@ -207,19 +195,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // the text phase addresses text and a batch's patterns with 32-bit buffer offsets
     const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
-    TextArgs shapeArgs{};
-    shapeArgs.winBlocks = winBlocks;
-    shapeArgs.patBlocks = c->patBlocks;
-    shapeArgs.exactWindow = exactWindow ? 1u : 0u;
-    if (c->verify && c->m <= 2047 && textLds3 <= 160 * 1024 && textFits)
-        tbpc = textBlocksPerCU(sigma, c->edit, textLds, planes, &shapeArgs);
+    if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
+        tbpc = textBlocksPerCU(sigma, c->edit, textLds);
     // overlapped with the FM phase, three text workgroups per CU beside its one
     // (four would fit: r2 v8 measured text 4 against 3 in alternating pairs,
     // C3 914-943M vs 880-952M on one box and 873-914M vs 953-956M on another,
     // C2 950-1013M vs 956-1026M: the sign flips with the box)
     if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
-    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0)
-        tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, textLds, planes, &shapeArgs), std::atoi(e)));
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, textLds), std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     // (pipelined) the first batch's text phase starts on its seed tasks while
     // its FM phase runs; only with several batches: a lone batch's FM phase
@@ -300,7 +283,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
         SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), s));
-        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 1024 * sizeof(uint32_t), s));
+        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 768 * sizeof(uint32_t), s));
         SH_HIP(hipEventRecord(sl.free, s));
     };
     for (auto& sl : c->slot) resetSlot(sl, sA);
@@ -310,7 +293,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
         sl.hits.reserve((size_t)c->hitCap + 1);
         sl.tasks.reserve((size_t)c->taskCap);
-        if (planes == 2) sl.exc.reserve((size_t)c->taskCap);  // at most every task of the batch
         SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
         SearchArgs a{};
         a.occF = c->I.occF.ptr;
@@ -361,17 +343,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sd.taskCount = sl.small.ptr + 4;
         sd.flags = sl.small.ptr + 2;
         sd.counters = count ? c->counters.ptr : nullptr;
-        // single-row seeds checked against the text (SAHARA_SEED_CHECK=0: not)
-        const char* checkEnv = std::getenv("SAHARA_SEED_CHECK");
-        if (sd.toText && sd.kmer && !(checkEnv && std::atoi(checkEnv) == 0)) {
-            sd.seedRun = c->seedRun.ptr;
-            sd.sa = c->I.saFull.ptr;
-            sd.text3 = c->I.text3.ptr;
-            sd.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
-            sd.pats3 = c->pats3.ptr + q0 * c->patBlocks;
-            sd.pats3Bytes = (uint32_t)std::min<uint64_t>((c->npat - q0) * c->patBlocks * 16, 0xFFFFFF00ull);
-            sd.patBlocks = c->patBlocks;
-        }
         a.seeds = sl.seeds.ptr;
         a.seedItem = sl.seedItem.ptr;
         a.seedCount = sl.small.ptr + 6;
@@ -432,10 +403,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
             t.stealAt = 8;
             if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-            t.planes = planes;
-            t.excTasks = sl.exc.ptr;
-            t.excCap = c->taskCap;
-            t.excCount = sl.small.ptr + 7;
             if (split0) {
                 // the first batch's seed tasks while its FM phase runs, then the
                 // tasks the FM phase appended after them
@@ -451,20 +418,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             }
             launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
             ++S.text_launches;
-            SH_HIP(hipEventRecord(sl.textMain, sB));
-            if (planes == 2) {  // the diverted tasks (text positions), three planes
-                TextArgs e = t;
-                e.planes = 3;
-                e.tasks = sl.exc.ptr;
-                e.taskCount = sl.small.ptr + 7;
-                e.taskBegin = nullptr;
-                e.work = sl.queues.ptr + 768;
-                e.excTasks = nullptr;
-                e.excCap = 0;
-                launchText(e, sigma, c->edit, count, (uint32_t)c->numCU, textLds3, sB);
-            }
-        } else {
-            SH_HIP(hipEventRecord(sl.textMain, sB));
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));
     };
@@ -496,14 +449,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         if (sl.twoText) {  // the two launches only, not the wait for the FM phase between them
             SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMid0));
             S.text_ms += ms;
-            SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textMain));
+            SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textDone));
         } else {
-            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMain));
+            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
         }
         S.text_ms += ms;
-        SH_HIP(hipEventElapsedTime(&ms, sl.textMain, sl.textDone));
-        S.text_exc_ms += ms;
-        S.text_exc_tasks += hs[7];
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
         if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
         if (hs[2] & (2u | 8u)) {  // hit or task buffer too small

@@ -60,23 +60,7 @@ struct SeedArgs {
     uint32_t* taskCount;
     uint32_t* flags;            // 8: task buffer too small
     unsigned long long* counters;  // count mode: text tasks (+6), else nullptr
-    // Single-row seeds: the forced matches that follow depth kmerK (u == 0
-    // there), checked against the text before the seed becomes a task.
-    // seedRun[s] = R | right << 8 (R <= 32 positions in one direction; 0: no
-    // check); a seed that passes goes to the text phase with its text position
-    // (kTaskResolved), one that fails ends here.
-    const uint32_t* seedRun;    // nullptr: no check
-    const uint32_t* sa;         // full SA
-    const uint4* text3;         // text, 3-bit-plane blocks
-    uint32_t text3Bytes;
-    const uint4* pats3;         // the batch's patterns, 3-bit-plane blocks
-    uint32_t pats3Bytes;
-    uint32_t patBlocks;
 };
-
-// Text task record flag (y, the matched length's high bit): x holds the text
-// position already, not an SA row.
-constexpr uint32_t kTaskResolved = 1u << 31;
 
 // Text phase LDS: the scheme table comes first and takes at least one block of
 // lane words (3 planes x 256 lanes), so that a read of a lane's window block -1
@@ -112,11 +96,6 @@ struct TextArgs {
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
-    uint32_t planes;         // LDS planes per block: 3 (any symbol) or 2 (A C G T codes; window / pattern with
-                             // '$' or N diverted to excTasks for a three-plane launch)
-    uint4* excTasks;         // planes 2: tasks diverted (text position in x), excCap entries, *excCount of them
-    uint32_t excCap;
-    uint32_t* excCount;
 };
 
 struct LocateArgs {
@@ -136,9 +115,7 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds, uint32_t planes = 3, const TextArgs* shapeOf = nullptr);
-// whether the two-plane kernel exists for this launch's shape
-bool textTwoPlanes(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow);
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);

@@ -223,80 +223,6 @@ __device__ __forceinline__ uint32_t childMeta(uint32_t pos, uint32_t e, uint32_t
     return npos | (ne << 16) | (nl << 20) | (nr << 22) | (nd << 25);
 }
 
-// ---- runs of symbols as bit masks: bit j = chain symbol j. Symbols come as
-// 3 bit planes (device_index.h), so the per-symbol equality of 32 symbols is
-// three word xors; the chain logic uses the low 16 bits.
-constexpr uint32_t kRun = 32;              // symbols per micro-step run (a forced node's match budget)
-constexpr uint32_t kRunMask = 0xFFFFFFFFu;
-// chain positions per micro-step of a node whose error children are forced:
-// the forced-run check of an error child at chain node i reads symbols
-// i .. i + 7 of the 32 (kChain + 7 <= kRun)
-constexpr uint32_t kChain = 25;
-__device__ __forceinline__ uint32_t onesR(uint32_t n) {  // symbols [0, n), capped at kRun
-    return n >= kRun ? kRunMask : (1u << n) - 1u;
-}
-__device__ __forceinline__ uint32_t beyondR(uint32_t n) { return kRunMask & ~onesR(n); }  // symbols >= n
-// bit j set iff bits j .. j+6 are all set (7 consecutive matches from j)
-__device__ __forceinline__ uint32_t run7(uint32_t m) {
-    const uint32_t m2 = m & (m >> 1), m4 = m2 & (m2 >> 2);
-    return m4 & (m2 >> 4) & (m >> 6);
-}
-struct Planes { uint32_t b0, b1, b2; };
-__device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
-    return ~((p.b0 ^ t.b0) | (p.b1 ^ t.b1) | (p.b2 ^ t.b2));
-}
-__device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
-__device__ __forceinline__ Planes shr2(const Planes& p) { return {p.b0 >> 2, p.b1 >> 2, p.b2 >> 2}; }
-// 32 symbols from offset o of a lane's interleaved plane array (block i, plane
-// b at word (PL i + b) * 256; PL = 3 rank planes, or 2 code planes). o may be
-// negative (down to -32): reads may run past either end of the array into the
-// lane's neighbouring LDS regions; callers mask.
-template <int PL>
-__device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b) {
-    const int i = o >> 5;
-    return __builtin_amdgcn_alignbit(A[(PL * i + PL + (int)b) * 256], A[(PL * i + (int)b) * 256], (uint32_t)o & 31u);
-}
-// 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
-// reversed (back: bit j = symbol o - 1 - j). Symbols outside the array are
-// whatever the LDS holds there (the window's block -1 is the table region,
-// kTextTableMin words, the pattern's is the window): the window's are masked
-// by its `avail`, the pattern's lie beyond the pattern, which the chain logic
-// never uses (tests/text_model.py reads arbitrary symbols there).
-// (PL = 2: b2 is 0 on both sides, and the compiler drops it.)
-template <int PL>
-__device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
-    const int off = (int)o - (fwd ? 0 : 32);
-    Planes r;
-    uint32_t v[3] = {0u, 0u, 0u};
-#pragma unroll
-    for (uint32_t b = 0; b < (uint32_t)PL; ++b) {
-        const uint32_t w = read32<PL>(A, off, b);
-        v[b] = fwd ? w : __builtin_bitreverse32(w);
-    }
-    r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
-    return r;
-}
-
-// Two code planes (PL = 2) for the symbols A C G T, from the three rank
-// planes: c0 = b0 (dna4: A 001, C 010, G 011, T 100) or b0 ^ b2 (dna5: T is
-// 101), c1 = b1 — four distinct codes, so symbol equality is code equality.
-// '$' (000) and dna5's N (100) have no code: a task whose window or pattern
-// holds one runs in the three-plane kernel instead (odd3 flags them).
-template <int SIGMA>
-__device__ __forceinline__ uint32_t code0(uint32_t b0, uint32_t b2) { return SIGMA == 6 ? b0 ^ b2 : b0; }
-template <int SIGMA>
-__device__ __forceinline__ uint32_t odd3(uint32_t b0, uint32_t b1, uint32_t b2) {
-    return ~(b0 | b1 | b2) | (SIGMA == 6 ? (b2 & ~b0) : 0u);
-}
-
-// Raw buffer resource over [base, base + bytes) (gfx9 dword3): loads at an
-// offset past the end return 0 without a memory request, so guarded loads
-// need no branch (and no wait at a branch join).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t bufferOf(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-constexpr uint32_t kBufOOB = 0xFFFFFFFFu;  // offset of a load that returns 0
-
 // ========================================================= seeds ====
 // One thread per work item (pattern, search): its starting cursor. A search
 // whose first kmerK steps admit no error starts at depth kmerK from the k-mer
@@ -368,71 +294,14 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t ltMask = (1ull << lane) - 1ull;
     uint64_t cTasks = 0;
-    const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
-    const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
     for (uint32_t base = blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
         uint4 cur[4];
         bool keep[4], task[4];
-        uint32_t resolved[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k]);
             task[k] = keep[k] && a.toText && cur[k].z == 1u && (cur[k].w & 0xFFFFu) < a.m;
             keep[k] = keep[k] && !task[k];
-        }
-        if (a.seedRun) {
-            // single-row seeds: their forced run checked against the text (the
-            // text phase's first micro-step, done where the SA and text reads of
-            // four items per lane are in flight together). A seed of a random
-            // occurrence — most of the reverse complements' — fails within a few
-            // symbols and ends here instead of costing the text phase a task start
-            uint32_t run[4], pos[4], sIdx[4], pid[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t item = base + k * 256u + threadIdx.x;
-                pid[k] = item / a.nsearch;
-                sIdx[k] = item - pid[k] * a.nsearch;
-                run[k] = task[k] ? a.seedRun[sIdx[k]] : 0u;
-                pos[k] = (run[k] & 0xFFu) ? a.sa[cur[k].x] : 0u;
-            }
-            uint4 tb[4][2], pb[4][2];
-            uint32_t tsh[4], psh[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t R = run[k] & 0xFFu;
-                const bool right = (run[k] >> 8) & 1u;
-                const uint32_t ks = R ? a.kmerStart[sIdx[k]] : 0u;
-                // text symbols [tq, tq + R) against pattern symbols [pq, pq + R)
-                const uint32_t tq = right ? pos[k] + a.kmerK : pos[k] - R, pq = right ? ks + a.kmerK : ks - R;
-                const bool live = R && (right || pos[k] >= R);
-                if (R && !live) task[k] = false;  // would run left of the text's first symbol
-                tsh[k] = tq & 31u;
-                psh[k] = pq & 31u;
-                const uint32_t to = live ? (tq >> 5) * 16u : kBufOOB;
-                const uint32_t po = live ? (pid[k] * a.patBlocks + (pq >> 5)) * 16u : kBufOOB;
-                tb[k][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(textBuf, to, 0, 0));
-                tb[k][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(textBuf, live ? to + 16u : kBufOOB, 0, 0));
-                pb[k][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(patBuf, po, 0, 0));
-                pb[k][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(patBuf, live ? po + 16u : kBufOOB, 0, 0));
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t R = run[k] & 0xFFu;
-                if (!task[k] || !R) continue;
-                const Planes T = {__builtin_amdgcn_alignbit(tb[k][1].x, tb[k][0].x, tsh[k]),
-                                  __builtin_amdgcn_alignbit(tb[k][1].y, tb[k][0].y, tsh[k]),
-                                  __builtin_amdgcn_alignbit(tb[k][1].z, tb[k][0].z, tsh[k])};
-                const Planes Pp = {__builtin_amdgcn_alignbit(pb[k][1].x, pb[k][0].x, psh[k]),
-                                   __builtin_amdgcn_alignbit(pb[k][1].y, pb[k][0].y, psh[k]),
-                                   __builtin_amdgcn_alignbit(pb[k][1].z, pb[k][0].z, psh[k])};
-                const uint32_t want = onesR(R);
-                if ((eqm(Pp, T) & want) != want) {
-                    task[k] = false;  // the forced run breaks: the seed's subtree is empty
-                } else {
-                    cur[k].x = pos[k];  // the text position: the text phase needs no SA read
-                    resolved[k] = kTaskResolved;
-                }
-            }
         }
         uint64_t m[4], mt[4];
         uint32_t wsum = 0, wtask = 0;
@@ -465,8 +334,7 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
                 const uint32_t at = tslot + (uint32_t)__popcll(mt[k] & ltMask);
                 const uint32_t pid = item / a.nsearch, sIdx = item - pid * a.nsearch;
                 if (at < a.taskCap)
-                    a.tasks[at] = make_uint4(cur[k].x, (cur[k].w & 0xFFFFu) | resolved[k], pid,
-                                             (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
+                    a.tasks[at] = make_uint4(cur[k].x, cur[k].w & 0xFFFFu, pid, (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
                 else
                     atomicOr(a.flags, 8u);
                 ++cTasks;
@@ -505,6 +373,17 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     bool qDone = false;
     SlotRange hitSlots, taskSlots;
     uint4 cur = make_uint4(0, 0, 0, 0);
+    // The stack's top entry (index sp - 1) is held in `top`: a pop takes it
+    // from the register and issues the load of the entry below, which is then
+    // in flight beside this node's Occ line fetch instead of before it (one
+    // memory round trip per node that pops, not two); a push stores the old top.
+    uint4 top = cur;
+    auto loadTop = [&]() {
+        if (sp > 0) {
+            const uint32_t i = sp - 1u;
+            top = i < ldsDepth ? lstk[i * 256u + threadIdx.x] : stk[(size_t)(i - ldsDepth) * T];
+        }
+    };
     uint64_t cNodes = 0, cRank = 0, cLines = 0, cTasks = 0, cIter = 0;
     // seeds (kSeedItems: starting cursor + item) arrive in chunks of 64, one
     // record per lane, prefetched a chunk ahead so a refill costs no memory trip
@@ -569,9 +448,10 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
         }
         if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
         if (!have && sp > 0) {
+            cur = top;
             --sp;
-            cur = sp < ldsDepth ? lstk[sp * 256u + threadIdx.x] : stk[(size_t)(sp - ldsDepth) * T];
             have = true;
+            loadTop();
         }
         if (!__any(have)) break;
         if (COUNT && lane == 0) ++cIter;
@@ -680,8 +560,12 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
             };
             auto push = [&](const uint4& v) {
                 if (sp < a.stackCap) {
-                    if (sp < ldsDepth) lstk[sp * 256u + threadIdx.x] = v;
-                    else stk[(size_t)(sp - ldsDepth) * T] = v;
+                    if (sp > 0) {
+                        const uint32_t i = sp - 1u;
+                        if (i < ldsDepth) lstk[i * 256u + threadIdx.x] = top;
+                        else stk[(size_t)(i - ldsDepth) * T] = top;
+                    }
+                    top = v;
                     ++sp;
                 } else {
                     atomicOr(a.flags, 1u);
@@ -727,17 +611,71 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 
 
 
+// ---- runs of symbols as bit masks: bit j = chain symbol j. Symbols come as
+// 3 bit planes (device_index.h), so the per-symbol equality of 32 symbols is
+// three word xors; the chain logic uses the low 16 bits.
+constexpr uint32_t kRun = 32;              // symbols per micro-step run (a forced node's match budget)
+constexpr uint32_t kRunMask = 0xFFFFFFFFu;
+// chain positions per micro-step of a node whose error children are forced:
+// the forced-run check of an error child at chain node i reads symbols
+// i .. i + 7 of the 32 (kChain + 7 <= kRun)
+constexpr uint32_t kChain = 25;
+__device__ __forceinline__ uint32_t onesR(uint32_t n) {  // symbols [0, n), capped at kRun
+    return n >= kRun ? kRunMask : (1u << n) - 1u;
+}
+__device__ __forceinline__ uint32_t beyondR(uint32_t n) { return kRunMask & ~onesR(n); }  // symbols >= n
+// bit j set iff bits j .. j+6 are all set (7 consecutive matches from j)
+__device__ __forceinline__ uint32_t run7(uint32_t m) {
+    const uint32_t m2 = m & (m >> 1), m4 = m2 & (m2 >> 2);
+    return m4 & (m2 >> 4) & (m >> 6);
+}
+struct Planes { uint32_t b0, b1, b2; };
+__device__ __forceinline__ uint32_t eqm(const Planes& p, const Planes& t) {
+    return ~((p.b0 ^ t.b0) | (p.b1 ^ t.b1) | (p.b2 ^ t.b2));
+}
+__device__ __forceinline__ Planes shr1(const Planes& p) { return {p.b0 >> 1, p.b1 >> 1, p.b2 >> 1}; }
+__device__ __forceinline__ Planes shr2(const Planes& p) { return {p.b0 >> 2, p.b1 >> 2, p.b2 >> 2}; }
+// 32 symbols from offset o of a lane's interleaved plane array (block i, plane
+// b at word (3i + b) * 256). o may be negative (down to -32): reads may run
+// past either end of the array into the lane's neighbouring LDS regions; callers
+// mask.
+__device__ __forceinline__ uint32_t read32(const uint32_t* A, int o, uint32_t b) {
+    const int i = o >> 5;
+    return __builtin_amdgcn_alignbit(A[(3 * i + 3 + (int)b) * 256], A[(3 * i + (int)b) * 256], (uint32_t)o & 31u);
+}
+// 32 symbols in chain order: right (fwd) from o, or left ending at o - 1 and
+// reversed (back: bit j = symbol o - 1 - j). Symbols outside the array are
+// whatever the LDS holds there (the window's block -1 is the table region,
+// kTextTableMin words, the pattern's is the window): the window's are masked
+// by its `avail`, the pattern's lie beyond the pattern, which the chain logic
+// never uses (tests/text_model.py reads arbitrary symbols there).
+__device__ __forceinline__ Planes chain32(const uint32_t* A, uint32_t o, bool fwd) {
+    const int off = (int)o - (fwd ? 0 : 32);
+    Planes r;
+    uint32_t v[3];
+#pragma unroll
+    for (uint32_t b = 0; b < 3; ++b) {
+        const uint32_t w = read32(A, off, b);
+        v[b] = fwd ? w : __builtin_bitreverse32(w);
+    }
+    r.b0 = v[0]; r.b1 = v[1]; r.b2 = v[2];
+    return r;
+}
+
+// Raw buffer resource over [base, base + bytes) (gfx9 dword3): loads at an
+// offset past the end return 0 without a memory request, so guarded loads
+// need no branch (and no wait at a branch join).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bufferOf(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+constexpr uint32_t kBufOOB = 0xFFFFFFFFu;  // offset of a load that returns 0
 
 // Copy two block arrays (window, pattern) from global memory into this lane's
 // interleaved LDS slots (3 words per block): all loads of up to 8 blocks of
 // each array are issued before the first store, so a task start costs one
 // memory round trip for m <~ 190.
-// PL = 2: stored as code planes, and `odd` collects the symbols that have no
-// code (the window's '$' / N, the pattern's N).
-template <int SIGMA, int PL>
 __device__ __forceinline__ void copyBlocks(uint32_t* DA, __amdgpu_buffer_rsrc_t RA, uint32_t offA, uint32_t na,
-                                           uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB, uint32_t nb,
-                                           uint32_t& odd) {
+                                           uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB, uint32_t nb) {
     const uint32_t n = max(na, nb);
     for (uint32_t c = 0; c < n; c += 8) {
         decltype(__builtin_amdgcn_raw_buffer_load_b128(RA, 0u, 0, 0)) va[8], vb[8];
@@ -750,33 +688,17 @@ __device__ __forceinline__ void copyBlocks(uint32_t* DA, __amdgpu_buffer_rsrc_t 
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
             const uint32_t j = c + i;
-            if (PL == 3) {
-                if (j < na) { uint32_t* D = DA + 3u * j * 256u; D[0] = va[i][0]; D[256] = va[i][1]; D[512] = va[i][2]; }
-                if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[i][0]; D[256] = vb[i][1]; D[512] = vb[i][2]; }
-            } else {
-                if (j < na) {
-                    uint32_t* D = DA + 2u * j * 256u;
-                    D[0] = code0<SIGMA>(va[i][0], va[i][2]);
-                    D[256] = va[i][1];
-                    odd |= odd3<SIGMA>(va[i][0], va[i][1], va[i][2]);
-                }
-                if (j < nb) {
-                    uint32_t* D = DB + 2u * j * 256u;
-                    D[0] = code0<SIGMA>(vb[i][0], vb[i][2]);
-                    D[256] = vb[i][1];
-                    if (SIGMA == 6) odd |= vb[i][2] & ~vb[i][0];  // N (the padding past m is 000: not odd here)
-                }
-            }
+            if (j < na) { uint32_t* D = DA + 3u * j * 256u; D[0] = va[i][0]; D[256] = va[i][1]; D[512] = va[i][2]; }
+            if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[i][0]; D[256] = vb[i][1]; D[512] = vb[i][2]; }
         }
     }
 }
 
 // Same, but the window starts at any symbol: na blocks come from na + 1
 // source blocks funnel-shifted by sh symbols (na + 1 <= 8, nb <= 8).
-template <int SIGMA, int PL>
 __device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_rsrc_t RA, uint32_t offA, uint32_t sh,
                                                   uint32_t na, uint32_t* DB, __amdgpu_buffer_rsrc_t RB, uint32_t offB,
-                                                  uint32_t nb, uint32_t& odd) {
+                                                  uint32_t nb) {
     decltype(__builtin_amdgcn_raw_buffer_load_b128(RA, 0u, 0, 0)) va[8], vb[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) {
@@ -786,32 +708,14 @@ __device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_
 #pragma unroll
     for (uint32_t j = 0; j < 7; ++j)
         if (j < na) {
-            const uint32_t b0 = __builtin_amdgcn_alignbit(va[j + 1][0], va[j][0], sh);
-            const uint32_t b1 = __builtin_amdgcn_alignbit(va[j + 1][1], va[j][1], sh);
-            const uint32_t b2 = __builtin_amdgcn_alignbit(va[j + 1][2], va[j][2], sh);
-            if (PL == 3) {
-                uint32_t* D = DA + 3u * j * 256u;
-                D[0] = b0; D[256] = b1; D[512] = b2;
-            } else {
-                uint32_t* D = DA + 2u * j * 256u;
-                D[0] = code0<SIGMA>(b0, b2);
-                D[256] = b1;
-                odd |= odd3<SIGMA>(b0, b1, b2);
-            }
+            uint32_t* D = DA + 3u * j * 256u;
+            D[0] = __builtin_amdgcn_alignbit(va[j + 1][0], va[j][0], sh);
+            D[256] = __builtin_amdgcn_alignbit(va[j + 1][1], va[j][1], sh);
+            D[512] = __builtin_amdgcn_alignbit(va[j + 1][2], va[j][2], sh);
         }
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j)
-        if (j < nb) {
-            if (PL == 3) {
-                uint32_t* D = DB + 3u * j * 256u;
-                D[0] = vb[j][0]; D[256] = vb[j][1]; D[512] = vb[j][2];
-            } else {
-                uint32_t* D = DB + 2u * j * 256u;
-                D[0] = code0<SIGMA>(vb[j][0], vb[j][2]);
-                D[256] = vb[j][1];
-                if (SIGMA == 6) odd |= vb[j][2] & ~vb[j][0];
-            }
-        }
+        if (j < nb) { uint32_t* D = DB + 3u * j * 256u; D[0] = vb[j][0]; D[256] = vb[j][1]; D[512] = vb[j][2]; }
 }
 
 // SHAPE fixes the window and pattern block counts at compile time, so that
@@ -825,12 +729,7 @@ struct TextShape { uint32_t win, pat; bool exact; };
 __host__ __device__ constexpr TextShape textShape(int shape) {
     return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
-// PL: LDS planes per block. 3 = the rank planes of device_index.h, any
-// symbol; 2 = the code planes of code0 (a quarter less LDS per lane and
-// fewer instructions per compare), with the tasks whose window or pattern
-// holds a '$' or N appended to a.excTasks (text positions resolved) for a
-// three-plane launch over them after this one.
-template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0, int PL = 3>
+template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     uint2* SC = reinterpret_cast<uint2*>(lds);
@@ -844,8 +743,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     const uint32_t winBlocks = SHAPE ? kShape.win : a.winBlocks, patBlocks = SHAPE ? kShape.pat : a.patBlocks;
     const bool exactWindow = SHAPE ? kShape.exact : a.exactWindow != 0u;
     uint32_t* W = slot + threadIdx.x;
-    uint32_t* P = slot + (uint32_t)PL * winBlocks * 256u + threadIdx.x;
-    uint2* S = reinterpret_cast<uint2*>(slot + (uint32_t)PL * (winBlocks + patBlocks) * 256u) + threadIdx.x;
+    uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
+    uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
     auto stackGet = [&](uint32_t d) -> uint2 { return S[d * 256u]; };
     auto stackPut = [&](uint32_t d, const uint2& v) { S[d * 256u] = v; };
     const uint32_t winLen = winBlocks * 32u;
@@ -867,16 +766,13 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
     uint32_t nBase = 0, nEnd = 0, qBase = 0;
     bool haveNext = false;
-    // The prefetched chunk's records hold SA rows (FM-phase tasks) or text
-    // positions (kTaskResolved: seeds checked by kSeedItems, diverted tasks).
-    // The rows' text positions are read at the next refill, beside its window
-    // loads (one round trip for both), or at the latest when the chunk becomes
-    // current.
+    // The prefetched chunk's records still hold SA rows. Their text positions
+    // are read at the next refill, beside its window loads (one round trip for
+    // both), or at the latest when the chunk becomes current.
     bool nextRaw = false;
     auto resolveNext = [&]() {
         if (nextRaw) {  // wave-uniform
-            if (nBase + lane < nEnd && !(nextRec.y & kTaskResolved)) nextRec.x = a.sa[nextRec.x];
-            nextRec.y &= ~kTaskResolved;
+            if (nBase + lane < nEnd) nextRec.x = a.sa[nextRec.x];
             nextRaw = false;
         }
     };
@@ -941,7 +837,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t srcLane = (qNext - qBase + rank) & 63u;
             const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
                                        __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
-            bool divert = false;
             if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
                 // ---- start a task (x = its text position): copy the pattern
                 // and the text window its subtree can reach
@@ -954,33 +849,15 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
                 wb = x > left ? x - left : 0u;  // window start
-                uint32_t odd = 0u;
                 if (exactWindow) {              // at wb: m + 2k symbols fit in winBlocks blocks
-                    copyBlocksShifted<SIGMA, PL>(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
-                                                 pid * patBlocks * 16u, patBlocks, odd);
+                    copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
+                                      pid * patBlocks * 16u, patBlocks);
                 } else {                        // at the block start below wb (31 more symbols)
                     wb &= ~31u;
-                    copyBlocks<SIGMA, PL>(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u,
-                                          patBlocks, odd);
+                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
                 }
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
-                divert = PL == 2 && odd != 0u;
-                have = !divert;
-            }
-            if (PL == 2) {
-                // tasks with a '$' or N go to the three-plane launch (wave-uniform:
-                // one atomic per wave and refill round that has any)
-                const uint64_t dm = __ballot(divert);
-                if (dm) {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(a.excCount, (uint32_t)__popcll(dm));
-                    base = __shfl(base, 0);
-                    if (divert) {
-                        const uint32_t s = base + (uint32_t)__popcll(dm & ltMask);
-                        if (s < a.excCap) a.excTasks[s] = make_uint4(t.x, t.y | kTaskResolved, t.z, t.w);
-                        else atomicOr(a.flags, 8u);
-                    }
-                }
+                have = true;
             }
             pending &= ~__ballot(mine);
             qNext += take;
@@ -1017,9 +894,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 if (takes) {
                     const uint32_t* src = slot + dTid;
                     uint32_t* dst = slot + threadIdx.x;
-                    for (uint32_t k = 0; k < (uint32_t)PL * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
-                    const uint2 node =
-                        reinterpret_cast<const uint2*>(slot + (uint32_t)PL * (winBlocks + patBlocks) * 256u)[dTid];
+                    for (uint32_t k = 0; k < 3u * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
+                    const uint2 node = reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
                     cur = node;
                     pid = dPid;
                     wb = dWb;
@@ -1072,15 +948,14 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             // edge or before the text start reads as 0 and never matches.
             // One read each at a side-dependent offset (a left run ends at the
             // position and is bit-reversed), so the lanes of both sides share it
-            const Planes P16 = chain32<PL>(P, r0 ? q0 : q0 + 1u, r0);
-            const Planes T16 = chain32<PL>(W, r0 ? yo : xo, r0);
+            const Planes P16 = chain32(P, r0 ? q0 : q0 + 1u, r0);
+            const Planes T16 = chain32(W, r0 ? yo : xo, r0);
             const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
             const uint32_t VT = onesR(avail);
             const uint32_t E0 = eqm(P16, T16) & VT;                 // p_j == t_j     (M chain, S runs)
             const uint32_t ED = eqm(P16, shr1(T16)) & (VT >> 1);    // p_j == t_{j+1} (D runs)
             const uint32_t EI = eqm(shr1(P16), T16) & VT;           // p_{j+1} == t_j (I runs)
-            // t_j is a symbol (not '$' / edge); a two-plane window holds no '$'
-            const uint32_t TZ = PL == 3 ? (T16.b0 | T16.b1 | T16.b2) & VT : VT;
+            const uint32_t TZ = (T16.b0 | T16.b1 | T16.b2) & VT;    // t_j is a symbol (not '$' / edge)
 
             const bool atLeaf = live && pos == m;
             const bool node = live && pos < m;
@@ -1752,28 +1627,23 @@ int textShapeOf(const TextArgs& a) {
     return 0;
 }
 
-template <int SIGMA, int SHAPE, int PL>
+template <int SIGMA, int SHAPE>
 void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     if (edit) {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, SHAPE, PL>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, SHAPE, PL>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, SHAPE>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, SHAPE>), grid, dim3(256), lds, st, a);
     } else {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, SHAPE, PL>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, SHAPE, PL>), grid, dim3(256), lds, st, a);
+        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, SHAPE>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, SHAPE>), grid, dim3(256), lds, st, a);
     }
 }
 
-// two-plane kernels: the compile-time shapes (C2 / C3, C5); the generic
-// shape keeps three planes
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     const int shape = textShapeOf(a);
-    const bool two = a.planes == 2;
-    if (shape == 1 && two) launchTextShaped<SIGMA, 1, 2>(a, edit, count, grid, lds, st);
-    else if (shape == 1) launchTextShaped<SIGMA, 1, 3>(a, edit, count, grid, lds, st);
-    else if (shape == 2 && two) launchTextShaped<SIGMA, 2, 2>(a, edit, count, grid, lds, st);
-    else if (shape == 2) launchTextShaped<SIGMA, 2, 3>(a, edit, count, grid, lds, st);
-    else launchTextShaped<SIGMA, 0, 3>(a, edit, count, grid, lds, st);
+    if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
+    else if (shape == 2) launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
+    else launchTextShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
 }
 
 }  // namespace
@@ -1787,32 +1657,13 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     return b < 1 ? 1 : b;
 }
 
-// occupancy of the kernel a launch of this shape uses (shapeOf: its args;
-// nullptr: the generic kernel)
-template <int SIGMA, bool EDIT>
-const void* textKernelFor(uint32_t planes, int shape) {
-    if (shape == 1) return planes == 2 ? (const void*)kSearchText<SIGMA, EDIT, false, 1, 2>
-                                       : (const void*)kSearchText<SIGMA, EDIT, false, 1, 3>;
-    if (shape == 2) return planes == 2 ? (const void*)kSearchText<SIGMA, EDIT, false, 2, 2>
-                                       : (const void*)kSearchText<SIGMA, EDIT, false, 2, 3>;
-    return (const void*)kSearchText<SIGMA, EDIT, false, 0, 3>;
-}
-
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds, uint32_t planes, const TextArgs* shapeOf) {
-    const int shape = shapeOf ? textShapeOf(*shapeOf) : 0;
-    const void* f = sigma == 5 ? (edit ? textKernelFor<5, true>(planes, shape) : textKernelFor<5, false>(planes, shape))
-                               : (edit ? textKernelFor<6, true>(planes, shape) : textKernelFor<6, false>(planes, shape));
+int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     int b = 0;
+    const void* f;
+    if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false> : (const void*)kSearchText<5, false, false>;
+    else            f = edit ? (const void*)kSearchText<6, true, false> : (const void*)kSearchText<6, false, false>;
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b;
-}
-
-bool textTwoPlanes(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow) {
-    TextArgs a{};
-    a.winBlocks = winBlocks;
-    a.patBlocks = patBlocks;
-    a.exactWindow = exactWindow ? 1u : 0u;
-    return textShapeOf(a) != 0;
 }
 
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,

@@ -629,33 +629,20 @@ void stageScheme(Ctx* c, uint64_t npat, uint32_t m, const uint32_t* pi, const ui
     SH_HIP(hipMemcpyAsync(c->scheme.ptr, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, c->st));
     c->cover.reserve(cover.size());
     SH_HIP(hipMemcpyAsync(c->cover.ptr, cover.data(), cover.size() * 4, hipMemcpyHostToDevice, c->st));
-    // searches whose first kmerK steps admit no error start from the k-mer
-    // table; seedRun: the forced run that follows in one direction (u == 0),
-    // which kSeedItems checks for single-row seeds (R | right << 8, R <= 32)
-    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu), run(ns, 0u);
+    // searches whose first kmerK steps admit no error start from the k-mer table
+    std::vector<uint32_t> kst(ns, 0xFFFFFFFFu);
     const uint32_t K = c->I.kmerK;
     for (uint32_t s = 0; K && K <= m && s < ns; ++s) {
-        const uint32_t* P = pi + (size_t)s * m;
-        const uint32_t* U = u + (size_t)s * m;
         bool exact = true;
-        uint32_t lo = P[0];
+        uint32_t lo = pi[(size_t)s * m];
         for (uint32_t p = 0; p < K; ++p) {
-            exact = exact && U[p] == 0;
-            lo = std::min(lo, P[p]);
+            exact = exact && u[(size_t)s * m + p] == 0;
+            lo = std::min(lo, pi[(size_t)s * m + p]);
         }
-        if (!exact) continue;
-        kst[s] = lo;
-        if (K < m) {
-            const bool right = P[K] == lo + K;  // else P[K] == lo - 1 (a connected order)
-            uint32_t R = 0;
-            for (uint32_t p = K; p < m && R < 32 && U[p] == 0 && P[p] == (right ? lo + K + R : lo - 1 - R); ++p) ++R;
-            run[s] = R | (right ? 1u << 8 : 0u);
-        }
+        if (exact) kst[s] = lo;
     }
     c->kmerStart.reserve(ns);
     SH_HIP(hipMemcpyAsync(c->kmerStart.ptr, kst.data(), ns * 4, hipMemcpyHostToDevice, c->st));
-    c->seedRun.reserve(ns);
-    SH_HIP(hipMemcpyAsync(c->seedRun.ptr, run.data(), ns * 4, hipMemcpyHostToDevice, c->st));
     SH_HIP(hipStreamSynchronize(c->st));
     c->nsearch = ns;
     c->edit = edit != 0;

@@ -596,13 +596,11 @@ def test_long_and_huge_segments(gpu_device, monkeypatch, batch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k", [(100, 2), (250, 3), (100, 1)])
-def test_two_plane_text_phase_diverts_dollar_and_n(gpu_device, monkeypatch, m, k):
+def test_text_shapes_with_dollar_and_n(gpu_device, monkeypatch, m, k):
     """The compile-time text shapes (m = 100: C2 / C3, m = 250 with k = 3: C5)
-    keep window and pattern in two code planes; a task whose window holds a
-    record delimiter '$' (short records), an N of the text or whose pattern
-    holds an N runs in a three-plane launch after the batch's. Same multiset
-    as the oracle and as three planes everywhere (SAHARA_TEXT_PLANES=3), in
-    one batch and many, with tasks diverted and tasks not."""
+    on windows that hold a record delimiter '$' (short records) or an N of the
+    text, and patterns that hold an N: the oracle's multiset, in one batch
+    and many."""
     rng = np.random.default_rng(m + k)
     lens = [int(x) for x in rng.integers(m // 2, 3 * m, 60)] + [20000, 9000]
     recs = random_records(rng, lens, 6, with_n=True, repeats=True)
@@ -616,23 +614,17 @@ def test_two_plane_text_phase_diverts_dollar_and_n(gpu_device, monkeypatch, m, k
     for batch in (None, "131"):
         if batch:
             monkeypatch.setenv("SAHARA_BATCH", batch)
-        monkeypatch.delenv("SAHARA_TEXT_PLANES", raising=False)
         assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), batch
-        st = gpu.stats()
-        assert st["text_exc_tasks"] > 0
         assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme)), want), batch
-        monkeypatch.setenv("SAHARA_TEXT_PLANES", "3")
-        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), batch
-        assert gpu.stats()["text_exc_tasks"] == 0
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k,gen", [(100, 2, "h2-k2"), (60, 3, "h2-k3"), (50, 1, "pigeon"), (80, 2, "pex-bu")])
-def test_seed_forced_run_check(gpu_device, monkeypatch, m, k, gen):
-    """kSeedItems checks the forced run after a single-row seed against the
-    text: the same multiset as the oracle with and without the check
-    (SAHARA_SEED_CHECK=0), on reads and their reverse complements (mostly
-    random occurrences), text ends included; with it fewer text tasks."""
+def test_single_row_seeds_near_text_ends(gpu_device, m, k, gen):
+    """Single-row k-mer seeds going straight to the text phase, on reads and
+    their reverse complements (mostly random occurrences) and random reads,
+    over short records and text ends: the oracle's multiset through the
+    staged and the counting pass."""
     rng = np.random.default_rng(m * 10 + k)
     recs = random_records(rng, [60000, 30000, 700, 150], 6, with_n=True, repeats=True)
     reads = np.vstack([mutate_reads(rng, recs, 300, m, k, 6), random_records(rng, [m] * 60, 6)])
@@ -640,12 +632,8 @@ def test_seed_forced_run_check(gpu_device, monkeypatch, m, k, gen):
     scheme = sa.search_scheme(gen, 0, k, m)
     want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)[0])
     gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
-    tasks = {}
-    for check in ("1", "0"):
-        monkeypatch.setenv("SAHARA_SEED_CHECK", check)
-        assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want), check
-        gpu.stage(pats, scheme)
-        gpu.run(count=True)
-        tasks[check] = gpu.stats()["conversions"]
-        assert np.array_equal(hits_as_rows(gpu.fetch()), want), check
-    assert tasks["1"] < tasks["0"], tasks
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want)
+    gpu.stage(pats, scheme)
+    gpu.run(count=True)
+    assert gpu.stats()["conversions"] > 0
+    assert np.array_equal(hits_as_rows(gpu.fetch()), want)
