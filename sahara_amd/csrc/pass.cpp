@@ -173,7 +173,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const uint32_t firstBlocks = std::getenv("SAHARA_FM_BPC") ? blocks : (uint32_t)(c->numCU * fullBpc);
     const uint64_t T = (uint64_t)std::max(blocks, firstBlocks) * 256;
     const uint32_t stackCap = std::max<uint32_t>(c->maxErr, 1) * (2 * sigma - 2) + 2;
-    c->stack.reserve((size_t)std::max<uint32_t>(stackCap, 5) * T);  // levels beyond the LDS part
+    // a ring of stackCap levels per lane (work stealing moves a stack's bottom up)
+    const uint32_t stackLevels = stackCap;
+    c->stack.reserve((size_t)stackLevels * T);  // levels beyond the LDS part
     S.search_grid = blocks;
 
     // text phase geometry (LDS per lane: window | pattern | stack)
@@ -312,6 +314,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.taskCount = sl.small.ptr + 4;
         a.stack = c->stack.ptr;
         a.stackCap = stackCap;
+        a.stackLevels = stackLevels;
+        a.stealAt = 8;
+        if (const char* e = std::getenv("SAHARA_FM_STEAL_AT")) a.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
         a.hits = sl.hits.ptr;
         a.hitCap = c->hitCap;
         a.counters = c->counters.ptr;

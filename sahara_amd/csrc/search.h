@@ -25,7 +25,10 @@ struct SearchArgs {
     const uint32_t* scheme;  // nsearch * m packed entries (packScheme)
     uint32_t* work;          // item counter
     uint4* stack;            // spilled DFS levels beyond the LDS part, [depth][grid thread]
-    uint32_t stackCap;
+    uint32_t stackCap;       // most entries a lane's stack holds (the DFS bound)
+    uint32_t stackLevels;    // levels per lane, a ring (>= stackCap: work stealing moves a stack's bottom up)
+    uint32_t stealAt;        // once the seed queue is dry: idle lanes take the bottom stack entry of a busy
+                             // lane of their wave once this many are idle (0: off)
     uint4* hits;             // (qid, lb, len, e) or (qid, text pos, 1, e | kPosKnown)
     uint32_t hitCap;
     uint32_t* hitCount;      // reserved slots (waves reserve ranges; unused slots have len 0)

@@ -367,24 +367,26 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     const uint32_t ldsDepth = a.ldsDepth;
     uint4* stk = a.stack + gtid;
 
-    uint32_t sp = 0, pid = 0, sIdx = 0;
+    // the lane's stack holds entries [bot, sp) in a ring of stackLevels levels
+    // (entry d at level d mod stackLevels; bot < stackLevels): pushes and pops
+    // at sp, work stealing takes the bottom entry (bot++)
+    uint32_t sp = 0, bot = 0, pid = 0, sIdx = 0;
     bool have = false, exhausted = false;
     uint32_t qNext = 0, qEnd = 0, filled = 0;  // wave-uniform
     bool qDone = false;
     SlotRange hitSlots, taskSlots;
     uint4 cur = make_uint4(0, 0, 0, 0);
-    // The stack's top entry (index sp - 1) is held in `top`: a pop takes it
-    // from the register and issues the load of the entry below, which is then
-    // in flight beside this node's Occ line fetch instead of before it (one
-    // memory round trip per node that pops, not two); a push stores the old top.
-    uint4 top = cur;
-    auto loadTop = [&]() {
-        if (sp > 0) {
-            const uint32_t i = sp - 1u;
-            top = i < ldsDepth ? lstk[i * 256u + threadIdx.x] : stk[(size_t)(i - ldsDepth) * T];
-        }
-    };
     uint64_t cNodes = 0, cRank = 0, cLines = 0, cTasks = 0, cIter = 0;
+    const uint32_t L = a.stackLevels;
+    auto stackGet = [&](uint32_t d) -> uint4 {
+        d = d >= L ? d - L : d;
+        return d < ldsDepth ? lstk[d * 256u + threadIdx.x] : stk[(size_t)(d - ldsDepth) * T];
+    };
+    auto stackPut = [&](uint32_t d, const uint4& v) {
+        d = d >= L ? d - L : d;
+        if (d < ldsDepth) lstk[d * 256u + threadIdx.x] = v;
+        else stk[(size_t)(d - ldsDepth) * T] = v;
+    };
     // seeds (kSeedItems: starting cursor + item) arrive in chunks of 64, one
     // record per lane, prefetched a chunk ahead so a refill costs no memory trip
     const uint32_t nseeds = *a.seedCount;
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
 
     for (;;) {
         // ---- refill idle lanes from the wave's current seed chunk
-        const bool need = !have && sp == 0 && !exhausted;
+        const bool need = !have && sp == bot && !exhausted;
         uint64_t pending = __ballot(need);
         while (pending) {  // wave-uniform
             if (qNext >= qEnd) {
@@ -447,11 +449,57 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
             qNext += take;
         }
         if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
-        if (!have && sp > 0) {
-            cur = top;
+        if (!have && sp > bot) {
             --sp;
+            cur = stackGet(sp);
             have = true;
-            loadTop();
+        }
+        if (sp == bot) sp = bot = 0;
+        // ---- work stealing inside the wave once the seed queue is dry (wave-
+        // uniform: the queue state is the wave's). The DFS of one seed varies
+        // by orders of magnitude in size (repeats, and from the root every
+        // search ranks thousands of nodes at k = 3), so a launch otherwise ends
+        // with most lanes idle beside a few long ones (reference execution at
+        // C5: lanes busy 0.49). An idle lane takes the bottom (shallowest, so
+        // largest) stack entry of the r-th busy lane, with its pattern id and
+        // search by shuffle; the entry's subtree is the same DFS whichever lane
+        // runs it, so the leaves are too.
+        if (a.stealAt && qDone && !haveNext && qNext >= qEnd) {
+            const bool thief = !have;
+            const uint64_t I = __ballot(thief);
+            const uint64_t D = __ballot(have && sp > bot);
+            const uint32_t nI = (uint32_t)__popcll(I), nD = (uint32_t)__popcll(D);
+            if (nI >= a.stealAt && nD) {  // wave-uniform
+                const uint32_t n = min(nI, nD);
+                const uint32_t r = (uint32_t)__popcll(I & ltMask);
+                uint32_t donor = 0, rr = r;
+                uint64_t dm = D;
+#pragma unroll
+                for (uint32_t w = 32; w; w >>= 1) {  // the r-th set bit of D
+                    const uint32_t c = (uint32_t)__popcll(dm & ((1ull << w) - 1ull));
+                    if (rr >= c) { rr -= c; dm >>= w; donor += w; }
+                }
+                const bool takes = thief && r < n;
+                donor = takes ? donor : lane;
+                const uint32_t dPid = __shfl(pid, donor), dS = __shfl(sIdx, donor), dBot = __shfl(bot, donor);
+                if (takes) {
+                    const uint32_t dt = (threadIdx.x & ~63u) | donor;
+                    const uint32_t lv = dBot;  // < L
+                    cur = lv < ldsDepth ? lstk[lv * 256u + dt]
+                                        : a.stack[(size_t)(lv - ldsDepth) * T + (gtid & ~63u) + donor];
+                    pid = dPid;
+                    sIdx = dS;
+                    have = true;
+                }
+                // the thieves' reads complete before a donor's later pushes
+                // can reuse the level (its stack emptied and reset)
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (((D >> lane) & 1ull) && (uint32_t)__popcll(D & ltMask) < n && ++bot == L) {
+                    bot = 0;
+                    sp -= L;
+                }
+            }
         }
         if (!__any(have)) break;
         if (COUNT && lane == 0) ++cIter;
@@ -559,13 +607,8 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
                 return make_uint4(f, g, o, childMeta(pos, e, lastL, lastR, right, dl, kind));
             };
             auto push = [&](const uint4& v) {
-                if (sp < a.stackCap) {
-                    if (sp > 0) {
-                        const uint32_t i = sp - 1u;
-                        if (i < ldsDepth) lstk[i * 256u + threadIdx.x] = top;
-                        else stk[(size_t)(i - ldsDepth) * T] = top;
-                    }
-                    top = v;
+                if (sp - bot < a.stackCap) {
+                    stackPut(sp, v);
                     ++sp;
                 } else {
                     atomicOr(a.flags, 1u);

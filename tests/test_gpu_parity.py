@@ -506,6 +506,43 @@ def test_text_phase_work_stealing(gpu_device, monkeypatch, steal):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("steal", ["1", "8", "64"])
+def test_fm_phase_work_stealing(gpu_device, monkeypatch, steal):
+    """kSearchFM: idle lanes of a wave take the bottom stack entry (pattern id
+    and search by shuffle) of a busy lane once the seed queue is dry
+    (SAHARA_FM_STEAL_AT; the stack is a ring whose bottom moves up). The
+    oracle's hits whatever the threshold, in the reference execution (every
+    node ranked from the root, LF locate), FM only (no text phase) and the
+    default; the node and Occ-line counts equal those without stealing."""
+    monkeypatch.setenv("SAHARA_BATCH", "333")
+    rng = np.random.default_rng(78)
+    recs = random_records(rng, [30000, 12000], 6, repeats=True)
+    reads = mutate_reads(rng, recs, 400, 80, 3, 6)
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme("h2-k3", 0, 3, 80)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    gpu.stage(pats, scheme)
+    for mode, split in (((False, False), None), ((True, True), "0"), ((True, True), None)):
+        if split:
+            monkeypatch.setenv("SAHARA_SPLIT", split)
+        else:
+            monkeypatch.delenv("SAHARA_SPLIT", raising=False)
+        gpu.set_mode(verify=mode[0], locate_sa=mode[1])
+        counts = {}
+        for at in ("0", steal):
+            monkeypatch.setenv("SAHARA_FM_STEAL_AT", at)
+            gpu.run(count=True)
+            st = gpu.stats()
+            counts[at] = (st["nodes"], st["ext_lines"], st["hits"])
+            assert np.array_equal(hits_as_rows(gpu.fetch()), want), (mode, split, at)
+        assert counts["0"] == counts[steal], (mode, split, counts)
+    gpu.set_mode(verify=True, locate_sa=True)
+    monkeypatch.delenv("SAHARA_SPLIT", raising=False)
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, scheme)), want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,batch", [(1, "257"), (2, "257"), (5, "257"), (3, "7")])
 def test_max_hits_on_the_device(gpu_device, monkeypatch, n, batch):
     """--max_hits n limited per batch on the device (search.hip limitBatch)
