@@ -315,7 +315,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.stack = c->stack.ptr;
         a.stackCap = stackCap;
         a.stackLevels = stackLevels;
-        a.stealAt = 8;
+        // in-wave work stealing at the launch's end: in the reference execution
+        // (verify off) the FM phase is the whole search and its tail idles half
+        // the lanes (C5 2.7M -> 5.3M reads/s, C3 52.7M -> 62.7M); beside the
+        // text phase it changed nothing measurable (C5 93.4M vs 94.8M, C3
+        // within the spread; profiles/r04_fm_steal_ab.txt)
+        a.stealAt = c->verify ? 0u : 8u;
         if (const char* e = std::getenv("SAHARA_FM_STEAL_AT")) a.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
         a.hits = sl.hits.ptr;
         a.hitCap = c->hitCap;
