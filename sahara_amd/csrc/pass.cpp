@@ -5,7 +5,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <exception>
+#include <thread>
 
 #include "ctx.h"
 
@@ -127,6 +129,24 @@ void growCap(uint32_t& cap, uint32_t seen) {
     const uint64_t want = (uint64_t)seen + seen / 4 + 1024;
     if (want >= (1ull << 32) - 2) throw Error("a work buffer would exceed 2^32 entries in one batch");
     cap = std::max<uint32_t>(cap, (uint32_t)want);
+}
+
+// The finisher's waits in a streamed call. A blocking-sync wait sleeps in
+// the driver until an interrupt wakes it, which took up to ~0.4 ms here (C2:
+// the row total after a 50 us scan waited 0.07 ms in one call, 0.37 ms in the
+// next); polling the event every pollUs microseconds keeps the thread asleep
+// almost all the time and wakes within one period. pollUs 0: blocking sync.
+static void waitSleepy(hipEvent_t e, uint32_t pollUs) {
+    if (!pollUs) {
+        SH_HIP(hipEventSynchronize(e));
+        return;
+    }
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r == hipSuccess) return;
+        if (r != hipErrorNotReady) SH_HIP(r);
+        std::this_thread::sleep_for(std::chrono::microseconds(pollUs));
+    }
 }
 
 void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
@@ -439,6 +459,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // a streamed call's finisher sleeps in its waits while the calling thread
     // and the pool pack (device-resident runs spin)
     const bool sleepy = c->streaming && !serial;
+    uint32_t pollUs = 20;
+    if (const char* e = std::getenv("SAHARA_POLL_US")) pollUs = (uint32_t)std::max(0, std::atoi(e));
     auto finish = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
@@ -448,7 +470,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
         SH_HIP(hipMemcpyAsync(c->pinned + b * 16, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(sleepy ? c->evSleep[0] : c->ev[6], sC));
-        SH_HIP(hipEventSynchronize(sleepy ? c->evSleep[0] : c->ev[6]));
+        if (sleepy) waitSleepy(c->evSleep[0], pollUs);
+        else SH_HIP(hipEventSynchronize(c->ev[6]));
         c->mark("text done", b);
         const uint32_t* hs = c->pinned + b * 16;
         float ms = 0;
@@ -490,7 +513,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipMemcpyAsync(pr + 10, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));  // long, huge segments
         if (sleepy) {
             SH_HIP(hipEventRecord(c->evSleep[1], sC));
-            SH_HIP(hipEventSynchronize(c->evSleep[1]));
+            waitSleepy(c->evSleep[1], pollUs);
         } else {
             SH_HIP(hipStreamSynchronize(sC));
         }
@@ -593,7 +616,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         return true;
     };
     auto finishCheck = [&](uint64_t b) {
-        if (sleepy) SH_HIP(hipEventSynchronize(c->evSleep[2]));  // recorded beside ev[5]
+        if (sleepy) waitSleepy(c->evSleep[2], pollUs);  // recorded beside ev[5]
         SH_HIP(hipEventSynchronize(c->ev[5]));
         if (c->pinned[b * 16 + 7] & 4u) throw Error("locate walked off the SA samples (corrupt index)");
         float ms = 0;

@@ -408,7 +408,7 @@ static void submitPack(Ctx* c, uint64_t j) {
     const size_t slot = (size_t)(j % Ctx::kRingSlots);
     Ctx::PackJob& J = c->packJobs[slot];
     J.group.wait();  // (finished by its uploadChunk already; never blocks)
-    SH_HIP(hipEventSynchronize(c->ringEv[slot]));
+    if (!(U.prepacked && U.srcPinned)) SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // (pinned codes: no ring)
     const uint32_t m = c->m, sigma = c->I.sigma;
     const uint64_t r0 = j * U.chunk, r1 = std::min(U.rows, r0 + U.chunk);
     const uint64_t s0 = r0 * m, n = (r1 - r0) * m;
