@@ -346,6 +346,8 @@ struct Ctx {
     struct Slot {
         DevBuf<uint4> hits, tasks, seeds;  // seeds: starting cursors (kSeedItems -> kSearchFM)
         DevBuf<uint32_t> seedItem;
+        DevBuf<uint32_t> qcnt, rank;      // rows ranked at emission: per-query row counts (zero between
+                                          // batches), per hit slot its first row's place in its segment
         DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
         DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512),
                                           // [512, 768) (batch 0's second launch)
@@ -375,8 +377,7 @@ struct Ctx {
     DevBuf<unsigned long long> counters;  // nodes, rank nodes, lines, lf steps, digest, text nodes, tasks
     DevBuf<uint64_t> qoff, k0, k1;        // per-query row segments of a batch; locate keys
     DevBuf<uint64_t> partial;             // tile sums of the segment scan
-    DevBuf<uint32_t> qcnt, big, huge;     // per-query row counts (zero between batches); long / huge segments
-    DevBuf<uint32_t> hrank;               // per reported cursor: its first row's slot in its query's segment
+    DevBuf<uint32_t> big, huge;           // long / huge segments
     DevBuf<char> tmp;
     DevBuf<sahara_hit> out;
     uint64_t nout = 0;

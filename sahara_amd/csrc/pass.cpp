@@ -281,13 +281,21 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->pinnedCap = nbatch * 16;
         SH_HIP(hipHostMalloc(&c->pinned, c->pinnedCap * sizeof(uint32_t)));
     }
-    if (c->qcnt.cap < maxBatch + 1) {
-        c->qcnt.reserve(maxBatch + 1);
+    if (c->qoff.cap < maxBatch + 1) {
         c->qoff.reserve(maxBatch + 1);
         c->big.reserve(maxBatch);
         c->huge.reserve(maxBatch);
     }
-    SH_HIP(hipMemsetAsync(c->qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
+    // The search kernels rank each hit's rows in its query's segment as they
+    // write it (an atomic add on the slot's per-query count), so the locate
+    // chain starts at the scan. Until r4 a pass of scattered atomics in the
+    // chain (kCountRows) did it, beside the next batches' search, where the
+    // chain lagged behind them: C3 805M -> 843M, C2 482M -> 503M, C5 94.2M ->
+    // 95.6M reads/s (profiles/r04_emit_rank_ab.txt)
+    for (auto& sl : c->slot) {
+        sl.qcnt.reserve(maxBatch + 1);
+        SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
+    }
     hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
     c->mark("pass", 0);
     SH_HIP(hipStreamSynchronize(c->st));
@@ -314,6 +322,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
         sl.hits.reserve((size_t)c->hitCap + 1);
+        sl.rank.reserve((size_t)c->hitCap + 1);
         sl.tasks.reserve((size_t)c->taskCap);
         SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
         SearchArgs a{};
@@ -349,6 +358,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         a.taskCap = c->taskCap;
         a.split = split;
         a.ldsDepth = fmLdsDepth;
+        a.qcnt = sl.qcnt.ptr;
+        a.rank = sl.rank.ptr;
         // starting cursors; reference execution (verify off) ranks every node
         // from the root, so it does not use the k-mer table
         SeedArgs sd{};
@@ -433,6 +444,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
             t.stealAt = 8;
             if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
+            t.qcnt = sl.qcnt.ptr;
+            t.rank = sl.rank.ptr;
             if (split0) {
                 // the first batch's seed tasks while its FM phase runs, then the
                 // tasks the FM phase appended after them
@@ -495,6 +508,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             if (hs[2] & 8u) growCap(serial ? c->taskCap : seenTask, hs[4]);
             if (hs[2] & 2u) growCap(serial ? c->hitCap : seenHit, hs[1]);
             overflow = true;
+            SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (nb + 1) * sizeof(uint32_t), sC));  // the re-run counts again
             resetSlot(sl, sC);
             return false;
         }
@@ -505,9 +519,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(c->ev[2], sC));
         SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
         c->partial.reserve(scanTiles((uint32_t)nb));
-        c->hrank.reserve(std::max<uint64_t>(nh, 1));
-        querySegments(sl.hits.ptr, nh, c->qcnt.ptr, c->hrank.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr,
-                      c->big.ptr, c->small.ptr + 4, c->huge.ptr, c->small.ptr + 5, sC);
+        querySegments(sl.qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4,
+                      c->huge.ptr, c->small.ptr + 5, sC);
         uint32_t* pr = c->pinned + b * 16;
         SH_HIP(hipMemcpyAsync(pr + 8, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipMemcpyAsync(pr + 10, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));  // long, huge segments
@@ -530,7 +543,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         la.hits = sl.hits.ptr;
         la.nhits = nh;
         la.qoff = c->qoff.ptr;
-        la.rank = c->hrank.ptr;
+        la.rank = sl.rank.ptr;
         la.occF = c->I.occF.ptr;
         for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
         la.samples = c->I.samples.ptr;

@@ -40,6 +40,11 @@ struct SearchArgs {
     uint32_t* taskCount;
     uint32_t split;          // intervals of <= split rows go to the text phase (0: never)
     uint32_t ldsDepth;       // DFS levels kept in LDS (after the scheme table; the rest spill to HBM)
+    // rows ranked where the hits are written: rank[slot] = the hit's first
+    // row in its query's segment, qcnt[qid] += len (the batch's per-query row
+    // counts, zero on entry; the locate chain's scan reads and clears them)
+    uint32_t* qcnt;
+    uint32_t* rank;
 };
 
 struct SeedArgs {
@@ -99,6 +104,8 @@ struct TextArgs {
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
+    uint32_t* qcnt;          // as SearchArgs: rows ranked where the hits are written
+    uint32_t* rank;
 };
 
 struct LocateArgs {
@@ -156,9 +163,10 @@ void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, ui
 // segments in registers, medium across a wave, long in LDS, huge by segmented
 // radix sort).
 uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
-// qcnt: all zero on entry and on return; rank: one slot per hit
-void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* rank, uint32_t nq, uint64_t* qoff,
-                   uint64_t* partial, uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st);
+// qcnt: the batch's per-query row counts, which the search kernels add up
+// as they write the hits (SearchArgs::qcnt); all zero on return
+void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
+                   uint32_t* huge, uint32_t* nhuge, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
 size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
 // long segments (> 64 rows, listed in big) are sorted in LDS, huge ones

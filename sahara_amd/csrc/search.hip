@@ -510,8 +510,12 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
             const bool leaf = have && pos == a.m;
             uint32_t slot;
             if (hitSlots.take(leaf, lane, ltMask, a.hitCount, slot) && leaf) {
-                if (slot < a.hitCap) a.hits[slot] = make_uint4(pid, cur.x, cur.z, (cur.w >> 16) & 0xFu);
-                else atomicOr(a.flags, 2u);
+                if (slot < a.hitCap) {
+                    a.hits[slot] = make_uint4(pid, cur.x, cur.z, (cur.w >> 16) & 0xFu);
+                    a.rank[slot] = atomicAdd(a.qcnt + pid, cur.z);  // its first row's place in the query's segment
+                } else {
+                    atomicOr(a.flags, 2u);
+                }
                 have = false;
                 ++filled;
             }
@@ -833,6 +837,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         }
     }
     SlotRange hitSlots;
+    uint32_t rankSlot = ~0u, rankVal = 0;  // the lane's last hit whose rank is not stored yet
     uint2 cur = make_uint2(0, 0);
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
@@ -1154,14 +1159,24 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         {
             uint32_t s;
             if (hitSlots.take(leaf, lane, ltMask, a.hitCount, s) && leaf) {
-                if (s < a.hitCap) a.hits[s] = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
-                else atomicOr(a.flags, 2u);
+                if (s < a.hitCap) {
+                    a.hits[s] = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
+                    // the hit's row ranked in its query's segment (a.qcnt):
+                    // the atomic's result is stored at the next emission, so
+                    // its round trip overlaps the micro-steps in between
+                    if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
+                    rankVal = atomicAdd(a.qcnt + pid, 1u);
+                    rankSlot = s;
+                } else {
+                    atomicOr(a.flags, 2u);
+                }
                 ++filled;
             }
         }
         if (COUNT) cyEmit += clock64() - t0;
     }
     hitSlots.close(lane, a.hits, a.hitCap);
+    if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
     if (filled) atomicAdd(a.filled, filled);  // per-lane counts
     if (__any(bad) && lane == 0) atomicOr(a.flags, 16u);
     if (COUNT) {
@@ -1180,21 +1195,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
 }
 
 // ================================================================ locate ====
-
-// Rows per query: qcnt[qid] += len for every reported cursor, and the count
-// before the add is the cursor's first slot in its query's segment (rank), so
-// that kLocate places its rows without atomics of its own. The adds execute
-// at the memory side (one 64-B request per lane for scattered qids); this is
-// the only atomic pass of the locate chain. qcnt is all zero between batches
-// (kScanTiles clears what it read).
-__global__ void kCountRows(const uint4* __restrict__ hits, uint64_t nhits, uint32_t* __restrict__ qcnt,
-                           uint32_t* __restrict__ rank) {
-    for (uint64_t h = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; h < nhits;
-         h += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 hit = hits[h];
-        if (hit.z) rank[h] = atomicAdd(qcnt + hit.x, hit.z);
-    }
-}
 
 // Segment tiers: <= kSmallSeg rows sorted in a lane's registers,
 // <= kMediumSeg by a wave (one key per lane, bitonic over shuffles), longer
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, ui
 
 // One lane per reported cursor: locate every row of [lb, lb+len) into the
 // query's segment [qoff[qid], qoff[qid+1]) of the key array (key = text
-// position << 4 | e), from the slot kCountRows ranked it at.
+// position << 4 | e), from the slot the search kernel ranked it at (rank).
 template <bool COUNT>
 __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
     uint64_t steps = 0;
@@ -2046,14 +2046,9 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
     SH_HIP(hipGetLastError());
 }
 
-void querySegments(const uint4* hits, uint64_t nhits, uint32_t* qcnt, uint32_t* rank, uint32_t nq, uint64_t* qoff,
-                   uint64_t* partial, uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
+void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
+                   uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
     // qcnt[nq] stays 0, so qoff[nq] = total rows
-    if (nhits) {
-        const uint64_t blocks = std::min<uint64_t>((nhits + 255) / 256, 65536);
-        hipLaunchKernelGGL(kCountRows, dim3((unsigned)blocks), dim3(256), 0, st, hits, nhits, qcnt, rank);
-        SH_HIP(hipGetLastError());
-    }
     const uint32_t n = nq + 1, tiles = (n + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, n, partial);
     hipLaunchKernelGGL(kScanPartials, dim3(1), dim3(256), 0, st, partial, tiles);
