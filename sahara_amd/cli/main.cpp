@@ -372,6 +372,36 @@ int cmdSearch(int argc, char** argv) {
     std::vector<std::tuple<std::string, double>> timing;
     StopWatch sw;
 
+    // index residency (search.cpp:162-169): one context per device, the
+    // devices loading the one mapped .idx image side by side, beside the query
+    // ingest below (the ingest runs on host threads, the load is DMA)
+    std::vector<void*> ctx(ngpu, nullptr);
+    std::vector<double> devLoad(ngpu, 0.0);
+    std::vector<std::string> loadErrs(ngpu);
+    struct Loaders {
+        MappedFile img;
+        std::vector<std::thread> th;
+        std::vector<void*>& ctx;
+        Loaders(const std::string& path, std::vector<void*>& c) : img(path), ctx(c) {}
+        void join() {
+            for (auto& t : th)
+                if (t.joinable()) t.join();
+        }
+        ~Loaders() {  // also on an exception: the contexts close after their loads end
+            join();
+            for (void*& c : ctx) {
+                sahara_gpu_close(c);
+                c = nullptr;
+            }
+        }
+    } L(index.value, ctx);
+    const auto loadStart = std::chrono::steady_clock::now();
+    for (uint32_t g = 0; g < ngpu; ++g)
+        L.th.emplace_back([&, g] {
+            if (sahara_gpu_open((int)g, L.img.data, L.img.size, &ctx[g]) != 0) loadErrs[g] = sahara_gpu_last_error();
+            devLoad[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - loadStart).count();
+        });
+
     // queries (search.cpp:111-130): parsed and verified on the host (parallel
     // whole-file ingest) straight into two bits per symbol with the N
     // positions listed (besthits: one rank per byte); the reverse-complement
@@ -420,27 +450,10 @@ int cmdSearch(int argc, char** argv) {
     }
     std::fflush(stdout);
 
-    // index residency (search.cpp:162-169): one context per device, the
-    // devices loading the one mapped .idx image side by side
-    std::vector<void*> ctx(ngpu, nullptr);
-    std::vector<double> devLoad(ngpu, 0.0);
-    {
-        MappedFile img(index.value);
-        std::vector<std::string> errs(ngpu);
-        std::vector<std::thread> th;
-        for (uint32_t g = 0; g < ngpu; ++g)
-            th.emplace_back([&, g] {
-                const auto t0 = std::chrono::steady_clock::now();
-                if (sahara_gpu_open((int)g, img.data, img.size, &ctx[g]) != 0) errs[g] = sahara_gpu_last_error();
-                devLoad[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            });
-        for (auto& t : th) t.join();
-        for (uint32_t g = 0; g < ngpu; ++g)
-            if (!errs[g].empty()) {
-                for (void* c : ctx) sahara_gpu_close(c);
-                throw CliError("loading index: " + errs[g]);
-            }
-    }
+    // the index: whatever of its load the ingest did not hide
+    L.join();
+    for (uint32_t g = 0; g < ngpu; ++g)
+        if (!loadErrs[g].empty()) throw CliError("loading index: " + loadErrs[g]);
     if (fmOnly.given)
         for (void* c : ctx) check(sahara_gpu_set_mode(c, 0, 0), "set mode");
     sahara_index_info info{};
@@ -605,7 +618,10 @@ int cmdSearch(int argc, char** argv) {
     writeHits(output.value, parts, emitErr.given, nt);
     for (auto& hp : parts) hp.release();
     timing.emplace_back("result", sw.reset());
-    for (void* c : ctx) sahara_gpu_close(c);
+    for (void*& c : ctx) {
+        sahara_gpu_close(c);
+        c = nullptr;
+    }
 
     std::printf("stats:\n");
     double total = 0;
@@ -616,6 +632,10 @@ int cmdSearch(int argc, char** argv) {
     std::printf("  total time:          %10.2fs\n", total);
     std::printf("  queries per second:  %10.0fq/s\n", (double)nq / total);
     std::printf("  number of hits:      %10llu\n", (unsigned long long)nhits);
+    // the index loads beside the query ingest: "ld index" above is the part of
+    // its load the ingest did not hide; this is its whole load
+    std::printf("  index load:          %10.2fs (beside ld queries)\n",
+                *std::max_element(devLoad.begin(), devLoad.end()));
     if (ngpu > 1)  // --gpus N: each device's index load and search (an imbalance shows by name)
         for (uint32_t g = 0; g < ngpu; ++g)
             std::printf("  device %u:            ld index %.2fs, search %.2fs, hits %llu\n", g, devLoad[g],
