@@ -444,8 +444,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
             t.stealAt = 8;
             if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-            t.deferStart = 1;
-            if (const char* e = std::getenv("SAHARA_DEFER_START")) t.deferStart = std::atoi(e) != 0;
             t.qcnt = sl.qcnt.ptr;
             t.rank = sl.rank.ptr;
             if (split0) {

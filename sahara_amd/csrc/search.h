@@ -104,8 +104,6 @@ struct TextArgs {
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
-    uint32_t deferStart;     // 1: a task start's loads are issued before the wave's micro-steps and land in
-                             // LDS after them (compile-time shape 1 only)
     uint32_t* qcnt;          // as SearchArgs: rows ranked where the hits are written
     uint32_t* rank;
 };

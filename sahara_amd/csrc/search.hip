@@ -772,10 +772,9 @@ __device__ __forceinline__ void copyBlocksShifted(uint32_t* DA, __amdgpu_buffer_
 // VGPRs; C3 850-863M -> 886-893M reads/s).
 //   1: window 4 blocks at an exact start, pattern 4 blocks (C2, C3: m = 100)
 //   2: window 9 blocks block-aligned, pattern 8 blocks (C5: m = 250, k = 3)
-//   3: shape 1 with deferred task starts (TextArgs::deferStart)
 struct TextShape { uint32_t win, pat; bool exact; };
 __host__ __device__ constexpr TextShape textShape(int shape) {
-    return shape == 1 || shape == 3 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
+    return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
 template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
@@ -840,14 +839,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     SlotRange hitSlots;
     uint32_t rankSlot = ~0u, rankVal = 0;  // the lane's last hit whose rank is not stored yet
     uint2 cur = make_uint2(0, 0);
-    // Deferred task starts (shape 3): a refill issues the new tasks' window
-    // and pattern loads into registers and the wave goes on with its busy
-    // lanes' micro-steps; the blocks land in the new lanes' LDS slots after
-    // them, so the wave does not stall on the refill's round trip.
-    constexpr bool kDefer = SHAPE == 3;
-    bool starting = false;
-    uint32_t dsh = 0;
-    decltype(__builtin_amdgcn_raw_buffer_load_b96(textBuf, 0u, 0, 0)) dva[kDefer ? 5 : 1], dvb[kDefer ? 4 : 1];
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
 
@@ -856,9 +847,9 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         // stalls the whole wave, so idle lanes are refilled in batches: once
         // refillAt lanes are idle (or nothing else is left).
         if (COUNT) t0 = clock64();
-        const bool idle = !have && sp == 0 && !exhausted && !starting;
+        const bool idle = !have && sp == 0 && !exhausted;
         const uint64_t idleMask = __ballot(idle);
-        const bool busy = __any(have || sp > 0 || starting);
+        const bool busy = __any(have || sp > 0);
         const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
         const bool need = refill && idle;
         uint64_t pending = refill ? idleMask : 0ull;
@@ -906,14 +897,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
                 wb = x > left ? x - left : 0u;  // window start
-                if (kDefer) {  // loads now, LDS stores after the micro-steps
-                    const uint32_t offA = (wb >> 5) * 16u, offB = pid * patBlocks * 16u;
-#pragma unroll
-                    for (uint32_t j = 0; j < 5; ++j) dva[j] = __builtin_amdgcn_raw_buffer_load_b96(textBuf, offA + 16u * j, 0, 0);
-#pragma unroll
-                    for (uint32_t j = 0; j < 4; ++j) dvb[j] = __builtin_amdgcn_raw_buffer_load_b96(patBuf, offB + 16u * j, 0, 0);
-                    dsh = wb & 31u;
-                } else if (exactWindow) {       // at wb: m + 2k symbols fit in winBlocks blocks
+                if (exactWindow) {              // at wb: m + 2k symbols fit in winBlocks blocks
                     copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
                                       pid * patBlocks * 16u, patBlocks);
                 } else {                        // at the block start below wb (31 more symbols)
@@ -921,13 +905,12 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
                 }
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
-                if (kDefer) starting = true;
-                else have = true;
+                have = true;
             }
             pending &= ~__ballot(mine);
             qNext += take;
         }
-        if (qDone && !haveNext && qNext >= qEnd && need && !have && !starting) exhausted = true;
+        if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
         // ---- work stealing inside the wave once the task queue is dry (wave-
         // uniform: the queue state is the wave's). A launch ends on its longest
         // subtrees, each on one lane while the others idle (C5: lanes busy
@@ -937,7 +920,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         // window start, scheme row) by shuffle. The DFS of the entry is the
         // same whichever lane runs it, so the hits are too.
         if (a.stealAt && qDone && !haveNext && qNext >= qEnd) {
-            const bool thief = !have && sp == 0u && !starting;
+            const bool thief = !have && sp == 0u;
             const uint64_t I = __ballot(thief);
             const uint64_t D = __ballot(sp >= 2u || (sp == 1u && have));
             const uint32_t nI = (uint32_t)__popcll(I), nD = (uint32_t)__popcll(D);
@@ -977,7 +960,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 }
             }
         }
-        if (!__any(have || sp > 0 || starting || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
+        if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);
             if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
@@ -1167,21 +1150,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 cCmp += (node && forced) ? 1u : 0u;
                 cSteps += node ? 1u : 0u;
             }
-        }
-        if (kDefer && starting) {  // the deferred starts' blocks into their lanes' slots
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                uint32_t* D = W + 3u * j * 256u;
-                D[0] = __builtin_amdgcn_alignbit(dva[j + 1][0], dva[j][0], dsh);
-                D[256] = __builtin_amdgcn_alignbit(dva[j + 1][1], dva[j][1], dsh);
-                D[512] = __builtin_amdgcn_alignbit(dva[j + 1][2], dva[j][2], dsh);
-                uint32_t* E = P + 3u * j * 256u;
-                E[0] = dvb[j][0];
-                E[256] = dvb[j][1];
-                E[512] = dvb[j][2];
-            }
-            starting = false;
-            have = true;
         }
         if (COUNT) {
             const uint64_t t1 = clock64();
@@ -1716,8 +1684,7 @@ void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     const int shape = textShapeOf(a);
-    if (shape == 1 && a.deferStart) launchTextShaped<SIGMA, 3>(a, edit, count, grid, lds, st);
-    else if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
+    if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
     else if (shape == 2) launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
     else launchTextShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
 }
