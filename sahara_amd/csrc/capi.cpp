@@ -178,16 +178,7 @@ Ctx* newCtx(int device) {
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    {
-        // (A/B) SAHARA_TEXT_PRIO=1: the text stream at the highest priority, so
-        // that its launch's workgroups go first when CU slots free up
-        const char* pe = std::getenv("SAHARA_TEXT_PRIO");
-        int lo = 0, hi = 0;
-        if (pe && std::atoi(pe) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-            SH_HIP(hipStreamCreateWithPriority(&c->stB, hipStreamNonBlocking, hi));
-        else
-            SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
-    }
+    SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stD, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
