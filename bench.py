@@ -399,10 +399,17 @@ def main():
                  }
 
     extra["timed_call"] = ("sahara_gpu_search_packed_compact from host reads two bits per symbol (N listed; the "
-                           "form sahara_read_fasta form 2 produces): each chunk copied into a pinned ring and "
-                           "uploaded, RC interleave and pattern packing on the device (kPackFrom2), search, locate, "
-                           "sort, each batch's hits as 8-B records (qid, text position, e; sahara_hit_blocks) copied "
-                           "into pinned host memory recycled through sahara_gpu_free_blocks")
+                           "form sahara_read_fasta form 2 produces, in page-locked memory): each chunk DMAed straight "
+                           "from the caller's buffer, RC interleave and pattern packing on the device (kPackFrom2), "
+                           "search, locate, sort, each batch's hits as 8-B records (qid, text position, e; "
+                           "sahara_hit_blocks) copied into pinned host memory recycled through sahara_gpu_free_blocks")
+    # the timed calls' own launches, timed with HIP events on their streams
+    # (comparable with a rocprofv3 kernel trace of this same command)
+    extra["timed_launches"] = {
+        "kSearchText": {"launches_per_step": text_launches / args.steps,
+                        "avg_launch_ms": round(text_ms / max(1, text_launches), 4)},
+        "kSearchFM": {"launches_per_step": launches / args.steps,
+                      "avg_launch_ms": round(search_ms / max(1, launches), 4)}}
     extra["same_hits"] = same_hits
     if dr_elapsed:
         extra["device_resident"] = {
