@@ -185,7 +185,27 @@ def main():
 
     # ---- the headline: SURVEY §8(d)'s search wall time per call, host reads
     # (packed) in, every located hit in host memory out
-    packed_call = lambda: sa.search_packed_compact(idx, packed, scheme, edit=edit)  # noqa: E731
+    # (a multi-part index, C6: whole 24-B records, sahara_gpu_search_packed;
+    # compact records address one part's text)
+    multi_part = info["n_parts"] > 1
+
+    class _Whole:  # the whole-records call's result with CompactHits' surface
+        def __init__(self, hits):
+            self.hits = hits
+
+        def close(self):
+            pass
+
+        def __len__(self):
+            return len(self.hits)
+
+        def to_hits(self):
+            return self.hits
+
+    if multi_part:
+        packed_call = lambda: _Whole(sa.search_packed(idx, packed, scheme, edit=edit))  # noqa: E731
+    else:
+        packed_call = lambda: sa.search_packed_compact(idx, packed, scheme, edit=edit)  # noqa: E731
     step_stats = {"search_ms": 0.0, "text_ms": 0.0, "locate_ms": 0.0, "sort_ms": 0.0, "seed_ms": 0.0,
                   "stage_ms": 0.0, "output_ms": 0.0, "search_launches": 0, "text_launches": 0}
     h = None
@@ -403,6 +423,9 @@ def main():
                            "from the caller's buffer, RC interleave and pattern packing on the device (kPackFrom2), "
                            "search, locate, sort, each batch's hits as 8-B records (qid, text position, e; "
                            "sahara_hit_blocks) copied into pinned host memory recycled through sahara_gpu_free_blocks")
+    if multi_part:
+        extra["timed_call"] = extra["timed_call"].replace("sahara_gpu_search_packed_compact", "sahara_gpu_search_packed")
+        extra["timed_call"] += "; multi-part index: whole 24-B hit records (compact records address one part)"
     # the timed calls' own launches, timed with HIP events on their streams
     # (comparable with a rocprofv3 kernel trace of this same command)
     extra["timed_launches"] = {
