@@ -202,7 +202,7 @@ Ctx* newCtx(int device) {
             raw->downRing = nullptr;  // no compact download: hits go to a pinned sink whole
     });
     for (auto& sl : c->slot) {
-        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.fmBegin, &sl.fmDone, &sl.textStart, &sl.textMid0,
+        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.seedDone0, &sl.fmBegin, &sl.fmDone, &sl.textStart, &sl.textMid0,
                               &sl.textMid1, &sl.textDone, &sl.free})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);

@@ -355,7 +355,7 @@ struct Ctx {
         // its launch(es): seeds fmStart..seedDone (sD), FM fmBegin..fmDone
         // (sA), text textStart..textDone, or for the first batch's two text
         // launches textStart..textMid0 and textMid1..textDone (sB)
-        hipEvent_t fmStart = nullptr, seedDone = nullptr, fmBegin = nullptr, fmDone = nullptr, textStart = nullptr,
+        hipEvent_t fmStart = nullptr, seedDone = nullptr, seedDone0 = nullptr, fmBegin = nullptr, fmDone = nullptr, textStart = nullptr,
                    textMid0 = nullptr, textMid1 = nullptr, textDone = nullptr, free = nullptr;
         bool twoText = false;
     } slot[kSlots];
@@ -515,7 +515,7 @@ struct Ctx {
         }
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
-            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
+            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.seedDone0, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
                                  sl.textMid1, sl.textDone, sl.free})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);

@@ -227,10 +227,20 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, textLds), std::atoi(e)));
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     // (pipelined) the first batch's text phase starts on its seed tasks while
-    // its FM phase runs; only with several batches: a lone batch's FM phase
+    // its FM phase runs; a device-resident lone batch does not: its FM phase
     // runs at full occupancy, and its text phase split in two measured 45M
-    // against 68M reads/s at C5
-    const bool early = !serial && split && batchesHere > 1;
+    // against 68M reads/s at C5 (r1)
+    // A streamed call seeds its first batch in two parts, the first chunk's
+    // as soon as that chunk is up, and starts the text phase on their tasks
+    // while the rest of the batch uploads, seeds and runs its FM phase, also
+    // when the call is one batch (C5 95.2M -> 100.2M, C2 500M -> 503M, C3
+    // 792M -> 805M; without the split seeds a lone batch's early text phase
+    // lost: C5 89.9M, C2 475M; profiles/r04_chunk_seeds_ab.txt).
+    // SAHARA_CHUNK_SEEDS=0: one seed launch per batch
+    const char* csEnv = std::getenv("SAHARA_CHUNK_SEEDS");
+    const bool chunkSeeds = c->streaming && !serial && split && !(csEnv && std::atoi(csEnv) == 0);
+    const bool early = !serial && split && (batchesHere > 1 || chunkSeeds);
+    const bool chunked0 = early && chunkSeeds;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -392,11 +402,31 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamWaitEvent(sD, sl.free, 0));
         // streamed upload: the batch's patterns (packed here on the host while
         // the batches before it search; unpacked on sD ahead of its seeds)
-        ensureUploaded(c, bstart[b + 1], sD);
-        SH_HIP(hipEventRecord(sl.fmStart, sD));
-        launchSeeds(sd, sigma, std::min<uint32_t>((a.nitems + 1023) / 1024, (uint32_t)c->numCU * 8), sD);
-        if (early && b == 0)  // the seed tasks end here: the text phase may start on them
+        auto seeds = [&](uint32_t i0, uint32_t i1) {
+            sd.itemBegin = i0;
+            sd.nitems = i1;
+            launchSeeds(sd, sigma, std::max<uint32_t>(1, std::min<uint32_t>((i1 - i0 + 1023) / 1024, (uint32_t)c->numCU * 8)), sD);
+        };
+        if (chunked0 && b == 0) {
+            // (streamed, early text) the first chunk's seeds as soon as it is
+            // up; the text phase starts on their tasks while the rest of the
+            // batch uploads, seeds and runs its FM phase
+            const uint64_t p1 = std::min<uint64_t>(bstart[1], c->up.rc ? 2 * c->up.chunk : c->up.chunk);
+            ensureUploaded(c, p1, sD);
+            SH_HIP(hipEventRecord(sl.fmStart, sD));
+            seeds(0, (uint32_t)(p1 * c->nsearch));
             SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+            SH_HIP(hipEventRecord(sl.seedDone0, sD));
+            ensureUploaded(c, bstart[b + 1], sD);
+            seeds((uint32_t)(p1 * c->nsearch), a.nitems);
+        } else {
+            ensureUploaded(c, bstart[b + 1], sD);
+            SH_HIP(hipEventRecord(sl.fmStart, sD));
+            seeds(0, a.nitems);
+            if (early && b == 0)  // the seed tasks end here: the text phase may start on them
+                SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+            SH_HIP(hipEventRecord(sl.seedDone0, sD));
+        }
         SH_HIP(hipEventRecord(sl.seedDone, sD));
         SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
         SH_HIP(hipEventRecord(sl.fmBegin, sA));
@@ -408,7 +438,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b];
         const bool split0 = early && b == 0;
-        SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone : sl.fmDone, 0));
+        SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone0 : sl.fmDone, 0));
         SH_HIP(hipEventRecord(sl.textStart, sB));
         sl.twoText = split && split0;
         if (split) {

@@ -51,6 +51,7 @@ struct SeedArgs {
     const uint32_t* pats;
     uint32_t patWords;
     uint32_t nsearch;
+    uint32_t itemBegin;         // items [itemBegin, nitems) of the batch (a batch's seeds in parts)
     uint32_t nitems;
     uint32_t n;
     const uint4* kmer;          // k-mer table (DeviceIndex::kmer), nullptr = start every item at the root

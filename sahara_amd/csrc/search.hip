@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t ltMask = (1ull << lane) - 1ull;
     uint64_t cTasks = 0;
-    for (uint32_t base = blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
+    for (uint32_t base = a.itemBegin + blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
         uint4 cur[4];
         bool keep[4], task[4];
 #pragma unroll

@@ -161,3 +161,28 @@ def test_packed_from_fasta_and_dna4(gpu_device, tmp_path):
         again = sa.search_packed_compact(gpu, pk, sch)  # still usable
         assert len(again) == len(sa.search_reads(gpu, reads, sch))
         again.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"SAHARA_CHUNK_SEEDS": "0"}, {"SAHARA_BATCH": "997"},
+                                 {"SAHARA_CHUNK_SEEDS": "0", "SAHARA_BATCH": "997"}])
+def test_packed_first_batch_seeds_in_parts(gpu_device, monkeypatch, env):
+    """The first batch's text phase started on its seed tasks (also for a lone
+    batch), its seeds in two parts: the first chunk's as soon as it is up,
+    the rest after (small chunks, so the split falls inside the batch); and
+    with one seed launch per batch (SAHARA_CHUNK_SEEDS=0)."""
+    monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "150")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    flat, lens, reads, sch = _setup(n_reads=1200)
+    gpu = sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=gpu_device)
+    want = _ordered(sa.search_reads(gpu, reads, sch))
+    pk = sa.pack_reads(reads, 6, pinned=True)
+    for _ in range(2):
+        got = sa.search_packed_compact(gpu, pk, sch)
+        assert np.array_equal(_ordered(got.to_hits()), want)
+        got.close()
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    ref = O.Index.build([flat[offs[i]:offs[i + 1]] for i in range(len(lens))], 6, 16)
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)),
+                          hits_as_rows(ref.search(sa.interleave_rc(reads, 6), sch, nthreads=8)[0]))
