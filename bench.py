@@ -59,6 +59,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # wave64 VALU instructions per second: 256 CUs x 4 SIMDs x 2.4 GHz, one
 # instruction per SIMD every 2 cycles (MI355X_MICROARCH.md: 32 lanes/cycle)
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
+# sahara_hit (include/sahara_hip.h) as numpy: the fields hits_digest reads
+HIT_DTYPE_BENCH = np.dtype([("qid", "<u8"), ("seq_id", "<u4"), ("err", "<u4"), ("pos", "<u8")])
 
 
 def log(*a):
@@ -122,6 +124,8 @@ def main():
     args = ap.parse_args()
 
     if args.no_device_resident:
+        if args.execution == "reference":
+            ap.error("--execution reference times the device-resident pass: it cannot go with --no-device-resident")
         args.no_count = args.no_verify = args.no_e2e = args.no_ref_path = args.no_cpu = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -207,8 +211,9 @@ def main():
     else:
         packed_call = lambda: sa.search_packed_compact(idx, packed, scheme, edit=edit)  # noqa: E731
     step_stats = {"search_ms": 0.0, "text_ms": 0.0, "locate_ms": 0.0, "sort_ms": 0.0, "seed_ms": 0.0,
-                  "stage_ms": 0.0, "output_ms": 0.0, "search_launches": 0, "text_launches": 0}
+                  "stage_ms": 0.0, "output_ms": 0.0, "search_launches": 0, "text_launches": 0, "text_fallbacks": 0}
     h = None
+    last_result = None
     if args.execution != "reference":
         # two warmup calls whatever --warmup says: the first sizes the hit
         # sink from its own result, the second pins it into the pool every
@@ -232,8 +237,7 @@ def main():
         elapsed = time.perf_counter() - t0
         n_packed = len(h)
         packed_hits = h.to_hits()
-        h.close()
-        del h
+        last_result = h  # gathered to rank 0 after the timing (N > 1), then closed
 
     # ---- the same pass device-resident: reads staged in HBM, hits left there
     dr_stats = {"search_ms": 0.0, "text_ms": 0.0, "search_launches": 0, "text_launches": 0}
@@ -270,13 +274,16 @@ def main():
         elapsed = max_over_ranks(elapsed, device="cuda")  # RCCL over xGMI
         dr_elapsed = max_over_ranks(dr_elapsed, device="cuda") if dr_elapsed else None
         total_hits = sum_over_ranks(nh, device="cuda")
-        if not args.no_gather:
-            gather = gather_step(idx, nh, nreads, world, rank, barrier, dist, torch)
+        if not args.no_gather and last_result is not None:
+            gather = gather_step(last_result, getattr(last_result, "rec_starts", None), nreads, world, rank, barrier,
+                                 dist, torch)
     else:
         total_hits = nh
+    if last_result is not None:
+        last_result.close()
+        last_result = None
     same_hits = None if digest is None else (n_packed == nh and (packed_hits is None or
                                                                   hits_digest(packed_hits) == digest))
-    del packed_hits
 
     # full-size checks that do not lean on the GPU's own index: every read is
     # found where it was sampled (all ranks), and rank 0 checks the whole GPU
@@ -409,6 +416,7 @@ def main():
                  "search_launches_per_step": launches // args.steps,
                  "text_launches_per_step": text_launches // args.steps,
                  "search_grid": cnt["search_grid"], "text_grid": cnt["text_grid"],
+                 "text_fallbacks_timed": step_stats.get("text_fallbacks", 0),
                  "pipelined": bool(cnt["pipelined"]),
                  "reference_algorithm": {"ext_lines_per_read": round(ref_cnt["ext_lines"] / nreads, 1),
                                          "lf_steps_per_read": round(ref_cnt["lf_steps"] / nreads, 2),
@@ -488,7 +496,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(sa, idx, pats, scheme, edit, nreads, args.cpu_seconds)
+        cpu = cpu_baseline(sa, idx, pats, scheme, edit, nreads, args.cpu_seconds, packed_hits)
+    packed_hits = None
 
     out = {
         "metric": METRIC,
@@ -580,35 +589,67 @@ def time_ingest(sa, reads, sigma):
         os.unlink(path)
 
 
-def gather_step(idx, nh, nreads, world, rank, barrier, dist, torch, device="cuda"):
-    """the last step's hit records (24-B sahara_hit, global
-    qids) gathered to rank 0 over RCCL (xGMI), timed on its own (barrier +
-    synchronize on both sides, max over ranks) and checked record for record
-    by per-rank word sums. Not part of `value` (hits stay in HBM at N=1 too)."""
-    from sahara_amd.dist import gather_hit_records, max_over_ranks
+def gather_step(result, rec_starts, nreads, world, rank, barrier, dist, torch, device="cuda"):
+    """the last timed call's hits gathered to rank 0 over
+    RCCL (xGMI). The records are the ones sahara_gpu_search_packed_compact
+    left in this rank's host memory — 8-B compact records and their block
+    table (first qid and end of each batch) — which go host -> device, are
+    gathered to rank 0 (sahara_amd.dist.gather_compact_records) and come back
+    to its host memory there, with global qids (the rank's first pattern
+    added to its block qids). A whole-records result (multi-part index) is
+    gathered as (qid, seq_id, pos, e) rows instead. Timed on its own (barrier
+    + synchronize on both sides, max over ranks) and reported beside `value`
+    (config.hit_gather, with the rate including it); verified after the timing
+    by an order-independent digest per rank of the decoded rows."""
+    from sahara_amd.dist import gather_compact_records, gather_hits, max_over_ranks, records_to_rows
 
-    local = {}
-
-    def fill(buf):
-        idx.copy_hits(buf.data_ptr(), buf.shape[0], qid_offset=2 * nreads * rank)
-        local["sum"] = buf[:nh].sum()
-
+    qoff = 2 * nreads * rank
+    compact = hasattr(result, "recs")
+    if compact:
+        local = records_to_rows(result.recs, result.block_qid0 + np.uint64(qoff), result.block_end, rec_starts)
+    else:
+        h = result.to_hits()
+        local = np.stack([h["qid"] + np.uint64(qoff), h["seq_id"], h["pos"], h["err"]], 1).astype(np.uint64)
     barrier()
     t = time.perf_counter()
-    parts, counts = gather_hit_records(nh, fill, device=device)
+    if compact:
+        parts = gather_compact_records(result.recs, result.block_qid0, result.block_end, qoff, device=device)
+    else:
+        parts = gather_hits(local, 0, device=device)
     barrier()
     el = max_over_ranks(time.perf_counter() - t, device=device)
-    sums = [torch.zeros_like(local["sum"]) for _ in range(world)]
-    dist.all_gather(sums, local["sum"])
-    ok = None
+    mine = torch.tensor([rows_digest(local)], dtype=torch.int64, device=device)
+    digs = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(digs, mine)
+    ok, nrec = None, None
     if rank == 0:
-        ok = bool(all(int(p.sum().item()) == int(s.item()) for p, s in zip(parts, sums)))
-        qmin = [int(p[:, 0].min().item()) if len(p) else None for p in parts]
-        ok = ok and all(q is None or q >= 2 * nreads * r for r, q in enumerate(qmin))
-    nrec = sum(counts)
-    return {"ms": round(el * 1e3, 2), "records": nrec, "bytes": nrec * 24,
-            "GBs_into_rank0": round(nrec * 24 / el / 1e9, 1), "verified": ok,
-            "collective": "all_gather of counts + gather of padded 24-B records to rank 0 (RCCL over xGMI)"}
+        if compact:
+            rows = [records_to_rows(r, q0, e, rec_starts) for r, q0, e in parts]
+            nrec = sum(len(r) for r, _, _ in parts)
+            ok = all(rows_digest(x) == int(d.item()) for x, d in zip(rows, digs))
+            ok = ok and all(len(x) == 0 or int(x[:, 0].min()) >= 2 * nreads * r for r, x in enumerate(rows))
+        else:
+            nrec = len(parts)
+            ok = rows_digest(parts) % (1 << 64) == sum(int(d.item()) % (1 << 64) for d in digs) % (1 << 64)
+    rec_bytes = 8 if compact else 32
+    out = {"ms": round(el * 1e3, 2), "verified": ok,
+           "collective": ("all_gather of counts + gather of the 8-B compact records and of the block tables to rank "
+                          "0 (RCCL over xGMI); host -> device before, device -> host on rank 0 after, inside the "
+                          "timing") if compact else "all_gather of (qid, seq_id, pos, e) rows (RCCL over xGMI)",
+           "source": "the last timed call's result (host memory)"}
+    if rank == 0:
+        out.update({"records": nrec, "bytes": nrec * rec_bytes, "GBs_into_rank0": round(nrec * rec_bytes / el / 1e9, 1)})
+    return out
+
+
+def rows_digest(rows):
+    """hits_digest over (n, 4) u64 rows (qid, seq_id, pos, e), as a signed
+    int64 (a torch tensor's word)."""
+    rows = np.asarray(rows, np.uint64).reshape(-1, 4)
+    h = np.zeros(len(rows), HIT_DTYPE_BENCH)
+    h["qid"], h["seq_id"], h["pos"], h["err"] = rows[:, 0], rows[:, 1], rows[:, 2], rows[:, 3]
+    d = hits_digest(h)
+    return d - (1 << 64) if d >= (1 << 63) else d
 
 
 def origin_recall(h, origin, k):
@@ -873,8 +914,11 @@ def reference_path(idx, ref_cnt, nreads, pat_bytes, steps, world, barrier, confi
     return out
 
 
-def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):
-    """Time the CPU restatement on a bounded sample; check GPU == CPU on it."""
+def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s, timed_hits=None):
+    """Time the CPU restatement on a bounded sample; check GPU == CPU on it:
+    `timed_hits` (the last timed call's hits, decoded; sorted by qid) cut to
+    the sample's queries — the headline call at its default chunking and
+    batching — and the patterns call (sahara_gpu_search) over the sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -923,17 +967,31 @@ def cpu_baseline(sa, idx, pats, scheme, edit, nreads, target_s):
     cpu_search(pats[: 2 * n1], 1)
     rate1 = n1 / (time.perf_counter() - t)
     # parity on the sample
-    gpu_hits = sa.search(idx, pats[: 2 * n2], scheme, edit=edit)
-    from_gpu = np.stack([gpu_hits["qid"], gpu_hits["seq_id"], gpu_hits["pos"], gpu_hits["err"]], 1).astype(np.uint64)
     h = hits
-    order = np.lexsort((h[:, 3], h[:, 2], h[:, 1], h[:, 0]))
-    parity = bool(len(h) == len(from_gpu) and np.array_equal(h[order], from_gpu))
+    want = h[np.lexsort((h[:, 3], h[:, 2], h[:, 1], h[:, 0]))]
+
+    def rows_of(g):
+        return np.stack([g["qid"], g["seq_id"], g["pos"], g["err"]], 1).astype(np.uint64)
+
+    gpu_hits = sa.search(idx, pats[: 2 * n2], scheme, edit=edit)
+    from_gpu = rows_of(gpu_hits)
+    parity_patterns = bool(len(want) == len(from_gpu) and np.array_equal(want, from_gpu))
+    parity = None
+    if timed_hits is not None:
+        cut = int(np.searchsorted(timed_hits["qid"], np.uint64(2 * n2)))
+        from_timed = rows_of(timed_hits[:cut])
+        parity = bool(len(want) == len(from_timed) and np.array_equal(want, from_timed))
     log(f"cpu baseline: {n2} reads in {dt:.1f}s on {threads} threads = {rate:.0f} reads/s "
-        f"(1 thread: {rate1:.0f} reads/s); GPU==CPU on sample: {parity}")
+        f"(1 thread: {rate1:.0f} reads/s); GPU==CPU on sample: timed call {parity}, patterns call {parity_patterns}")
     return {"value": round(rate, 1), "unit": "reads/s", "cores": threads, "kind": "port",
             "sample": f"first {n2} reads (+RC) of the same workload, {dt:.1f}s; "
                       f"1-thread rate {rate1:.1f} reads/s on {n1} reads; host CPU: {cpu_model()}",
-            "single_thread_value": round(rate1, 1), "parity_on_sample": parity, "index_parts": len(refs)}
+            "single_thread_value": round(rate1, 1),
+            "parity_on_sample": parity if parity is not None else parity_patterns,
+            "parity_source": ("the last timed call's records (sahara_gpu_search_packed_compact at its default chunks "
+                              "and batches), cut to the sample's queries") if parity is not None
+                             else "sahara_gpu_search over the sample",
+            "parity_patterns_call": parity_patterns, "index_parts": len(refs)}
 
 
 if __name__ == "__main__":

@@ -94,6 +94,7 @@ typedef struct sahara_stats {
     double   output_ms;          /* sahara_gpu_search: wall time of handing the hits to the host */
     uint64_t text_launches;      /* text-phase kernel launches in the pass */
     uint64_t upload_chunks[3];   /* streamed upload chunks sent at 2 / 4 / 8 bits per symbol */
+    uint64_t text_fallbacks;     /* passes whose one text launch gave up (a wait timed out) and were redone batch by batch */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);
@@ -202,6 +203,16 @@ int  sahara_gpu_search_packed_compact(void* ctx, const uint8_t* codes, uint64_t 
                                       uint64_t n_count, uint64_t n_reads, uint32_t len, int reverse, uint64_t limit,
                                       const uint32_t* pi, const uint32_t* l, const uint32_t* u,
                                       uint32_t n_searches, int edit, sahara_hit_blocks* out);
+/* Optional: a context's first search call does one-time work later calls
+ * skip — the page-locked hit sink, the device buffers of the streamed pass.
+ * A one-shot process (`sahara search`) can do it ahead, beside other work
+ * (reading its queries): a sink for the hits of n_patterns patterns (as the
+ * first compact call sizes it: two per pattern) pinned into the library's
+ * pool, and the pass's device buffers for n_patterns patterns of length len
+ * (0: unknown, those are left to the call). ctx NULL: the sink only (it
+ * needs no device, so it can be pinned while the index loads). Results never
+ * depend on it. */
+int  sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len);
 /* --search_mode besthits (search_ng21::search_best[_n], search.cpp:233-241):
  * n_schemes expanded schemes, scheme j covering exactly j errors, stored one
  * after another in pi/l/u (n_searches[j] rows of len entries each). A pattern's

@@ -77,7 +77,7 @@ class Stats(C.Structure):
                 ("text_compare_steps", C.c_uint64), ("text_grid", C.c_uint32), ("pipelined", C.c_uint32),
                 ("seed_ms", C.c_double), ("text_steps", C.c_uint64), ("stage_ms", C.c_double),
                 ("output_ms", C.c_double), ("text_launches", C.c_uint64),
-                ("upload_chunks", C.c_uint64 * 3)]
+                ("upload_chunks", C.c_uint64 * 3), ("text_fallbacks", C.c_uint64)]
 
     def as_dict(self):
         return {n: (list(v) if isinstance(v, C.Array) else v) for n, v in
@@ -112,6 +112,7 @@ EXPORTED = {
     "sahara_gpu_search_packed": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u64p, C.c_uint64, C.c_uint64, C.c_uint32,
                                            C.c_int, C.c_uint64, u32p, u32p, u32p, C.c_uint32, C.c_int, C.c_uint32,
                                            C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "sahara_gpu_prepare": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32]),
     "sahara_gpu_search_packed_compact": (C.c_int, [C.c_void_p, u8p, C.c_uint64, u64p, C.c_uint64, C.c_uint64,
                                                    C.c_uint32, C.c_int, C.c_uint64, u32p, u32p, u32p, C.c_uint32,
                                                    C.c_int, C.POINTER(HitBlocks)]),
@@ -325,6 +326,11 @@ class BiFMIndex:
         _check(lib().sahara_gpu_placement(self._h, C.byref(d), C.byref(node), C.byref(ncpu)))
         return {"device": d.value, "numa_node": node.value, "n_cpus": ncpu.value}
 
+    def prepare(self, n_patterns, length=0):
+        """sahara_gpu_prepare: the first search call's one-time work ahead
+        (pinned hit sink, device buffers of the streamed pass)."""
+        _check(lib().sahara_gpu_prepare(self._h, int(n_patterns), int(length)))
+
     def stats(self):
         s = Stats()
         _check(lib().sahara_gpu_stats(self._h, C.byref(s)))
@@ -439,8 +445,10 @@ class CompactHits:
     """Hits of sahara_gpu_search_reads_compact (include/sahara_hip.h
     sahara_hit_blocks): 8-B records in page-locked host memory, one block per
     batch. `recs` is a read-only zero-copy view that keeps the memory alive;
-    close() releases the memory at once, after which views taken earlier must
-    not be read (copy them first). to_hits() expands the records to HIT_DTYPE."""
+    close() drops this object's hold on it: the memory goes back to the
+    library's pool at once, unless a view of `recs` taken earlier is still
+    alive, which keeps it until that view goes. to_hits() expands the records
+    to HIT_DTYPE."""
 
     def __init__(self, blocks, index):
         self._own = _Blocks(blocks)
@@ -479,7 +487,7 @@ class CompactHits:
     def close(self):
         if self._b is not None:
             self.recs = None
-            self._own.free()
+            self._own = None  # freed with the last reference (this one, or a view's)
             self._b = None
 
 

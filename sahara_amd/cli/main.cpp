@@ -12,6 +12,7 @@
 // locate). The compute goes through the C ABI of libsahara_hip.so only.
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <chrono>
 #include <cmath>
@@ -21,6 +22,7 @@
 #include <cstring>
 #include <fstream>
 #include <functional>
+#include <future>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -213,12 +215,16 @@ struct HitPart {
 };
 
 // Text output of hits: "qid seqId pos[ e]\n" (search.cpp:254-261). Blocks of
-// hits are formatted on nt threads, then written in order. Compact records
-// are decoded right here, in the formatting loop that runs anyway: record id
-// by the record starts (usually the previous hit's record), position, errors.
+// hits are formatted by nt threads, each taking the next block in order; a
+// block's file offset is the previous block's end, published as soon as that
+// block is formatted, so each thread writes its own block (pwrite) while the
+// others format theirs: formatting and writing both run on every thread.
+// Compact records are decoded right here, in the formatting loop that runs
+// anyway: record id by the record starts (usually the previous hit's record),
+// position, errors.
 void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool emitErrors, unsigned nt) {
-    std::FILE* f = std::fopen(path.c_str(), "w");
-    if (!f) throw CliError("can not open output file " + path);
+    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) throw CliError("can not open output file " + path);
     struct Block {
         const HitPart* part;
         uint64_t lo, hi;
@@ -227,13 +233,16 @@ void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool 
     constexpr uint64_t kBlock = 1u << 18;  // hits per block (~7 MB of text)
     for (const auto& hp : parts)
         for (uint64_t lo = 0; lo < hp.n; lo += kBlock) blocks.push_back({&hp, lo, std::min(hp.n, lo + kBlock)});
-    const size_t wave = (size_t)nt * 2;  // blocks formatted per round (bounds the memory held)
-    std::vector<std::vector<char>> text(std::min(wave, blocks.size()));
-    for (size_t b0 = 0; b0 < blocks.size(); b0 += wave) {
-        const size_t nb = std::min(wave, blocks.size() - b0);
-        parallelFor(nt, nb, [&](size_t i) {
-            const Block& B = blocks[b0 + i];
-            std::vector<char>& buf = text[i];
+    std::vector<std::atomic<int64_t>> ends(blocks.size());
+    for (auto& e : ends) e.store(-1, std::memory_order_relaxed);
+    std::atomic<size_t> next{0};
+    std::atomic<bool> failed{false};
+    parallelFor(nt, nt, [&](size_t) {
+        std::vector<char> buf;
+        for (;;) {
+            const size_t bi = next.fetch_add(1, std::memory_order_relaxed);
+            if (bi >= blocks.size()) return;
+            const Block& B = blocks[bi];
             buf.resize((B.hi - B.lo) * 96);
             char* o = buf.data();
             char* e = o + buf.size();
@@ -271,15 +280,19 @@ void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool 
                     line(H.block_qid0[blk] + (v >> 36) + P.qidOffset, seq, g - lo, (uint32_t)(v & 15u));
                 }
             }
-            buf.resize((size_t)(o - buf.data()));
-        });
-        for (size_t i = 0; i < nb; ++i)
-            if (std::fwrite(text[i].data(), 1, text[i].size(), f) != text[i].size()) {
-                std::fclose(f);
-                throw CliError("can not write output file " + path);
+            const int64_t size = (int64_t)(o - buf.data());
+            int64_t off = 0;
+            if (bi > 0)
+                while ((off = ends[bi - 1].load(std::memory_order_acquire)) < 0) std::this_thread::yield();
+            ends[bi].store(off + size, std::memory_order_release);
+            for (int64_t done = 0; done < size && !failed.load(std::memory_order_relaxed);) {
+                const ssize_t w = ::pwrite(fd, buf.data() + done, (size_t)(size - done), off + done);
+                if (w <= 0) failed.store(true);
+                else done += w;
             }
-    }
-    if (std::fclose(f) != 0) throw CliError("can not write output file " + path);
+        }
+    });
+    if (::close(fd) != 0 || failed.load()) throw CliError("can not write output file " + path);
 }
 
 // A read-only mapping of a whole file (the .idx image every device loads).
@@ -307,6 +320,33 @@ struct MappedFile {
     MappedFile(const MappedFile&) = delete;
     MappedFile& operator=(const MappedFile&) = delete;
 };
+
+// Reads in a FASTA file and their length, estimated from its first 256 KB
+// and its size (sahara_gpu_prepare's sizes; 0 when unknown). Errs high.
+struct QueryEstimate {
+    uint64_t reads = 0;
+    uint32_t len = 0;
+};
+QueryEstimate estimateQueries(const std::string& path) {
+    QueryEstimate q;
+    struct stat sb {};
+    if (::stat(path.c_str(), &sb) != 0 || sb.st_size <= 0) return q;
+    std::ifstream f(path, std::ios::binary);
+    std::vector<char> buf(256u << 10);
+    f.read(buf.data(), (std::streamsize)buf.size());
+    const size_t n = (size_t)f.gcount();
+    std::vector<size_t> heads;  // '>' at line starts
+    for (size_t i = 0; i < n; ++i)
+        if (buf[i] == '>' && (i == 0 || buf[i - 1] == '\n')) heads.push_back(i);
+    if (heads.size() < 2) return q;
+    const double perRec = (double)(heads.back() - heads[0]) / (double)(heads.size() - 1);
+    size_t i = heads[0];
+    while (i < heads[1] && buf[i] != '\n') ++i;  // the first header line
+    for (; i < heads[1]; ++i)
+        if (buf[i] != '\n' && buf[i] != '\r') ++q.len;
+    q.reads = (uint64_t)((double)sb.st_size / perRec * 1.05) + 16;
+    return q;
+}
 
 uint64_t readSigma(const std::string& path) {
     std::ifstream f(path, std::ios::binary);
@@ -395,11 +435,27 @@ int cmdSearch(int argc, char** argv) {
             }
         }
     } L(index.value, ctx);
+    // The search call's one-time work (the pinned hit sink, the pass's device
+    // buffers) happens here too, beside the ingest, sized by an estimate of
+    // the queries (sahara_gpu_prepare): the sink is pinned while the index
+    // loads, the buffers once it is resident. Compact records only, <= 2
+    // devices (the library's pool keeps two idle sinks).
+    const bool prepare = !besthits && mh <= 0 && ngpu <= 2;
+    const QueryEstimate qe = prepare ? estimateQueries(query.value) : QueryEstimate{};
+    uint64_t npatEst = (noRev.given ? 1 : 2) * qe.reads;
+    if (limit.given) npatEst = std::min<uint64_t>(npatEst, toU64(limit.value, "--limit_queries"));
+    npatEst = (npatEst + ngpu - 1) / ngpu + 2;
+    std::shared_future<void> pinned;
+    if (qe.reads) pinned = std::async(std::launch::async, [npatEst] { (void)sahara_gpu_prepare(nullptr, npatEst, 0); }).share();
     const auto loadStart = std::chrono::steady_clock::now();
     for (uint32_t g = 0; g < ngpu; ++g)
         L.th.emplace_back([&, g] {
             if (sahara_gpu_open((int)g, L.img.data, L.img.size, &ctx[g]) != 0) loadErrs[g] = sahara_gpu_last_error();
             devLoad[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - loadStart).count();
+            if (qe.reads && ctx[g]) {
+                pinned.wait();
+                (void)sahara_gpu_prepare(ctx[g], npatEst, qe.len);  // a failure only costs the call its time
+            }
         });
 
     // queries (search.cpp:111-130): parsed and verified on the host (parallel

@@ -178,12 +178,25 @@ Ctx* newCtx(int device) {
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
+    // the text stream gets a hardware queue of its own (a stream with a CU
+    // mask is never given a shared queue): its one launch per pass waits for
+    // the seed and FM kernels, which must not queue behind it
+    {
+        std::vector<uint32_t> mask((size_t)(c->numCU + 31) / 32, 0xFFFFFFFFu);
+        if (hipExtStreamCreateWithCUMask(&c->stB, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+            c->textOwnQueue = true;
+        } else {
+            (void)hipGetLastError();
+            SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
+        }
+    }
     SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stD, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stF, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
+    SH_HIP(hipEventCreate(&c->txStart));
+    SH_HIP(hipEventCreate(&c->txEnd));
     for (auto& e : c->evSleep) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     for (auto& e : c->ringEv) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // the streamed upload's pinned ring, pinned while the caller builds or
@@ -202,8 +215,8 @@ Ctx* newCtx(int device) {
             raw->downRing = nullptr;  // no compact download: hits go to a pinned sink whole
     });
     for (auto& sl : c->slot) {
-        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.seedDone0, &sl.fmBegin, &sl.fmDone, &sl.textStart, &sl.textMid0,
-                              &sl.textMid1, &sl.textDone, &sl.free})
+        for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.seedDone0, &sl.seedMid, &sl.fmBegin, &sl.fmDone,
+                              &sl.textStart, &sl.textDone, &sl.free})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);
         sl.queues.reserve(768);
@@ -965,6 +978,55 @@ int sahara_gpu_search_packed_compact(void* ctx, const uint8_t* codes, uint64_t s
         if (!codes || (n_count && !n_pos)) throw Error("sahara_gpu_search_packed_compact: null input");
         const PackedReads pk{sym0, n_pos, n_count};
         searchReadsCompact(ctxOf(ctx), codes, n_reads, len, reverse, limit, pi, l, u, n_searches, edit, out, &pk);
+    });
+}
+
+int sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len) {
+    return guarded([&] {
+        if (n_patterns == 0) return;
+        Ctx* c = ctx ? ctxOf(ctx) : nullptr;
+        if (c) SH_HIP(hipSetDevice(c->device));
+        // the sink the first compact call asks the pool for (searchReadsCompact),
+        // pinned now and handed back to the pool, where the call finds it
+        const uint64_t est = c && c->lastHits ? c->lastHits + c->lastHits / 8 + 1024 : 2 * n_patterns + 1024;
+        bool pinned = false;
+        size_t capBytes = 0;
+        {
+            HitPool& P = hitPool();
+            std::lock_guard<std::mutex> g(P.mu);
+            for (auto& e : P.idle)
+                if (e.second >= est * 8) {  // pinned already (a NULL-context call before)
+                    pinned = true;
+                    capBytes = e.second;
+                }
+        }
+        if (!pinned) {
+            void* p = allocPinned(est * 8, &pinned, &capBytes, true, true);
+            if (!p) throw Error("out of host memory for hits");
+            freeHits(p);
+        }
+        if (!c) return;  // (NULL context: the host part only, e.g. beside the index load)
+        if (pinned) c->outRecs.reserve(capBytes / 8);
+        c->out.reserve(est);
+        // the slots of a streamed pass (pass.cpp runPass: 2M-pattern batches)
+        const uint64_t maxBatch = 1ull << 21;
+        if (c->hitCap == 0) c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (c->taskCap == 0) c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        const uint64_t nb = std::min<uint64_t>((n_patterns + maxBatch - 1) / maxBatch, Ctx::kSlots);
+        for (uint64_t i = 0; i < nb; ++i) {
+            Ctx::Slot& sl = c->slot[i];
+            sl.hits.reserve((size_t)c->hitCap + 1);
+            sl.rank.reserve((size_t)c->hitCap + 1);
+            sl.tasks.reserve((size_t)c->taskCap);
+            sl.qcnt.reserve(maxBatch + 1);
+        }
+        if (len) {
+            const uint64_t patWords = (len + 7) / 8, patBlocks = (len + 31) / 32;
+            c->rawPats.reserve(n_patterns * len);
+            c->pats.reserve(n_patterns * patWords + 4);
+            c->pats3.reserve(n_patterns * patBlocks);
+            c->readRaw.reserve((n_patterns + 1) / 2 * len);
+        }
     });
 }
 

@@ -349,17 +349,35 @@ struct Ctx {
         DevBuf<uint32_t> qcnt, rank;      // rows ranked at emission: per-query row counts (zero between
                                           // batches), per hit slot its first row's place in its segment
         DevBuf<uint32_t> small;           // -, hitCount, flags, filled, taskCount, seed tasks, seedCount
-        DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks [256, 512),
-                                          // [512, 768) (batch 0's second launch)
+        DevBuf<uint32_t> queues;          // striped work counters: FM seeds [0, 256), text tasks: the seed
+                                          // tasks [256, 512), the FM phase's [512, 768)
         // kernel spans, each recorded on the kernel's own stream right around
         // its launch(es): seeds fmStart..seedDone (sD), FM fmBegin..fmDone
-        // (sA), text textStart..textDone, or for the first batch's two text
-        // launches textStart..textMid0 and textMid1..textDone (sB)
-        hipEvent_t fmStart = nullptr, seedDone = nullptr, seedDone0 = nullptr, fmBegin = nullptr, fmDone = nullptr, textStart = nullptr,
-                   textMid0 = nullptr, textMid1 = nullptr, textDone = nullptr, free = nullptr;
-        bool twoText = false;
+        // (sA), text textStart..textDone (sB, one launch per batch; with one
+        // launch per pass, Ctx::txStart..txEnd); seedDone0: the batch's first
+        // seed tasks are published
+        hipEvent_t fmStart = nullptr, seedDone = nullptr, seedDone0 = nullptr, seedMid = nullptr, fmBegin = nullptr,
+                   fmDone = nullptr, textStart = nullptr, textDone = nullptr, free = nullptr;
+        bool seedsInParts = false;        // seeds in two launches: fmStart..seedDone0, seedMid..seedDone
     } slot[kSlots];
     hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
+    // The text phase of a pipelined pass is one launch (search.hip kSearchText)
+    // that takes each batch's tasks as the seed and FM streams publish them
+    // (bflags) and tells the finisher when a batch is done (hostDone, pinned).
+    // Its stream stB has a hardware queue of its own (created with a CU mask),
+    // so that no kernel it waits for can queue behind it.
+    DevBuf<uint32_t> bflags;              // per batch 4 words (TextArgs::bflags)
+    DevBuf<uint32_t> ctl;                 // [0]: abort the launch (set by an H2D copy on stE)
+    DevBuf<TextBatch> batchTab;
+    DevBuf<TextSlot> slotTab;
+    TextBatch* batchHost = nullptr;       // pinned staging of the tables
+    size_t batchHostCap = 0;
+    TextSlot* slotHost = nullptr;
+    uint32_t* hostDone = nullptr;         // pinned, per batch (TextArgs::hostDone)
+    size_t hostDoneCap = 0;
+    uint32_t* ctlHost = nullptr;          // pinned: the abort word's source (1)
+    hipEvent_t txStart = nullptr, txEnd = nullptr;  // around the pass's text launch
+    bool textOwnQueue = false;            // stB was created with its own hardware queue
     uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
     // two pinned staging chunks for handing hits to pageable host memory: the
     // DMA of one chunk overlaps the host copy out of the other (copyOut)
@@ -515,10 +533,16 @@ struct Ctx {
         }
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
-            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.seedDone0, sl.fmBegin, sl.fmDone, sl.textStart, sl.textMid0,
-                                 sl.textMid1, sl.textDone, sl.free})
+            for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.seedDone0, sl.seedMid, sl.fmBegin, sl.fmDone, sl.textStart,
+                                 sl.textDone, sl.free})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
+        if (batchHost) (void)hipHostFree(batchHost);
+        if (slotHost) (void)hipHostFree(slotHost);
+        if (hostDone) (void)hipHostFree(hostDone);
+        if (ctlHost) (void)hipHostFree(ctlHost);
+        if (txStart) (void)hipEventDestroy(txStart);
+        if (txEnd) (void)hipEventDestroy(txEnd);
         if (nibHost) (void)hipHostFree(nibHost);
         for (void* p : outStage)
             if (p) (void)hipHostFree(p);

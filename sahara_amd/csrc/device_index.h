@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -23,6 +24,50 @@ struct Error : std::runtime_error {
                                   "' at " __FILE__ ":" + std::to_string(__LINE__) + ": " #expr); \
     } while (0)
 
+// hipFree synchronizes the whole device. A pipelined pass's text launch waits
+// for work the host issues during the pass (search.hip kSearchText), so a
+// buffer that grows inside the pass (locate keys, the hit output) must not be
+// freed there: the free would wait for the launch and the launch for the host.
+// While any such pass runs, frees are deferred; the last pass to end does them.
+struct FreeDeferral {
+    std::mutex mu;
+    int active = 0;
+    std::vector<void*> list;
+};
+inline FreeDeferral& freeDeferral() {
+    static FreeDeferral* d = new FreeDeferral;  // never destroyed: frees may run after static destructors
+    return *d;
+}
+inline void deviceFree(void* p) {
+    FreeDeferral& d = freeDeferral();
+    {
+        std::lock_guard<std::mutex> g(d.mu);
+        if (d.active) {
+            d.list.push_back(p);
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+struct DeferFrees {  // scope of a pass whose text launch outlives host calls
+    DeferFrees() {
+        FreeDeferral& d = freeDeferral();
+        std::lock_guard<std::mutex> g(d.mu);
+        ++d.active;
+    }
+    ~DeferFrees() {
+        FreeDeferral& d = freeDeferral();
+        std::vector<void*> drop;
+        {
+            std::lock_guard<std::mutex> g(d.mu);
+            if (--d.active == 0) drop.swap(d.list);
+        }
+        for (void* p : drop) (void)hipFree(p);
+    }
+    DeferFrees(const DeferFrees&) = delete;
+    DeferFrees& operator=(const DeferFrees&) = delete;
+};
+
 template <typename T>
 struct DevBuf {  // minimal owning device buffer that only ever grows
     T* ptr = nullptr;
@@ -34,7 +79,7 @@ struct DevBuf {  // minimal owning device buffer that only ever grows
         cap = n;
     }
     void release() {
-        if (ptr) (void)hipFree(ptr);
+        if (ptr) deviceFree(ptr);
         ptr = nullptr;
         cap = 0;
     }

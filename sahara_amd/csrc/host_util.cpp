@@ -4,7 +4,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <thread>
+#include <unordered_set>
 
 #include <hip/hip_runtime.h>
 
@@ -269,6 +271,18 @@ T* copyOut(const std::vector<T>& v) {
     if (!v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
     return p;
 }
+// the form-2 buffers sahara_read_fasta page-locked (hipHostMalloc), so that
+// sahara_free_fasta frees each the way it was allocated without asking HIP
+std::mutex g_pinnedFastaMu;
+std::unordered_set<void*> g_pinnedFasta;
+void rememberPinnedFasta(void* p) {
+    std::lock_guard<std::mutex> g(g_pinnedFastaMu);
+    g_pinnedFasta.insert(p);
+}
+bool forgetPinnedFasta(void* p) {
+    std::lock_guard<std::mutex> g(g_pinnedFastaMu);
+    return g_pinnedFasta.erase(p) != 0;
+}
 }  // namespace
 
 extern "C" {
@@ -289,6 +303,7 @@ int sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threa
                 out->data = copyOut(D.ranks);  // pageable: the calls copy it through their staging ring
             } else {
                 out->data = static_cast<uint8_t*>(p);
+                rememberPinnedFasta(p);
                 if (!D.ranks.empty()) std::memcpy(p, D.ranks.data(), D.ranks.size());
             }
         } else {
@@ -316,14 +331,10 @@ int sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threa
 
 void sahara_free_fasta(sahara_fasta* f) {
     if (!f) return;
-    hipPointerAttribute_t at{};
-    if (f->data && hipPointerGetAttributes(&at, f->data) == hipSuccess && at.type == hipMemoryTypeHost &&
-        at.hostPointer) {
-        (void)hipHostFree(f->data);
-    } else {
-        (void)hipGetLastError();
-        std::free(f->data);
-    }
+    // freed the way sahara_read_fasta allocated it (recorded there): no HIP
+    // call for a rank-form (CPU-only) ingest
+    if (f->data && forgetPinnedFasta(f->data)) (void)hipHostFree(f->data);
+    else std::free(f->data);
     std::free(f->offs);
     std::free(f->n_pos);
     std::free(f->bad_id);

@@ -80,7 +80,7 @@ void run(Ctx* c, bool count) {
                   &sahara_stats::conversions, &sahara_stats::fm_iterations, &sahara_stats::text_iterations,
                   &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
                   &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
-                  &sahara_stats::text_steps, &sahara_stats::text_launches})
+                  &sahara_stats::text_steps, &sahara_stats::text_launches, &sahara_stats::text_fallbacks})
                 T.*f += S.*f;
             for (double sahara_stats::*f : {&sahara_stats::search_ms, &sahara_stats::locate_ms, &sahara_stats::sort_ms,
                                             &sahara_stats::text_ms, &sahara_stats::seed_ms})
@@ -117,7 +117,9 @@ void runOne(Ctx* c, bool count) {
     bool overflow = false;
     runPass(c, count, !c->pipeline, S, overflow);
     if (overflow) {
+        const uint64_t fallbacks = S.text_fallbacks;
         S = sahara_stats{};
+        S.text_fallbacks = fallbacks;
         runPass(c, count, true, S, overflow);
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -225,6 +227,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // C2 950-1013M vs 956-1026M: the sign flips with the box)
     if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
     if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, textLds), std::atoi(e)));
+    // (pipelined) the text launch waits for the seed and FM kernels, which
+    // must fit beside its workgroups (count mode's kernels hold more VGPRs)
+    if (!serial && tbpc > 0)
+        tbpc = textBlocksBeside(sigma, c->edit, count, textShapeOf(winBlocks, c->patBlocks, exactWindow), textLds, lds,
+                                tbpc);
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     // (pipelined) the first batch's text phase starts on its seed tasks while
     // its FM phase runs; a device-resident lone batch does not: its FM phase
@@ -241,6 +248,15 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool chunkSeeds = c->streaming && !serial && split && !(csEnv && std::atoi(csEnv) == 0);
     const bool early = !serial && split && (batchesHere > 1 || chunkSeeds);
     const bool chunked0 = early && chunkSeeds;
+    // (pipelined) the text phase of the whole pass is one launch that takes
+    // each batch's tasks as the seed and FM streams publish them (search.hip
+    // kSearchText), so no launch boundary falls between batches: C3's call had
+    // 11% of its time between the per-batch text launches, waiting for CU slots
+    // (profiles/r04_head_c3_timeline_split.txt). SAHARA_TEXT_ONE_LAUNCH=0: one
+    // launch per batch (the same kernel over [b, b + 1)).
+    const char* olEnv = std::getenv("SAHARA_TEXT_ONE_LAUNCH");
+    const bool persist = split && !serial;
+    const bool oneLaunch = persist && !(olEnv && std::atoi(olEnv) == 0);
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -319,6 +335,58 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     c->sinkOk = c->sink != nullptr || c->blockRecs != nullptr;
     c->batchQ0.clear();
     c->batchEnd.clear();
+    // The text phase's hand-off state: per batch 4 words (zero), the batch
+    // table, the host's done words; every slot's buffers are sized before the
+    // launch, so their addresses hold for the pass (the slot table).
+    const size_t usedSlots = (size_t)std::min<uint64_t>(nbatch, Ctx::kSlots);
+    uint64_t maxItems = 0;
+    for (uint64_t b = 0; b < nbatch; ++b) maxItems = std::max(maxItems, (bstart[b + 1] - bstart[b]) * c->nsearch);
+    for (size_t i = 0; i < usedSlots; ++i) {
+        Ctx::Slot& sl = c->slot[i];
+        sl.hits.reserve((size_t)c->hitCap + 1);
+        sl.rank.reserve((size_t)c->hitCap + 1);
+        sl.tasks.reserve((size_t)c->taskCap);
+        sl.seeds.reserve(maxItems);
+        sl.seedItem.reserve(maxItems);
+    }
+    auto writeSlotTable = [&](hipStream_t s) {
+        for (size_t i = 0; i < Ctx::kSlots; ++i) {
+            Ctx::Slot& sl = c->slot[i];
+            c->slotHost[i] = TextSlot{sl.tasks.ptr, sl.queues.ptr, sl.hits.ptr, sl.rank.ptr, sl.qcnt.ptr, sl.small.ptr};
+        }
+        SH_HIP(hipMemcpyAsync(c->slotTab.ptr, c->slotHost, Ctx::kSlots * sizeof(TextSlot), hipMemcpyHostToDevice, s));
+    };
+    if (split) {
+        if (c->batchHostCap < nbatch + 1) {
+            if (c->batchHost) SH_HIP(hipHostFree(c->batchHost));
+            c->batchHost = nullptr;
+            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->batchHost), (nbatch + 1) * sizeof(TextBatch)));
+            c->batchHostCap = nbatch + 1;
+        }
+        if (c->hostDoneCap < nbatch) {
+            if (c->hostDone) SH_HIP(hipHostFree(c->hostDone));
+            c->hostDone = nullptr;
+            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hostDone), nbatch * sizeof(uint32_t)));
+            c->hostDoneCap = nbatch;
+        }
+        if (!c->slotHost) SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->slotHost), Ctx::kSlots * sizeof(TextSlot)));
+        if (!c->ctlHost) {
+            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ctlHost), 16));
+            c->ctlHost[0] = 1;
+        }
+        std::memset(c->hostDone, 0, nbatch * sizeof(uint32_t));
+        for (uint64_t b = 0; b <= nbatch; ++b)
+            c->batchHost[b] = b < nbatch ? TextBatch{bstart[b], (uint32_t)(bstart[b + 1] - bstart[b]), (uint32_t)(b % Ctx::kSlots)}
+                                         : TextBatch{bstart[nbatch], 0u, 0u};
+        c->bflags.reserve(nbatch * 4);
+        c->batchTab.reserve(nbatch + 1);
+        c->slotTab.reserve(Ctx::kSlots);
+        c->ctl.reserve(4);
+        SH_HIP(hipMemsetAsync(c->bflags.ptr, 0, nbatch * 4 * sizeof(uint32_t), sA));
+        SH_HIP(hipMemsetAsync(c->ctl.ptr, 0, 4 * sizeof(uint32_t), sA));
+        SH_HIP(hipMemcpyAsync(c->batchTab.ptr, c->batchHost, (nbatch + 1) * sizeof(TextBatch), hipMemcpyHostToDevice, sA));
+        writeSlotTable(sA);
+    }
     // a slot's counters and queues are zero when its `free` event fires:
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
@@ -335,6 +403,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sl.rank.reserve((size_t)c->hitCap + 1);
         sl.tasks.reserve((size_t)c->taskCap);
         SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
+        if (serial && split)  // a re-run of the batch publishes its tasks again
+            SH_HIP(hipMemsetAsync(c->bflags.ptr + 4 * b, 0, 4 * sizeof(uint32_t), sA));
         SearchArgs a{};
         a.occF = c->I.occF.ptr;
         a.occR = c->I.occR.ptr;
@@ -415,81 +485,107 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             ensureUploaded(c, p1, sD);
             SH_HIP(hipEventRecord(sl.fmStart, sD));
             seeds(0, (uint32_t)(p1 * c->nsearch));
-            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b, sD);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
             ensureUploaded(c, bstart[b + 1], sD);
+            SH_HIP(hipEventRecord(sl.seedMid, sD));  // the second part's seeds start (after the upload's wait)
             seeds((uint32_t)(p1 * c->nsearch), a.nitems);
+            sl.seedsInParts = true;
         } else {
+            sl.seedsInParts = false;
             ensureUploaded(c, bstart[b + 1], sD);
             SH_HIP(hipEventRecord(sl.fmStart, sD));
             seeds(0, a.nitems);
-            if (early && b == 0)  // the seed tasks end here: the text phase may start on them
-                SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+            // the seed tasks end here: the text phase may start on them (a
+            // lone device-resident batch's text phase waits for its FM phase:
+            // published after it below)
+            if (split && (early || serial)) launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b, sD);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
         }
         SH_HIP(hipEventRecord(sl.seedDone, sD));
         SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
         SH_HIP(hipEventRecord(sl.fmBegin, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
+        if (split) {  // the batch's task list is final
+            if (!early && !serial) launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b, sA);
+            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b + 1, sA);
+        }
         SH_HIP(hipEventRecord(sl.fmDone, sA));
         ++S.search_launches;
     };
+    // The text phase. Pipelined: one launch for the whole pass, issued with
+    // batch 0 (after its first seed tasks are published, or after its FM
+    // phase for a lone device-resident batch, whose FM phase runs at full
+    // occupancy alone); every batch's tasks reach it through bflags, and the
+    // finisher learns a batch is done from hostDone. Serial (overflow re-runs,
+    // SAHARA_PIPELINE=0): one launch per batch after its FM phase, on the one
+    // stream. SAHARA_TEXT_ONE_LAUNCH=0: one launch per batch, pipelined.
+    bool textLaunched = false;
+    uint64_t wallKHz = 0;
+    if (split) {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess && khz > 0)
+            wallKHz = (uint64_t)khz;
+        else
+            wallKHz = 100000;
+    }
+    auto launchTextRange = [&](uint64_t b0, uint64_t b1) {
+        TextArgs t{};
+        t.sa = c->I.saFull.ptr;
+        t.text3 = c->I.text3.ptr;
+        t.pats3 = c->pats3.ptr;
+        t.patBlocks = c->patBlocks;
+        t.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
+        t.m = c->m;
+        t.nsearch = c->nsearch;
+        t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
+        t.batches = c->batchTab.ptr;
+        t.slots = c->slotTab.ptr;
+        t.b0 = (uint32_t)b0;
+        t.b1 = (uint32_t)b1;
+        t.bflags = c->bflags.ptr;
+        t.hostDone = c->hostDone;
+        t.ctl = c->ctl.ptr;
+        // an idle wave gives up after 2 s without published work (the host
+        // then redoes the pass batch by batch): no legitimate wait is that long
+        t.timeoutTicks = wallKHz * 2000;
+        t.taskCap = c->taskCap;
+        t.hitCap = c->hitCap;
+        t.counters = c->counters.ptr;
+        t.winBlocks = winBlocks;
+        t.exactWindow = exactWindow ? 1u : 0u;
+        t.stackCap = textStack;
+        t.tableWords = tableWords;
+        t.steps = c->textSteps;
+        t.refillAt = c->refillAt;
+        // in-wave work stealing while no task is in hand, once SAHARA_STEAL_AT
+        // lanes of a wave are idle (0: off). Measured in one process,
+        // alternating: C5 80.4M (off) -> 124.3M (1) / 129.5M (8) reads/s,
+        // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
+        t.stealAt = 8;
+        if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
+        launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+    };
     auto issueText = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
-        const uint64_t q0 = bstart[b];
-        const bool split0 = early && b == 0;
-        SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone0 : sl.fmDone, 0));
+        if (oneLaunch) {
+            if (b != 0) return;
+            SH_HIP(hipStreamWaitEvent(sB, early ? sl.seedDone0 : sl.fmDone, 0));
+            SH_HIP(hipEventRecord(c->txStart, sB));
+            launchTextRange(0, nbatch);
+            SH_HIP(hipEventRecord(c->txEnd, sB));
+            textLaunched = true;
+            ++S.text_launches;
+            return;
+        }
+        SH_HIP(hipStreamWaitEvent(sB, early && b == 0 ? sl.seedDone0 : sl.fmDone, 0));
+        if (serial && split) {  // a re-run may have grown the slot's buffers
+            SH_HIP(hipStreamSynchronize(sB));
+            writeSlotTable(sB);
+        }
         SH_HIP(hipEventRecord(sl.textStart, sB));
-        sl.twoText = split && split0;
         if (split) {
-            TextArgs t{};
-            t.sa = c->I.saFull.ptr;
-            t.text3 = c->I.text3.ptr;
-            t.pats3 = c->pats3.ptr + q0 * c->patBlocks;
-            t.patBlocks = c->patBlocks;
-            t.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
-            t.pats3Bytes = (uint32_t)std::min<uint64_t>((c->npat - q0) * c->patBlocks * 16, 0xFFFFFF00ull);
-            t.m = c->m;
-            t.nsearch = c->nsearch;
-            t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
-            t.tasks = sl.tasks.ptr;
-            t.taskCount = sl.small.ptr + 4;
-            t.taskCap = c->taskCap;
-            t.work = sl.queues.ptr + 256;
-            t.hits = sl.hits.ptr;
-            t.hitCap = c->hitCap;
-            t.hitCount = sl.small.ptr + 1;
-            t.filled = sl.small.ptr + 3;
-            t.flags = sl.small.ptr + 2;
-            t.counters = c->counters.ptr;
-            t.winBlocks = winBlocks;
-            t.exactWindow = exactWindow ? 1u : 0u;
-            t.stackCap = textStack;
-            t.tableWords = tableWords;
-            t.steps = c->textSteps;
-            t.refillAt = c->refillAt;
-            // in-wave work stealing at the launch's end, once SAHARA_STEAL_AT
-            // lanes of a wave are idle (0: off). Measured in one process,
-            // alternating: C5 80.4M (off) -> 124.3M (1) / 129.5M (8) reads/s,
-            // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
-            t.stealAt = 8;
-            if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-            t.qcnt = sl.qcnt.ptr;
-            t.rank = sl.rank.ptr;
-            if (split0) {
-                // the first batch's seed tasks while its FM phase runs, then the
-                // tasks the FM phase appended after them
-                t.taskCount = sl.small.ptr + 5;
-                launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
-                SH_HIP(hipEventRecord(sl.textMid0, sB));
-                SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
-                SH_HIP(hipEventRecord(sl.textMid1, sB));
-                t.taskBegin = sl.small.ptr + 5;
-                t.taskCount = sl.small.ptr + 4;
-                t.work = sl.queues.ptr + 512;
-                ++S.text_launches;
-            }
-            launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
+            launchTextRange(b, b + 1);
             ++S.text_launches;
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));
@@ -504,13 +600,37 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool sleepy = c->streaming && !serial;
     uint32_t pollUs = 20;
     if (const char* e = std::getenv("SAHARA_POLL_US")) pollUs = (uint32_t)std::max(0, std::atoi(e));
+    // (one launch) the launch marks batch b done in pinned host memory; false
+    // if the launch ended without marking it (a wave gave up: the pass is redone)
+    bool textFailed = false;
+    auto waitTextDone = [&](uint64_t b) -> bool {
+        const volatile uint32_t* hd = c->hostDone + b;
+        for (uint32_t spin = 0;; ++spin) {
+            if (*hd) return true;
+            if (sleepy || (spin & 63u) == 0) {
+                const hipError_t r = hipEventQuery(c->txEnd);
+                if (r == hipSuccess) return *hd != 0;
+                if (r != hipErrorNotReady) SH_HIP(r);
+            }
+            if (sleepy && pollUs) std::this_thread::sleep_for(std::chrono::microseconds(pollUs));
+            else std::this_thread::yield();
+        }
+    };
     auto finish = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
         c->mark("finish", b);
         // the batch's counters, copied on sC (a copy on sB would wait for CU
         // slots between two text phases)
-        SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
+        if (oneLaunch) {
+            if (!waitTextDone(b)) {
+                textFailed = true;
+                overflow = true;  // redone batch by batch
+                return false;
+            }
+        } else {
+            SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
+        }
         SH_HIP(hipMemcpyAsync(c->pinned + b * 16, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(sleepy ? c->evSleep[0] : c->ev[6], sC));
         if (sleepy) waitSleepy(c->evSleep[0], pollUs);
@@ -518,18 +638,20 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->mark("text done", b);
         const uint32_t* hs = c->pinned + b * 16;
         float ms = 0;
-        SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
+        if (sl.seedsInParts) {  // the two seed launches, not the upload wait between them
+            SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone0));
+            S.seed_ms += ms;
+            SH_HIP(hipEventElapsedTime(&ms, sl.seedMid, sl.seedDone));
+        } else {
+            SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
+        }
         S.seed_ms += ms;
         SH_HIP(hipEventElapsedTime(&ms, sl.fmBegin, sl.fmDone));
         S.search_ms += ms;
-        if (sl.twoText) {  // the two launches only, not the wait for the FM phase between them
-            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMid0));
-            S.text_ms += ms;
-            SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textDone));
-        } else {
+        if (!oneLaunch) {  // (one launch: its span, after the pass)
             SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+            S.text_ms += ms;
         }
-        S.text_ms += ms;
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
         if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
         if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
@@ -671,6 +793,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     };
 
     if (!serial) {
+        DeferFrees deferFrees;  // no device-wide sync while the text launch waits on this host
         // Two host threads. This one packs the queries of a streamed upload
         // and issues seeds, FM(b) and text(b) as soon as batch b's slot is
         // free; a finisher thread waits for each batch's text phase and
@@ -742,11 +865,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         cv.notify_all();
         finisher.join();
         c->mark("finisher joined", 0);
-        if (issueErr) std::rethrow_exception(issueErr);
-        if (finErr) std::rethrow_exception(finErr);
-        if (overflow) {
-            c->taskCap = std::max(c->taskCap, seenTask);
-            c->hitCap = std::max(c->hitCap, seenHit);
+        // a pass that stopped early: the text launch's waves end (they would
+        // otherwise wait for batches never issued until they time out)
+        if (textLaunched && (overflow || issueErr || finErr)) {
+            SH_HIP(hipMemcpyAsync(c->ctl.ptr, c->ctlHost, sizeof(uint32_t), hipMemcpyHostToDevice, c->stE));
+            SH_HIP(hipStreamSynchronize(c->stE));
         }
         SH_HIP(hipStreamSynchronize(sA));
         SH_HIP(hipStreamSynchronize(sB));
@@ -754,6 +877,18 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamSynchronize(sD));
         SH_HIP(hipStreamSynchronize(c->stF));
         c->mark("streams synced", 0);
+        if (issueErr) std::rethrow_exception(issueErr);
+        if (finErr) std::rethrow_exception(finErr);
+        if (overflow) {
+            c->taskCap = std::max(c->taskCap, seenTask);
+            c->hitCap = std::max(c->hitCap, seenHit);
+            if (textFailed) ++S.text_fallbacks;
+        }
+        if (textLaunched && !overflow) {
+            float ms = 0;
+            SH_HIP(hipEventElapsedTime(&ms, c->txStart, c->txEnd));
+            S.text_ms += ms;
+        }
         if (overflow) return;  // the caller redoes the pass serially with the grown buffers
     } else {
         for (uint64_t b = 0; b < nbatch; ++b) {

@@ -76,26 +76,45 @@ struct SeedArgs {
 // (left reads near the window start) stays inside the workgroup's LDS.
 constexpr uint32_t kTextTableMin = 3u * 256u;
 
+// One batch slot's buffers (Ctx::Slot) as the text phase sees them.
+struct TextSlot {
+    const uint4* tasks;      // text tasks (row, |t|, pattern, meta | search << 24)
+    uint32_t* queues;        // striped counters: [256, 512) the seed tasks, [512, 768) the FM phase's
+    uint4* hits;
+    uint32_t* rank;          // rows ranked where the hits are written (as SearchArgs)
+    uint32_t* qcnt;
+    uint32_t* small;         // -, hitCount, flags, filled, taskCount, ...
+};
+// One batch of a pass (its patterns [q0, q0 + npat) of the staged ones).
+struct TextBatch {
+    uint64_t q0;
+    uint32_t npat;
+    uint32_t slot;
+};
+// a published task count (kPublish): bit 31 set once the count is final for its phase
+constexpr uint32_t kTaskReady = 0x80000000u;
+
 struct TextArgs {
     const uint32_t* sa;      // full SA: task records carry SA rows, the kernel reads their text positions
     const uint4* text3;      // text as 3-bit-plane blocks of 32 symbols (device_index.h)
-    const uint4* pats3;      // patterns as 3-bit-plane blocks, patBlocks per pattern
+    const uint4* pats3;      // patterns of the pass as 3-bit-plane blocks, patBlocks per pattern
     uint32_t patBlocks;
-    uint32_t text3Bytes;     // bytes of text3 / of this batch's pats3 (buffer-load bounds; < 4 GiB)
-    uint32_t pats3Bytes;
+    uint32_t text3Bytes;     // bytes of text3 (buffer-load bound; < 4 GiB; a batch's patterns likewise)
     uint32_t m;
     uint32_t nsearch;
     const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
-    const uint4* tasks;
-    const uint32_t* taskCount;  // tasks written by the FM kernel (device-side: no host round trip)
-    const uint32_t* taskBegin;  // first task of this launch (device-side; nullptr: 0)
+    // the batches [b0, b1) of the pass this launch serves (one launch per pass
+    // when pipelined, one per batch when serial; kSearchText's header comment)
+    const TextBatch* batches;  // b1 + 1 entries (the last one is never a batch of the launch)
+    const TextSlot* slots;
+    uint32_t b0, b1;
+    uint32_t* bflags;        // per batch 4 words: seed tasks | kTaskReady, all tasks | kTaskReady,
+                             // workgroups past the batch, -; zero before the launch
+    uint32_t* hostDone;      // pinned host memory, per batch: 1 once its text phase is done
+    const uint32_t* ctl;     // [0] != 0: the host aborts the pass
+    uint64_t timeoutTicks;   // an idle wave gives up after waiting this long (wall clock ticks)
     uint32_t taskCap;
-    uint32_t* work;
-    uint4* hits;
     uint32_t hitCap;
-    uint32_t* hitCount;
-    uint32_t* filled;
-    uint32_t* flags;
     unsigned long long* counters;
     uint32_t winBlocks;      // window blocks per lane (32 symbols each)
     uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
@@ -103,10 +122,8 @@ struct TextArgs {
     uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)
     uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
-    uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
-                             // lane of their wave (with its window and pattern) once this many are idle (0: off)
-    uint32_t* qcnt;          // as SearchArgs: rows ranked where the hits are written
-    uint32_t* rank;
+    uint32_t stealAt;        // no task in hand: idle lanes take the bottom stack entry of a busy lane of
+                             // their wave (with its window and pattern) once this many are idle (0: off)
 };
 
 struct LocateArgs {
@@ -127,9 +144,15 @@ struct LocateArgs {
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
 int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
+// text workgroups per CU (<= want) that leave room for an FM workgroup and a
+// locate-chain workgroup beside them (shape: the compile-time text shape, 0-2)
+int textBlocksBeside(uint32_t sigma, bool edit, bool count, int shape, size_t textLds, size_t fmLds, int want);
+int textShapeOf(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);
+// *flag = min(*count, cap) | kTaskReady on stream st (the text phase's hand-off)
+void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, hipStream_t st);
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st);
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst

@@ -776,12 +776,55 @@ struct TextShape { uint32_t win, pat; bool exact; };
 __host__ __device__ constexpr TextShape textShape(int shape) {
     return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
+// ---- the text phase of a whole pass in one launch (r5)
+//
+// One launch serves the batches [b0, b1) of a pass, so the text phase has no
+// launch boundary (and no grid drain and refill) between batches. A batch's
+// task list fills in two steps: the tasks kSeedItems writes (their count
+// published in bflags[4b] by kPublish on the seed stream), then the tasks the
+// FM phase appends (the final count in bflags[4b + 1], published after
+// kSearchFM). A wave's queue walks the batches in order, phase by phase, taking
+// 64-task chunks from the phase's striped counters. The lanes of one wave hold
+// tasks of at most two consecutive batches (a lane's batch parity: `lpar`),
+// each with its own hit range: the queue moves on from batch qb only once the
+// wave holds nothing of qb - 1 any more.
+//
+// Retiring batch b (the wave holds nothing of it and its queue has moved past
+// it): the wave closes its hit range, stores its deferred ranks and releases
+// its writes (agent scope), then arrives at the workgroup's counter of b in
+// LDS; the workgroup's last wave adds one to bflags[4b + 2], and the workgroup
+// whose add completes the grid tells the host (hostDone[b] = 1, a system-scope
+// store to pinned memory), which starts the batch's locate chain and later
+// reuses the batch's slot: every wave has passed the batch by then, so none
+// reads its task list or queue counters again. Waves may drift apart by up to
+// four batches (a slot is reused five batches on, after its batch is done), so
+// the LDS counters are a ring of eight. A wave with nothing to do and nothing published
+// sleeps; it ends when the host aborts the pass (ctl[0]) or after waiting
+// timeoutTicks (wall clock) — the host then finds the launch ended with a
+// batch not done and redoes the pass one batch at a time (pass.cpp).
+typedef __attribute__((address_space(1))) uint32_t GlobalU32;
+// Pointers that come from memory (the slot table) are generic: accesses through
+// them would be flat instructions, which also count against the LDS counter
+// and make every LDS wait wait for them. They address global memory, so say so.
+// (The host pass of this file parses kernel bodies too, where class types in
+// an address space do not convert: there the cast is a plain one.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GLOB(T, p) ((__attribute__((address_space(1))) T*)(p))
+#else
+#define GLOB(T, p) ((T*)(p))
+#endif
+__device__ __forceinline__ uint32_t pollWord(const uint32_t* p) {  // relaxed, agent scope: an sc1 load
+    return __hip_atomic_load((GlobalU32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
+    __shared__ uint32_t arrive[8];  // waves of this workgroup past batch b, at b % 8
     uint2* SC = reinterpret_cast<uint2*>(lds);
     uint32_t* slot = lds + a.tableWords;  // >= kTextTableMin: the window's block -1 stays in LDS
     for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = a.table[i];
+    if (threadIdx.x < 8) arrive[threadIdx.x] = 0;
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -796,23 +839,36 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     auto stackPut = [&](uint32_t d, const uint2& v) { S[d * 256u] = v; };
     const uint32_t winLen = winBlocks * 32u;
     const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
-    const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
     const uint32_t m = a.m;
-    // this launch's tasks: [tBase, taskCount) of the batch's list
-    const uint32_t tEnd = min(*a.taskCount, a.taskCap);
-    const uint32_t tBase = a.taskBegin ? min(*a.taskBegin, tEnd) : 0u;
-    const uint32_t ntasks = tEnd - tBase;
-    const uint4* tasks = a.tasks + tBase;
+    const uint32_t patBytes = patBlocks * 16u;
+    // patterns of batch b (pattern ids in task records are batch-local)
+    auto patBufOf = [&](uint32_t b) {
+        const TextBatch& B = a.batches[b];
+        return bufferOf(a.pats3 + B.q0 * patBlocks, B.npat * patBytes);
+    };
+    auto slotOf = [&](uint32_t b) -> const TextSlot& { return a.slots[a.batches[b].slot]; };
 
-    uint32_t sp = 0, pid = 0, wb = 0, sBase = 0;
-    bool have = false, exhausted = false, bad = false;
-    uint32_t qNext = 0, qEnd = 0, filled = 0;
-    bool qDone = false;
+    // ---- the wave's place in the pass (wave-uniform)
+    uint32_t qb = a.b0, qph = 0, lo = a.b0;  // the queue's batch and phase; the oldest batch the wave holds
+    bool qReady = false;                      // (qb, qph)'s range is published and `queue` covers it
+    uint32_t qLo = 0, qSnap = 0;              // first task of the phase; the seed tasks of qb
+    uint32_t hn0 = 0, he0 = 0, hn1 = 0, he1 = 0;  // hit slot range [next, end) of the batch of parity 0 / 1
+    uint32_t* qCtr = nullptr;                 // the phase's striped counters (StripedQueue, unrolled
+    uint32_t qN = 0, qStripe = 0, qTries = 0; // into plain values: they stay in registers)
+    const uint4* qTasks = nullptr;
+    // the batch of parity p among the (at most two) the wave holds
+    auto batchOf = [&](uint32_t p) { return (lo & 1u) == p ? lo : qb; };
+
+    uint32_t sp = 0, pid = 0, wb = 0, sBase = 0, lpar = 0;
+    bool have = false, bad = false;
+    uint32_t qNext = 0, qEnd = 0, filled0 = 0, filled1 = 0;
     // task chunks: the current one's records (one per lane) and the next one's,
-    // prefetched a chunk ahead so a refill needs no dependent task read
+    // prefetched a chunk ahead so a refill needs no dependent task read; each
+    // with its batch (cBat, nBat) and the current one's pattern buffer
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
-    uint32_t nBase = 0, nEnd = 0, qBase = 0;
+    uint32_t nBase = 0, nEnd = 0, qBase = 0, cBat = a.b0, nBat = a.b0;
     bool haveNext = false;
+    __amdgpu_buffer_rsrc_t patBuf = patBufOf(a.b0);
     // The prefetched chunk's records still hold SA rows. Their text positions
     // are read at the next refill, beside its window loads (one round trip for
     // both), or at the latest when the chunk becomes current.
@@ -823,21 +879,110 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             nextRaw = false;
         }
     };
-    StripedQueue queue(a.work, ntasks);
-    {
-        uint32_t b = 0, e = 0;
-        if (queue.next(lane, kTaskChunk, b, e)) {
-            nBase = b;
-            nEnd = e;
-            if (b + lane < e) nextRec = tasks[b + lane];
-            haveNext = true;
-            nextRaw = true;
-        } else {
-            qDone = true;
+    // Next chunk into `next`: 1 got one; 0 none yet (nothing published, or the
+    // wave must retire batch qb - 1 first); 2 the pass's tasks are all taken.
+    // Wave-uniform.
+    auto grab = [&]() __attribute__((always_inline)) -> uint32_t {
+        for (;;) {
+            if (qb >= a.b1) return 2u;
+            if (!qReady) {
+                uint32_t f = 0;
+                if (lane == 0) f = pollWord(a.bflags + 4u * qb + qph);
+                f = __builtin_amdgcn_readfirstlane(f);
+                if (!(f & kTaskReady)) return 0u;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // then the task records
+                const uint32_t cnt = min(f & ~kTaskReady, a.taskCap);
+                const TextSlot& Sl = slotOf(qb);
+                if (qph == 0) qSnap = cnt;
+                qLo = qph == 0 ? 0u : min(qSnap, cnt);
+                qCtr = Sl.queues + 256u * (1u + qph);
+                qN = cnt - qLo;
+                qStripe = blockIdx.x % kStripes;
+                qTries = 0;
+                qTasks = Sl.tasks;
+                qReady = true;
+            }
+            uint32_t b = 0, e = 0;
+            bool got = false;
+            while (qTries < kStripes) {  // StripedQueue::next
+                const uint32_t s0 = (uint32_t)((uint64_t)qN * qStripe / kStripes);
+                const uint32_t s1 = (uint32_t)((uint64_t)qN * (qStripe + 1) / kStripes);
+                uint32_t off = 0;
+                if (lane == 0)
+                    off = s0 < s1 ? __hip_atomic_fetch_add(GLOB(uint32_t, qCtr + qStripe * kStripeStride), kTaskChunk,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0xFFFFFFFFu;
+                off = __builtin_amdgcn_readfirstlane(off);
+                if (off != 0xFFFFFFFFu && off < s1 - s0) {
+                    b = s0 + off;
+                    e = min(b + kTaskChunk, s1);
+                    got = true;
+                    break;
+                }
+                qStripe = (qStripe + 1) % kStripes;
+                ++qTries;
+            }
+            if (got) {
+                nBase = qLo + b;
+                nEnd = qLo + e;
+                nBat = qb;
+                nextRec = make_uint4(0, 0, 0, 0);
+                if (nBase + lane < nEnd) nextRec = uint4(*GLOB(const uint4, qTasks + nBase + lane));
+                haveNext = true;
+                nextRaw = true;
+                return 1u;
+            }
+            if (qph == 0) {
+                qph = 1;
+                qReady = false;
+                continue;
+            }
+            if (lo != qb) return 0u;  // at most two batches in flight per wave
+            ++qb;
+            qph = 0;
+            qReady = false;
         }
-    }
-    SlotRange hitSlots;
-    uint32_t rankSlot = ~0u, rankVal = 0;  // the lane's last hit whose rank is not stored yet
+    };
+    // This wave is past batch b: hit range closed, ranks stored, writes
+    // released, arrival counted. Wave-uniform, all lanes active.
+    uint32_t rankSlot = ~0u, rankVal = 0, rankPar = 0;  // the lane's last hit whose rank is not stored yet
+    auto retire = [&](uint32_t b) __attribute__((always_inline)) {
+        const uint32_t p = b & 1u;
+        const TextSlot& Sl = slotOf(b);
+        if (rankSlot != ~0u && rankPar == p) {
+            *GLOB(uint32_t, Sl.rank + rankSlot) = rankVal;
+            rankSlot = ~0u;
+        }
+        // the unused tail of the hit range: empty records (len 0) for the locate scan
+        const uint32_t hn = p ? hn1 : hn0, he = p ? he1 : he0;
+        for (uint32_t i = hn + lane; i < he; i += 64)
+            if (i < a.hitCap) *GLOB(uint4, Sl.hits + i) = make_uint4(0u, 0u, 0u, 0u);
+        if (p) hn1 = he1 = 0;
+        else hn0 = he0 = 0;
+        const uint32_t fl = p ? filled1 : filled0;
+        if (fl) __hip_atomic_fetch_add(GLOB(uint32_t, Sl.small + 3), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p) filled1 = 0;
+        else filled0 = 0;
+        if (__any(bad) && lane == 0)
+            __hip_atomic_fetch_or(GLOB(uint32_t, Sl.small + 2), 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the wave's hits, ranks and counts reach memory before it arrives
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            const uint32_t k = __hip_atomic_fetch_add(arrive + (b & 7u), 1u, __ATOMIC_ACQ_REL,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (k + 1u == blockDim.x / 64u) {  // the workgroup's last wave
+                arrive[b & 7u] = 0;
+                const uint32_t g = __hip_atomic_fetch_add((GlobalU32*)(a.bflags + 4u * b + 2u), 1u,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (g + 1u == gridDim.x) __hip_atomic_store(a.hostDone + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    };
+    uint32_t pollSkip = 0;  // busy waves poll an unpublished phase every few iterations only
+    uint64_t waitStart = 0;
+    uint32_t idleSpins = 0;
+    bool waiting = false;
     uint2 cur = make_uint2(0, 0);
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
@@ -847,35 +992,37 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         // stalls the whole wave, so idle lanes are refilled in batches: once
         // refillAt lanes are idle (or nothing else is left).
         if (COUNT) t0 = clock64();
-        const bool idle = !have && sp == 0 && !exhausted;
+        const bool idle = !have && sp == 0;
         const uint64_t idleMask = __ballot(idle);
-        const bool busy = __any(have || sp > 0);
+        const bool busy = idleMask != ~0ull;
         const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
-        const bool need = refill && idle;
         uint64_t pending = refill ? idleMask : 0ull;
         if (pending) resolveNext();
+        bool dry = false;  // no task in hand for an idle lane
+        // (re)fill the prefetched chunk: at most two chunks serve one refill
+        // (64 tasks each, <= 64 idle lanes), so one grab before and one after
+        // the lane loop keep a chunk prefetched; a busy wave polls an
+        // unpublished phase every few iterations only
+        auto prefetch = [&]() __attribute__((always_inline)) {
+            if (haveNext) return;
+            if (busy && pollSkip) --pollSkip;
+            else if (grab() != 1u) pollSkip = 8;
+        };
+        if (pending) prefetch();
         while (pending) {  // wave-uniform
-            if (qNext >= qEnd) {
-                // switch to the prefetched chunk, prefetch the one after it
-                if (!haveNext) break;
+            if (qNext >= qEnd) {  // switch to the prefetched chunk
+                if (!haveNext) {
+                    dry = true;
+                    break;
+                }
                 resolveNext();
                 qBase = nBase;
                 qNext = nBase;
                 qEnd = nEnd;
                 curRec = nextRec;
+                cBat = nBat;
+                patBuf = patBufOf(cBat);
                 haveNext = false;
-                if (!qDone) {
-                    uint32_t b = 0, e = 0;
-                    if (!queue.next(lane, kTaskChunk, b, e)) {
-                        qDone = true;
-                    } else {
-                        nBase = b;
-                        nEnd = e;
-                        if (b + lane < e) nextRec = tasks[b + lane];
-                        haveNext = true;
-                        nextRaw = true;
-                    }
-                }
                 if (qNext >= qEnd) continue;
             }
             const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
@@ -890,6 +1037,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 // and the text window its subtree can reach
                 const uint32_t x = t.x;
                 pid = t.z;
+                lpar = cBat & 1u;
                 sBase = (t.w >> 24) * m;
                 const uint32_t meta = t.w & 0x00FFFFFFu;
                 const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
@@ -899,10 +1047,10 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 wb = x > left ? x - left : 0u;  // window start
                 if (exactWindow) {              // at wb: m + 2k symbols fit in winBlocks blocks
                     copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
-                                      pid * patBlocks * 16u, patBlocks);
+                                      pid * patBytes, patBlocks);
                 } else {                        // at the block start below wb (31 more symbols)
                     wb &= ~31u;
-                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
+                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBytes, patBlocks);
                 }
                 cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
                 have = true;
@@ -910,16 +1058,29 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             pending &= ~__ballot(mine);
             qNext += take;
         }
-        if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
-        // ---- work stealing inside the wave once the task queue is dry (wave-
-        // uniform: the queue state is the wave's). A launch ends on its longest
-        // subtrees, each on one lane while the others idle (C5: lanes busy
-        // 0.655 of the time); an idle lane takes the bottom (shallowest, so
+        if (refill) prefetch();
+        if (!dry) dry = qNext >= qEnd && !haveNext;
+        // ---- retire the older batch once the wave holds nothing of it
+        bool retired = false;
+        if (lo != qb) {
+            const uint32_t p = lo & 1u;
+            const bool held = __any((have || sp > 0u) && lpar == p) || (cBat == lo && qNext < qEnd) ||
+                              (haveNext && nBat == lo);
+            if (!held) {
+                retire(lo);
+                ++lo;
+                retired = true;
+            }
+        }
+        // ---- work stealing inside the wave while no task is in hand (wave-
+        // uniform: the queue state is the wave's). A batch's tasks end on its
+        // longest subtrees, each on one lane while the others idle (C5: lanes
+        // busy 0.655 of the time); an idle lane takes the bottom (shallowest, so
         // largest) stack entry of a busy lane, with that lane's window and
         // pattern copied slot to slot in LDS, and the task state (pattern id,
-        // window start, scheme row) by shuffle. The DFS of the entry is the
-        // same whichever lane runs it, so the hits are too.
-        if (a.stealAt && qDone && !haveNext && qNext >= qEnd) {
+        // window start, scheme row, batch parity) by shuffle. The DFS of the
+        // entry is the same whichever lane runs it, so the hits are too.
+        if (a.stealAt && dry) {
             const bool thief = !have && sp == 0u;
             const uint64_t I = __ballot(thief);
             const uint64_t D = __ballot(sp >= 2u || (sp == 1u && have));
@@ -938,6 +1099,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 const bool takes = thief && r < n;
                 donor = takes ? donor : lane;
                 const uint32_t dPid = __shfl(pid, donor), dWb = __shfl(wb, donor), dBase = __shfl(sBase, donor);
+                const uint32_t dPar = __shfl(lpar, donor);
                 const uint32_t dTid = (threadIdx.x & ~63u) | donor;
                 if (takes) {
                     const uint32_t* src = slot + dTid;
@@ -948,6 +1110,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     pid = dPid;
                     wb = dWb;
                     sBase = dBase;
+                    lpar = dPar;
                     have = true;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -960,7 +1123,25 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 }
             }
         }
-        if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
+        if (!__any(have || sp > 0)) {
+            if (lo >= a.b1) break;  // every batch of the pass retired
+            if (retired) continue;  // the queue may move on now
+            // nothing to do: sleep until tasks are published, unless the host
+            // aborts the pass or the wait times out
+            if (!waiting) {
+                waiting = true;
+                waitStart = wall_clock64();
+            }
+            __builtin_amdgcn_s_sleep(20);  // ~0.5 us
+            if ((++idleSpins & 15u) == 0u) {
+                uint32_t abort = 0;
+                if (lane == 0) abort = pollWord(a.ctl);
+                if (__builtin_amdgcn_readfirstlane(abort) || wall_clock64() - waitStart > a.timeoutTicks) break;
+            }
+            pollSkip = 0;
+            continue;
+        }
+        waiting = false;
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);
             if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
@@ -1157,28 +1338,51 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             t0 = t1;
         }
         {
-            uint32_t s;
-            if (hitSlots.take(leaf, lane, ltMask, a.hitCount, s) && leaf) {
-                if (s < a.hitCap) {
-                    a.hits[s] = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
-                    // the hit's row ranked in its query's segment (a.qcnt):
-                    // the atomic's result is stored at the next emission, so
-                    // its round trip overlaps the micro-steps in between
-                    if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
-                    rankVal = atomicAdd(a.qcnt + pid, 1u);
-                    rankSlot = s;
-                } else {
-                    atomicOr(a.flags, 2u);
+            // leaves -> the hit buffer of their batch (one slot range per
+            // batch parity). The hit's row is ranked in its query's segment
+            // (qcnt); the atomic's result is stored at the lane's next
+            // emission, so its round trip overlaps the micro-steps between.
+            uint32_t* rk0 = slotOf(batchOf(0u)).rank;
+            uint32_t* rk1 = slotOf(batchOf(1u)).rank;
+            auto emit = [&](uint32_t p, uint32_t& hn, uint32_t& he) __attribute__((always_inline)) {
+                const bool want = leaf && lpar == p;
+                const uint64_t wm = __ballot(want);
+                if (!wm) return;
+                const TextSlot& Sl = slotOf(batchOf(p));
+                // SlotRange::take on (hn, he)
+                const uint32_t cnt = (uint32_t)__popcll(wm), rank = (uint32_t)__popcll(wm & ltMask);
+                const uint32_t avail = he - hn;
+                uint32_t base = 0;
+                if (cnt > avail) {
+                    if (lane == 0)
+                        base = __hip_atomic_fetch_add(GLOB(uint32_t, Sl.small + 1), kHitChunk, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                    base = __builtin_amdgcn_readfirstlane(base);
                 }
-                ++filled;
-            }
+                const uint32_t s = rank < avail ? hn + rank : base + (rank - avail);
+                if (cnt > avail) { hn = base + (cnt - avail); he = base + kHitChunk; }
+                else hn += cnt;
+                if (want) {
+                    if (s < a.hitCap) {
+                        *GLOB(uint4, Sl.hits + s) = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
+                        if (rankSlot != ~0u) *GLOB(uint32_t, (rankPar ? rk1 : rk0) + rankSlot) = rankVal;
+                        rankVal = __hip_atomic_fetch_add(GLOB(uint32_t, Sl.qcnt + pid), 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                        rankSlot = s;
+                        rankPar = p;
+                    } else {
+                        __hip_atomic_fetch_or(GLOB(uint32_t, Sl.small + 2), 2u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (p) ++filled1;
+                    else ++filled0;
+                }
+            };
+            emit(0u, hn0, he0);
+            emit(1u, hn1, he1);
         }
         if (COUNT) cyEmit += clock64() - t0;
     }
-    hitSlots.close(lane, a.hits, a.hitCap);
-    if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
-    if (filled) atomicAdd(a.filled, filled);  // per-lane counts
-    if (__any(bad) && lane == 0) atomicOr(a.flags, 16u);
     if (COUNT) {
         atomicAdd(a.counters + 5, (unsigned long long)cNodes);
         if (lane == 0) {
@@ -1192,6 +1396,15 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         atomicAdd(a.counters + 14, (unsigned long long)cCmp);
         atomicAdd(a.counters + 15, (unsigned long long)cSteps);
     }
+}
+
+// A producer stream's step of the text phase's hand-off: *flag = the task
+// count (capped) | kTaskReady, stored sc1 (relaxed, agent scope). The tasks
+// were written by the kernels before this one on its stream, whose end
+// released them; the text kernel polls the flag, then acquires.
+__global__ void kPublish(const uint32_t* count, uint32_t cap, uint32_t* flag) {
+    const uint32_t v = min(*count, cap) | kTaskReady;
+    __hip_atomic_store((GlobalU32*)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ================================================================ locate ====
@@ -1661,14 +1874,7 @@ void launchFMT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds
     }
 }
 
-// the compile-time shape matching a launch (0: the generic kernel)
-int textShapeOf(const TextArgs& a) {
-    for (int shape = 1; shape <= 2; ++shape) {
-        const TextShape t = textShape(shape);
-        if (a.winBlocks == t.win && a.patBlocks == t.pat && (a.exactWindow != 0u) == t.exact) return shape;
-    }
-    return 0;
-}
+
 
 template <int SIGMA, int SHAPE>
 void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
@@ -1683,13 +1889,22 @@ void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_
 
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
-    const int shape = textShapeOf(a);
+    const int shape = textShapeOf(a.winBlocks, a.patBlocks, a.exactWindow != 0u);
     if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
     else if (shape == 2) launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
     else launchTextShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
 }
 
 }  // namespace
+
+// the compile-time shape matching a launch (0: the generic kernel)
+int textShapeOf(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow) {
+    for (int shape = 1; shape <= 2; ++shape) {
+        const TextShape t = textShape(shape);
+        if (winBlocks == t.win && patBlocks == t.pat && exactWindow == t.exact) return shape;
+    }
+    return 0;
+}
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     int b = 0;
@@ -1709,6 +1924,48 @@ int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     return b;
 }
 
+// The text kernel waits inside its launch for tasks that the seed and FM
+// kernels publish, so those must be able to run beside its resident
+// workgroups: the most text workgroups per CU (at most `want`) that leave a
+// SIMD's VGPRs (512 per lane) and the CU's LDS (160 KB) for one FM workgroup
+// and a 16 KB locate-chain workgroup (kSortBigLds, kScanTiles).
+int textBlocksBeside(uint32_t sigma, bool edit, bool count, int shape, size_t textLds, size_t fmLds, int want) {
+    auto textFn = [&]() -> const void* {
+#define SH_TEXT_FN(S)                                                                                     \
+    if (shape == S) {                                                                                     \
+        if (sigma == 5)                                                                                   \
+            return edit ? (count ? (const void*)kSearchText<5, true, true, S> : (const void*)kSearchText<5, true, false, S>)    \
+                        : (count ? (const void*)kSearchText<5, false, true, S> : (const void*)kSearchText<5, false, false, S>); \
+        return edit ? (count ? (const void*)kSearchText<6, true, true, S> : (const void*)kSearchText<6, true, false, S>)        \
+                    : (count ? (const void*)kSearchText<6, false, true, S> : (const void*)kSearchText<6, false, false, S>);     \
+    }
+        SH_TEXT_FN(1)
+        SH_TEXT_FN(2)
+#undef SH_TEXT_FN
+        if (sigma == 5)
+            return edit ? (count ? (const void*)kSearchText<5, true, true, 0> : (const void*)kSearchText<5, true, false, 0>)
+                        : (count ? (const void*)kSearchText<5, false, true, 0> : (const void*)kSearchText<5, false, false, 0>);
+        return edit ? (count ? (const void*)kSearchText<6, true, true, 0> : (const void*)kSearchText<6, true, false, 0>)
+                    : (count ? (const void*)kSearchText<6, false, true, 0> : (const void*)kSearchText<6, false, false, 0>);
+    };
+    const void* fm;
+    if (sigma == 5)
+        fm = edit ? (count ? (const void*)kSearchFM<5, true, true> : (const void*)kSearchFM<5, true, false>)
+                  : (count ? (const void*)kSearchFM<5, false, true> : (const void*)kSearchFM<5, false, false>);
+    else
+        fm = edit ? (count ? (const void*)kSearchFM<6, true, true> : (const void*)kSearchFM<6, true, false>)
+                  : (count ? (const void*)kSearchFM<6, false, true> : (const void*)kSearchFM<6, false, false>);
+    hipFuncAttributes ta{}, fa{};
+    SH_HIP(hipFuncGetAttributes(&ta, textFn()));
+    SH_HIP(hipFuncGetAttributes(&fa, fm));
+    auto granule = [](int r) { return (std::max(r, 1) + 7) / 8 * 8; };
+    const int vt = granule(ta.numRegs), vf = granule(fa.numRegs);
+    const size_t lt = textLds + ta.sharedSizeBytes, lf = fmLds + fa.sharedSizeBytes;
+    for (int t = std::max(want, 1); t > 1; --t)
+        if (t * vt + vf <= 512 && t * lt + lf + (16u << 10) <= (160u << 10) && t + 1 <= 8) return t;
+    return 1;
+}
+
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                   hipStream_t st) {
     if (sigma == 5) launchFMT<5>(a, edit, count, dim3(blocks), lds, st);
@@ -1720,6 +1977,11 @@ void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32
                 hipStream_t st) {
     if (sigma == 5) launchTextT<5>(a, edit, count, dim3(blocks), lds, st);
     else            launchTextT<6>(a, edit, count, dim3(blocks), lds, st);
+    SH_HIP(hipGetLastError());
+}
+
+void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, hipStream_t st) {
+    hipLaunchKernelGGL(kPublish, dim3(1), dim3(64), 0, st, count, cap, flag);
     SH_HIP(hipGetLastError());
 }
 

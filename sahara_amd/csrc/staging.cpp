@@ -674,11 +674,14 @@ static void stagePackedN(Ctx* c, const PackedReads& P, uint64_t rows, uint32_t m
     U.srcPinned = pinned(U.src + b0) && pinned(U.src + b1 - 1);
     const uint64_t lo = P.sym0, hi = P.sym0 + rows * m;
     const uint64_t* all = P.nCount ? P.nPos : nullptr;
+    // the whole list, not only this call's range: the binary searches below
+    // place the range correctly only in an ascending list (a shard of a larger
+    // stream sees every entry)
+    for (uint64_t i = 1; i < P.nCount; ++i)
+        if (all[i] <= all[i - 1]) throw Error("N positions of packed reads must be strictly ascending");
     const uint64_t* b = all ? std::lower_bound(all, all + P.nCount, lo) : nullptr;
     const uint64_t* e = all ? std::lower_bound(b, all + P.nCount, hi) : nullptr;
     const uint64_t nN = all ? (uint64_t)(e - b) : 0;
-    for (uint64_t i = 1; i < nN; ++i)
-        if (b[i] <= b[i - 1]) throw Error("N positions of packed reads must be strictly ascending");
     if (nN && c->I.sigma == 5) throw Error("pattern rank out of range for this index");  // N is no dna4 rank
     const uint64_t nch = chunkCount(U);
     U.nFirst.assign(nch + 1, nN);

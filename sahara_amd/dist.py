@@ -83,6 +83,80 @@ def gather_hit_records(n_local: int, fill, device="cpu"):
     return [p[:c] for p, c in zip(parts, counts)], counts
 
 
+def gather_compact_records(recs, block_qid0, block_end, qid_offset: int, device="cpu"):
+    """Gather every rank's compact hit records — the 8-B records a
+    sahara_gpu_search_packed_compact / _reads_compact call leaves in host
+    memory (qid - its batch's first qid << 36 | text position << 4 | e) with
+    the per-batch block table (first qid, one past the last record) — to
+    rank 0 in rank order, over RCCL (xGMI) on GPUs, gloo on CPU. The block
+    qids are made global (+ qid_offset, the rank's first pattern) before they
+    leave the rank. Three collectives: an all_gather of the counts (records,
+    blocks), then a gather of the records and one of the block tables, each
+    padded to the largest count. Returns [(recs, block_qid0, block_end)] per
+    rank on rank 0, None elsewhere; records_to_rows decodes them."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    recs = np.ascontiguousarray(recs, dtype=np.uint64)
+    q0 = np.asarray(block_qid0, dtype=np.uint64) + np.uint64(qid_offset)
+    end = np.asarray(block_end, dtype=np.uint64)
+    cnt = torch.tensor([len(recs), len(q0)], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [(int(c[0].item()), int(c[1].item())) for c in counts]
+    cap = max(max(c[0] for c in counts), 1)
+    bcap = max(max(c[1] for c in counts), 1)
+    buf = torch.zeros(cap, dtype=torch.int64, device=device)
+    if len(recs):
+        buf[: len(recs)] = torch.from_numpy(recs.view(np.int64)).to(device)
+    blk = torch.zeros((bcap, 2), dtype=torch.int64, device=device)
+    if len(q0):
+        blk[: len(q0)] = torch.from_numpy(np.stack([q0, end], 1).view(np.int64)).to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    bparts = [torch.empty_like(blk) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gather_list=parts, dst=0)
+    dist.gather(blk, gather_list=bparts, dst=0)
+    if rank != 0:
+        return None
+    out = []
+    for p, b, (n, nb) in zip(parts, bparts, counts):
+        r = p[:n].cpu().numpy().view(np.uint64)
+        bt = b[:nb].cpu().numpy().view(np.uint64)
+        out.append((r, bt[:, 0].copy(), bt[:, 1].copy()))
+    return out
+
+
+def records_to_rows(recs, block_qid0, block_end, rec_starts) -> np.ndarray:
+    """Compact hit records + block table -> (n, 4) u64 rows (qid, seq_id,
+    pos, e), as sahara_amd.CompactHits.to_hits decodes them."""
+    recs = np.asarray(recs, np.uint64)
+    counts = np.diff(np.concatenate([[0], np.asarray(block_end, np.uint64)])).astype(np.int64)
+    out = np.empty((len(recs), 4), np.uint64)
+    out[:, 0] = np.repeat(np.asarray(block_qid0, np.uint64), counts) + (recs >> np.uint64(36))
+    g = (recs >> np.uint64(4)) & np.uint64(0xFFFFFFFF)
+    starts = np.asarray(rec_starts, np.uint64)
+    seq = np.searchsorted(starts, g, side="right") - 1
+    out[:, 1] = seq
+    out[:, 2] = g - starts[seq]
+    out[:, 3] = recs & np.uint64(15)
+    return out
+
+
+def rows_to_records(rows, rec_starts, batch: int):
+    """(n, 4) u64 rows sorted by qid -> compact records and a block table,
+    one block per `batch` consecutive qids (the layout of a compact call's
+    result; tests build rank-local results with it)."""
+    rows = np.asarray(rows, np.uint64).reshape(-1, 4)
+    starts = np.asarray(rec_starts, np.uint64)
+    q = rows[:, 0]
+    q0 = (q // np.uint64(batch)) * np.uint64(batch)
+    recs = ((q - q0) << np.uint64(36)) | ((starts[rows[:, 1].astype(np.int64)] + rows[:, 2]) << np.uint64(4)) | rows[:, 3]
+    firsts = np.unique(q0)
+    end = np.searchsorted(q0, firsts, side="right").astype(np.uint64)
+    return recs, firsts, end
+
+
 def hit_rows_from_records(rec) -> np.ndarray:
     """(n, 3) int64 sahara_hit records -> (n, 4) u64 rows (qid, seq_id, pos, e)."""
     a = np.ascontiguousarray(np.asarray(rec, dtype=np.int64)).view(np.uint64).reshape(-1, HIT_WORDS)

@@ -128,6 +128,19 @@ def test_compact_records_view_outlives_its_call(gpu_device, monkeypatch):
     owner = weakref.ref(r._own)
     del r
     assert owner() is None
+    # close() with a view still alive: the view keeps the memory (the pool
+    # cannot hand it to the next calls), and it goes with the view
+    r = sa.search_reads_compact(gpu, reads, sch)
+    owner = weakref.ref(r._own)
+    view = r.recs[::2]
+    saved = view.copy()
+    r.close()
+    assert owner() is not None
+    for _ in range(3):
+        sa.search_reads_compact(gpu, reads[::-1].copy(), sch).close()
+    assert np.array_equal(view, saved)
+    del view
+    assert owner() is None
 
 
 @pytest.mark.gpu

@@ -674,3 +674,76 @@ def test_single_row_seeds_near_text_ends(gpu_device, m, k, gen):
     gpu.run(count=True)
     assert gpu.stats()["conversions"] > 0
     assert np.array_equal(hits_as_rows(gpu.fetch()), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,one", [("61", "1"), ("61", "0"), ("1000", "1")])
+def test_one_text_launch_many_batches(gpu_device, monkeypatch, batch, one):
+    """The text phase of a pipelined pass is one launch (search.hip
+    kSearchText) that takes each batch's tasks as the seed and FM streams
+    publish them and tells the host when a batch is done. More batches than
+    slots (61 patterns per batch: 14 batches over 5 slots), repeat-rich text
+    with k = 3 (tasks that outlive their batch, work stealing across batch
+    parities): the oracle's hits through the device-resident pass, the rank-
+    form reads call and the packed call; one text launch per pass
+    (SAHARA_TEXT_ONE_LAUNCH=0: one per batch) and no wave gave up waiting."""
+    monkeypatch.setenv("SAHARA_BATCH", batch)
+    monkeypatch.setenv("SAHARA_TEXT_ONE_LAUNCH", one)
+    rng = np.random.default_rng(505)
+    recs = random_records(rng, [30000, 12000], 6, repeats=True)
+    reads = mutate_reads(rng, recs, 400, 80, 3, 6)
+    pats = sa.interleave_rc(reads, 6)
+    scheme = sa.search_scheme("h2-k3", 0, 3, 80)
+    want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)[0])
+    gpu = sa.BiFMIndex.build(recs, sigma=6, device=gpu_device)
+    nbatch = -(-len(pats) // int(batch))
+    gpu.stage(pats, scheme)
+    for count in (False, True):
+        gpu.run(count=count)
+        st = gpu.stats()
+        assert np.array_equal(hits_as_rows(gpu.fetch()), want), count
+        assert st["batches"] == nbatch and st["text_fallbacks"] == 0, st
+        assert st["text_launches"] == (1 if one == "1" else nbatch), st
+    assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme)), want)
+    assert gpu.stats()["text_fallbacks"] == 0
+    c = sa.search_packed_compact(gpu, sa.pack_reads(reads, 6, pinned=True), scheme)
+    got = c.to_hits()
+    c.close()
+    assert np.array_equal(hits_as_rows(got), want)
+    assert gpu.stats()["text_fallbacks"] == 0
+
+
+@pytest.mark.gpu
+def test_one_text_launch_with_few_hardware_queues(gpu_device, tmp_path):
+    """The text launch waits inside for kernels on the seed and FM streams.
+    Its stream is created with a CU mask, which gives it a hardware queue of
+    its own: with GPU_MAX_HW_QUEUES=1 (every other stream of the process on
+    one queue) no kernel it waits for queues behind it, so no wave gives up
+    (text_fallbacks 0) and the hits are the oracle's."""
+    import os
+    import subprocess
+    import sys
+    script = tmp_path / "q.py"
+    script.write_text(f"""
+import sys
+sys.path[:0] = {[os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__)), os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")]!r}
+import numpy as np
+import oracle as O
+import sahara_amd as sa
+from helpers import hits_as_rows, mutate_reads, random_records
+rng = np.random.default_rng(506)
+recs = random_records(rng, [20000, 9000], 6, repeats=True)
+reads = mutate_reads(rng, recs, 300, 60, 2, 6)
+pats = sa.interleave_rc(reads, 6)
+scheme = sa.search_scheme("h2-k2", 0, 2, 60)
+want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)[0])
+gpu = sa.BiFMIndex.build(recs, sigma=6, device={gpu_device})
+got = hits_as_rows(sa.search(gpu, pats, scheme))
+st = gpu.stats()
+print("fallbacks", st["text_fallbacks"], "launches", st["text_launches"], "batches", st["batches"])
+assert np.array_equal(got, want)
+assert st["text_fallbacks"] == 0 and st["text_launches"] == 1 and st["batches"] > 5
+""")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="1", SAHARA_BATCH="53")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -118,21 +118,28 @@ def test_two_rank_gather_equals_single_process(world):
     assert t == float(world)  # max over ranks
 
 
-class _FakeIndex:
-    """Stands in for BiFMIndex.copy_hits on CPU: writes this rank's records
-    (sahara_hit layout, qids shifted) to the destination pointer."""
+class _FakeCompact:
+    """Stands in for a sahara_gpu_search_packed_compact result on CPU: the
+    rank's rows (rank-local qids, sorted) as 8-B compact records with a block
+    table of 16-qid batches."""
+
+    def __init__(self, rows, rec_starts):
+        from sahara_amd.dist import rows_to_records
+        self.rec_starts = rec_starts
+        self.recs, self.block_qid0, self.block_end = rows_to_records(rows, rec_starts, 16)
+
+
+class _FakeWhole:
+    """A whole-records result (multi-part index): to_hits() only."""
 
     def __init__(self, rows):
-        from sahara_amd.dist import hit_records_from_rows
-        self.rec = hit_records_from_rows(rows)
+        import sahara_amd as sa
+        self.h = np.zeros(len(rows), sa.HIT_DTYPE)
+        for k, f in enumerate(("qid", "seq_id", "pos", "err")):
+            self.h[f] = rows[:, k]
 
-    def copy_hits(self, ptr, cap, qid_offset=0):
-        import ctypes
-        assert cap >= len(self.rec)
-        r = self.rec.copy()
-        r[:, 0] += qid_offset
-        ctypes.memmove(ptr, r.ctypes.data, r.nbytes)
-        return len(r)
+    def to_hits(self):
+        return self.h
 
 
 def _bench_gather_worker(rank, world, port, outdir):
@@ -142,16 +149,35 @@ def _bench_gather_worker(rank, world, port, outdir):
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
+    from sahara_amd.dist import gather_compact_records, records_to_rows
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rng = np.random.default_rng(100 + rank)
         n = 37 + 20 * rank  # ragged per-rank counts
-        rows = np.stack([rng.integers(0, 2 * 50, n), rng.integers(0, 24, n), rng.integers(0, 2**33, n),
-                         rng.integers(0, 3, n)], 1).astype(np.uint64)
-        g = bench.gather_step(_FakeIndex(rows), n, 50, world, rank, dist.barrier, dist, torch, device="cpu")
+        rec_starts = np.array([0, 1000, 5000, 2**32 - 10], np.uint64)
+        seq = rng.integers(0, 3, n).astype(np.uint64)
+        rows = np.stack([np.sort(rng.integers(0, 2 * 50, n)), seq,
+                         rng.integers(0, 900, n), rng.integers(0, 3, n)], 1).astype(np.uint64)
+        res = []
+        for obj in (_FakeCompact(rows, rec_starts), _FakeWhole(rows)):
+            g = bench.gather_step(obj, getattr(obj, "rec_starts", None), 50, world, rank, dist.barrier, dist, torch,
+                                  device="cpu")
+            res += [g.get("records", -1), int(bool(g["verified"]))]
+        # the gathered records decode to every rank's rows, qids made global
+        c = _FakeCompact(rows, rec_starts)
+        parts = gather_compact_records(c.recs, c.block_qid0, c.block_end, 2 * 50 * rank)
+        mine = rows.copy()
+        mine[:, 0] += np.uint64(2 * 50 * rank)
+        allrows = [torch.zeros((57, 4), dtype=torch.int64) for _ in range(world)]
+        pad = torch.zeros((57, 4), dtype=torch.int64)
+        pad[:n] = torch.from_numpy(mine.view(np.int64))
+        dist.all_gather(allrows, pad)
         if rank == 0:
-            np.save(os.path.join(outdir, "g.npy"), np.array([g["records"], int(g["verified"])]))
+            got = np.concatenate([records_to_rows(r, q, e, rec_starts) for r, q, e in parts])
+            want = np.concatenate([a.numpy()[: 37 + 20 * r].view(np.uint64) for r, a in enumerate(allrows)])
+            res.append(int(np.array_equal(got, want)))
+            np.save(os.path.join(outdir, "g.npy"), np.array(res))
     finally:
         dist.destroy_process_group()
 
@@ -160,5 +186,5 @@ def test_bench_gather_step_two_ranks():
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_bench_gather_worker, args=(2, _free_port(), d), nprocs=2, join=True,
                            start_method="spawn")
-        recs, ok = np.load(os.path.join(d, "g.npy"))
-    assert recs == 37 + 57 and ok == 1
+        r = np.load(os.path.join(d, "g.npy"))
+    assert list(r) == [37 + 57, 1, 37 + 57, 1, 1]
