@@ -331,11 +331,14 @@ def main():
         search_bytes = 64.0 * cnt["ext_lines"] + pats.shape[0] * ((rlen + 7) // 8) * 4.0
         # per text task: the source blocks of its window (16-B blocks of 32
         # symbols, 3 bit planes: pass.cpp winBlocks, plus the block its
-        # funnel-shifted copy starts in), the task record, the SA entry; per
-        # pattern its blocks once (the tasks of one pattern share them in L2)
+        # funnel-shifted copy starts in), the task record, and the SA entry
+        # unless the task came with its text position (k-mer seeds with one
+        # occurrence: text_pos_tasks); per pattern its blocks once (the tasks
+        # of one pattern share them in L2)
         win_blocks = (rlen + 2 * k + 62) // 32
         pat_blocks = (rlen + 31) // 32
-        text_bytes = cnt["conversions"] * (16.0 * win_blocks + 16 + 4) + pats.shape[0] * 16.0 * pat_blocks
+        text_bytes = (cnt["conversions"] * (16.0 * win_blocks + 16) + 4.0 * (cnt["conversions"] - cnt["text_pos_tasks"])
+                      + pats.shape[0] * 16.0 * pat_blocks)
         locate_bytes = 4.0 * cnt["hits"]
         text_ms_step = text_ms / args.steps
         kern = {"kSearchFM": {"ms": round(search_ms_step, 2), "bytes": search_bytes,
@@ -399,6 +402,7 @@ def main():
                  "rank_nodes_per_read": round(cnt["rank_nodes"] / nreads, 1),
                  "text_nodes_per_read": round(cnt["text_nodes"] / nreads, 1),
                  "conversions_per_read": round(cnt["conversions"] / nreads, 2),
+                 "positioned_tasks_per_read": round(cnt["text_pos_tasks"] / nreads, 2),
                  "fm_lane_util": round(cnt["nodes"] / max(1, 64 * cnt["fm_iterations"]), 3),
                  "text_lane_util": round(cnt["text_active"] / max(1, 64 * cnt["text_iterations"]), 3),
                  "text_iterations_per_wave": round(cnt["text_iterations"] / max(1, 4 * cnt["search_grid"]), 1),

@@ -183,7 +183,9 @@ Ctx* newCtx(int device) {
     // the seed and FM kernels, which must not queue behind it
     {
         std::vector<uint32_t> mask((size_t)(c->numCU + 31) / 32, 0xFFFFFFFFu);
-        if (hipExtStreamCreateWithCUMask(&c->stB, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+        const char* oq = std::getenv("SAHARA_TEXT_OWN_QUEUE");  // 0: a plain stream (A/B)
+        if (!(oq && std::atoi(oq) == 0) &&
+            hipExtStreamCreateWithCUMask(&c->stB, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
             c->textOwnQueue = true;
         } else {
             (void)hipGetLastError();
@@ -223,8 +225,8 @@ Ctx* newCtx(int device) {
     }
     for (void*& p : c->outStage) SH_HIP(hipHostMalloc(&p, Ctx::kOutChunk));
     c->small.reserve(8);
-    c->counters.reserve(16);
-    SH_HIP(hipMemset(c->counters.ptr, 0, 16 * sizeof(unsigned long long)));
+    c->counters.reserve(kCounters);
+    SH_HIP(hipMemset(c->counters.ptr, 0, kCounters * sizeof(unsigned long long)));
     return c.release();
 }
 
@@ -1018,7 +1020,7 @@ int sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len) {
             sl.hits.reserve((size_t)c->hitCap + 1);
             sl.rank.reserve((size_t)c->hitCap + 1);
             sl.tasks.reserve((size_t)c->taskCap);
-            sl.qcnt.reserve(maxBatch + 1);
+            sl.qcnt.reserve(2 * (maxBatch + 1));  // (FM counts, text counts: pass.cpp)
         }
         if (len) {
             const uint64_t patWords = (len + 7) / 8, patBlocks = (len + 31) / 32;

@@ -122,12 +122,13 @@ struct DeviceIndex {
     // Resident for the search (HBM is 288 GB; at 3 Gbp these are 12 + 1.5 GB):
     DevBuf<uint32_t> saFull;        // SA[row] for every row: locate = one read
     DevBuf<uint4> text3;            // text as 3-bit-plane blocks of 32 symbols, '$' = 0, kTextPadBlocks zero blocks after
-    // k-mer table: the bidirectional cursor {lb, lbRev, len, 0} of every
+    // k-mer table: the bidirectional cursor {lb, lbRev, len, pos} of every
     // ACGT string of length kmerK (2 bits per symbol, first symbol most
     // significant). A search whose first kmerK steps admit no error starts
     // at depth kmerK with one lookup instead of kmerK rank steps.
     DevBuf<uint4> kmer;
     uint32_t kmerK = 0;
+    bool kmerPos = false;           // an entry with len 1 holds SA[lb] in its fourth word
     uint64_t deviceBytes() const {
         return (occF.cap + occR.cap) * sizeof(OccLine) + samples.cap * 4 + dRecStarts.cap * 8 + saFull.cap * 4 +
                text3.cap * sizeof(uint4) + kmer.cap * sizeof(uint4);

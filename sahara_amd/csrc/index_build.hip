@@ -395,9 +395,12 @@ struct Cvec {
 // Level j of the table from level j-1: each string w extends to the right by
 // A, C, G, T (extendRight on the reverse BWT: one rank of all symbols at lbRev
 // and lbRev + len; the forward lb moves by the occurrences of the smaller
-// symbols, '$' first). Empty intervals stay empty.
+// symbols, '$' first). Empty intervals stay empty. At the last level (sa set)
+// a string that occurs once also gets its text position, SA[lb], in the
+// entry's fourth word: kSeedItems hands such a seed to the text phase as a
+// task that needs no SA read of its own.
 __global__ void kKmerLevel(const OccLine* __restrict__ occR, Cvec C, uint32_t sigma, const uint4* __restrict__ prev,
-                           uint64_t count, uint4* __restrict__ next) {
+                           uint64_t count, uint4* __restrict__ next, const uint32_t* __restrict__ sa) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 w = prev[i];
@@ -419,7 +422,9 @@ __global__ void kKmerLevel(const OccLine* __restrict__ occR, Cvec C, uint32_t si
             uint32_t j = 0;
             for (uint32_t c = 1; c < sigma; ++c) {
                 const bool acgt = !(sigma == 6 && c == 4);  // N is not in the table
-                if (acgt) out[j++] = occ[c] ? make_uint4(acc, base[c], occ[c], 0u) : make_uint4(0u, 0u, 0u, 0u);
+                if (acgt)
+                    out[j++] = occ[c] ? make_uint4(acc, base[c], occ[c], sa && occ[c] == 1u ? sa[acc] : 0u)
+                                      : make_uint4(0u, 0u, 0u, 0u);
                 acc += occ[c];
             }
         }
@@ -600,13 +605,15 @@ void buildKmerTable(DeviceIndex& I, uint32_t K, hipStream_t st) {
     for (uint32_t j = 1; j <= K; ++j) {
         uint4* next = j == K ? I.kmer.ptr : (prev == t0.ptr ? t1.ptr : t0.ptr);
         hipLaunchKernelGGL(kKmerLevel, dim3((unsigned)std::min<uint64_t>((count + 255) / 256, 1u << 16)), dim3(256), 0,
-                           st, I.occR.ptr, C, I.sigma, prev, count, next);
+                           st, I.occR.ptr, C, I.sigma, prev, count, next,
+                           j == K && I.saFull.cap >= I.n ? I.saFull.ptr : nullptr);
         SH_HIP(hipGetLastError());
         count *= 4;
         prev = next;
     }
     SH_HIP(hipStreamSynchronize(st));
     I.kmerK = K;
+    I.kmerPos = I.saFull.cap >= I.n;
 }
 
 void exportParts(const DeviceIndex& I, uint8_t* bwtF, uint8_t* bwtR, uint64_t* sampledBits, uint32_t* samples,

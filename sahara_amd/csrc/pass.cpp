@@ -80,7 +80,9 @@ void run(Ctx* c, bool count) {
                   &sahara_stats::conversions, &sahara_stats::fm_iterations, &sahara_stats::text_iterations,
                   &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
                   &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
-                  &sahara_stats::text_steps, &sahara_stats::text_launches, &sahara_stats::text_fallbacks})
+                  &sahara_stats::text_steps, &sahara_stats::text_launches, &sahara_stats::text_fallbacks,
+                  &sahara_stats::text_pos_tasks, &sahara_stats::text_cycles_idle, &sahara_stats::text_cycles_grab,
+                  &sahara_stats::text_cycles_life})
                 T.*f += S.*f;
             for (double sahara_stats::*f : {&sahara_stats::search_ms, &sahara_stats::locate_ms, &sahara_stats::sort_ms,
                                             &sahara_stats::text_ms, &sahara_stats::seed_ms})
@@ -318,10 +320,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // chain (kCountRows) did it, beside the next batches' search, where the
     // chain lagged behind them: C3 805M -> 843M, C2 482M -> 503M, C5 94.2M ->
     // 95.6M reads/s (profiles/r04_emit_rank_ab.txt)
+    // Text hits are counted per query without a rank (TextSlot::tcnt, the
+    // second half of the slot's qcnt buffer) and placed by kLocate.
     for (auto& sl : c->slot) {
-        sl.qcnt.reserve(maxBatch + 1);
-        SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
+        sl.qcnt.reserve(2 * (maxBatch + 1));
+        SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, 2 * (maxBatch + 1) * sizeof(uint32_t), c->st));
     }
+    auto tcntOf = [&](Ctx::Slot& sl) { return sl.qcnt.ptr + maxBatch + 1; };
     hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
     c->mark("pass", 0);
     SH_HIP(hipStreamSynchronize(c->st));
@@ -329,7 +334,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     SH_HIP(hipStreamSynchronize(c->stC));
     SH_HIP(hipStreamSynchronize(c->stD));
     c->mark("pass synced", 0);
-    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, 16 * sizeof(unsigned long long), sA));
+    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, kCounters * sizeof(unsigned long long), sA));
+    // the text launch's timeout report (search.hip kSearchText): count, max, min, max
+    SH_HIP(hipMemsetAsync(c->counters.ptr + 26, 0, 2 * sizeof(unsigned long long), sA));
+    SH_HIP(hipMemsetAsync(c->counters.ptr + 28, 0xFF, sizeof(unsigned long long), sA));
+    SH_HIP(hipMemsetAsync(c->counters.ptr + 29, 0, sizeof(unsigned long long), sA));
     c->nout = 0;
     c->sinkDone = 0;
     c->sinkOk = c->sink != nullptr || c->blockRecs != nullptr;
@@ -352,7 +361,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     auto writeSlotTable = [&](hipStream_t s) {
         for (size_t i = 0; i < Ctx::kSlots; ++i) {
             Ctx::Slot& sl = c->slot[i];
-            c->slotHost[i] = TextSlot{sl.tasks.ptr, sl.queues.ptr, sl.hits.ptr, sl.rank.ptr, sl.qcnt.ptr, sl.small.ptr};
+            c->slotHost[i] = TextSlot{sl.tasks.ptr, sl.queues.ptr, sl.hits.ptr, sl.rank.ptr, sl.qcnt.ptr, tcntOf(sl),
+                                      sl.small.ptr};
         }
         SH_HIP(hipMemcpyAsync(c->slotTab.ptr, c->slotHost, Ctx::kSlots * sizeof(TextSlot), hipMemcpyHostToDevice, s));
     };
@@ -378,11 +388,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         for (uint64_t b = 0; b <= nbatch; ++b)
             c->batchHost[b] = b < nbatch ? TextBatch{bstart[b], (uint32_t)(bstart[b + 1] - bstart[b]), (uint32_t)(b % Ctx::kSlots)}
                                          : TextBatch{bstart[nbatch], 0u, 0u};
-        c->bflags.reserve(nbatch * 4);
+        c->bflags.reserve(nbatch * textFlagWords(textBlocks));
         c->batchTab.reserve(nbatch + 1);
         c->slotTab.reserve(Ctx::kSlots);
         c->ctl.reserve(4);
-        SH_HIP(hipMemsetAsync(c->bflags.ptr, 0, nbatch * 4 * sizeof(uint32_t), sA));
+        SH_HIP(hipMemsetAsync(c->bflags.ptr, 0, nbatch * textFlagWords(textBlocks) * sizeof(uint32_t), sA));
         SH_HIP(hipMemsetAsync(c->ctl.ptr, 0, 4 * sizeof(uint32_t), sA));
         SH_HIP(hipMemcpyAsync(c->batchTab.ptr, c->batchHost, (nbatch + 1) * sizeof(TextBatch), hipMemcpyHostToDevice, sA));
         writeSlotTable(sA);
@@ -404,7 +414,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sl.tasks.reserve((size_t)c->taskCap);
         SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
         if (serial && split)  // a re-run of the batch publishes its tasks again
-            SH_HIP(hipMemsetAsync(c->bflags.ptr + 4 * b, 0, 4 * sizeof(uint32_t), sA));
+            SH_HIP(hipMemsetAsync(c->bflags.ptr + textFlag(b, 0, textBlocks), 0,
+                                  textFlagWords(textBlocks) * sizeof(uint32_t), sA));
         SearchArgs a{};
         a.occF = c->I.occF.ptr;
         a.occR = c->I.occR.ptr;
@@ -450,6 +461,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sd.n = a.n;
         sd.kmer = c->verify && c->I.kmerK ? c->I.kmer.ptr : nullptr;
         sd.kmerK = c->I.kmerK;
+        sd.kmerPos = c->I.kmerPos ? 1u : 0u;
+        if (const char* e = std::getenv("SAHARA_KMER_POS"); e && std::atoi(e) == 0) sd.kmerPos = 0;  // (A/B)
         sd.kmerStart = c->kmerStart.ptr;
         sl.seeds.reserve(a.nitems);
         sl.seedItem.reserve(a.nitems);
@@ -485,7 +498,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             ensureUploaded(c, p1, sD);
             SH_HIP(hipEventRecord(sl.fmStart, sD));
             seeds(0, (uint32_t)(p1 * c->nsearch));
-            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b, sD);
+            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sD);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
             ensureUploaded(c, bstart[b + 1], sD);
             SH_HIP(hipEventRecord(sl.seedMid, sD));  // the second part's seeds start (after the upload's wait)
@@ -499,7 +512,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // the seed tasks end here: the text phase may start on them (a
             // lone device-resident batch's text phase waits for its FM phase:
             // published after it below)
-            if (split && (early || serial)) launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b, sD);
+            if (split && (early || serial))
+                launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sD);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
         }
         SH_HIP(hipEventRecord(sl.seedDone, sD));
@@ -507,8 +521,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(sl.fmBegin, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
         if (split) {  // the batch's task list is final
-            if (!early && !serial) launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b, sA);
-            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + 4 * b + 1, sA);
+            if (!early && !serial)
+                launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sA);
+            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 1, textBlocks), textBlocks, sA);
         }
         SH_HIP(hipEventRecord(sl.fmDone, sA));
         ++S.search_launches;
@@ -521,14 +536,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // SAHARA_PIPELINE=0): one launch per batch after its FM phase, on the one
     // stream. SAHARA_TEXT_ONE_LAUNCH=0: one launch per batch, pipelined.
     bool textLaunched = false;
-    uint64_t wallKHz = 0;
-    if (split) {
-        int khz = 0;
-        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess && khz > 0)
-            wallKHz = (uint64_t)khz;
-        else
-            wallKHz = 100000;
-    }
+    // the kernel's wall clock (s_memrealtime) counts at 100 MHz on gfx950
+    // (MI355X_MICROARCH.md); the device attribute reported another rate
+    constexpr uint64_t wallKHz = 100000;
     auto launchTextRange = [&](uint64_t b0, uint64_t b1) {
         TextArgs t{};
         t.sa = c->I.saFull.ptr;
@@ -544,11 +554,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         t.b0 = (uint32_t)b0;
         t.b1 = (uint32_t)b1;
         t.bflags = c->bflags.ptr;
+        t.flagStride = (uint32_t)textFlagWords(textBlocks);
         t.hostDone = c->hostDone;
         t.ctl = c->ctl.ptr;
         // an idle wave gives up after 2 s without published work (the host
         // then redoes the pass batch by batch): no legitimate wait is that long
         t.timeoutTicks = wallKHz * 2000;
+        t.pollGap = std::max<uint64_t>(1, wallKHz * 2 / 1000);  // 2 us
         t.taskCap = c->taskCap;
         t.hitCap = c->hitCap;
         t.counters = c->counters.ptr;
@@ -624,6 +636,16 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // slots between two text phases)
         if (oneLaunch) {
             if (!waitTextDone(b)) {
+                if (std::getenv("SAHARA_DEBUG_TEXT")) {
+                    unsigned long long h[kCounters];
+                    SH_HIP(hipMemcpy(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost));
+                    std::fprintf(stderr, "text launch gave up at batch %llu of %llu: timed-out waves %llu, "
+                                 "waited max (b*2+ph %llu, ready %llu) min (b*2+ph %llu, lo %llu), pub %llu/%llu; "
+                                 "host done:", (unsigned long long)b, (unsigned long long)nbatch, h[26], h[27] >> 32,
+                                 h[27] & 1, h[28] >> 32, h[28] & 0xFFFFFFFFull, h[29] >> 32, h[29] & 0xFFFFFFFFull);
+                    for (uint64_t i = 0; i < nbatch; ++i) std::fprintf(stderr, " %u", c->hostDone[i]);
+                    std::fprintf(stderr, "\n");
+                }
                 textFailed = true;
                 overflow = true;  // redone batch by batch
                 return false;
@@ -661,6 +683,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             if (hs[2] & 2u) growCap(serial ? c->hitCap : seenHit, hs[1]);
             overflow = true;
             SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (nb + 1) * sizeof(uint32_t), sC));  // the re-run counts again
+            SH_HIP(hipMemsetAsync(tcntOf(sl), 0, (nb + 1) * sizeof(uint32_t), sC));
             resetSlot(sl, sC);
             return false;
         }
@@ -671,7 +694,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(c->ev[2], sC));
         SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
         c->partial.reserve(scanTiles((uint32_t)nb));
-        querySegments(sl.qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4,
+        querySegments(sl.qcnt.ptr, tcntOf(sl), (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4,
                       c->huge.ptr, c->small.ptr + 5, sC);
         uint32_t* pr = c->pinned + b * 16;
         SH_HIP(hipMemcpyAsync(pr + 8, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
@@ -696,6 +719,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         la.nhits = nh;
         la.qoff = c->qoff.ptr;
         la.rank = sl.rank.ptr;
+        la.tcnt = tcntOf(sl);
         la.occF = c->I.occF.ptr;
         for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
         la.samples = c->I.samples.ptr;
@@ -907,7 +931,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipStreamSynchronize(c->stF));
     }
     if (count) {
-        unsigned long long h[16];
+        unsigned long long h[kCounters];
         SH_HIP(hipMemcpyAsync(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost, sC));
         SH_HIP(hipStreamSynchronize(sC));
         S.nodes = h[0];
@@ -925,6 +949,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         S.text_cycles_emit = h[13];
         S.text_compare_steps = h[14];
         S.text_steps = h[15];
+        S.text_pos_tasks = h[16];
+        S.text_cycles_idle = h[17];
+        S.text_cycles_grab = h[18];
+        S.text_cycles_life = h[19];
+        if (std::getenv("SAHARA_DUMP_COUNTERS")) {  // (profiling hook: the raw count-mode counters)
+            for (uint32_t i = 0; i < kCounters; ++i) std::fprintf(stderr, "%s%llu", i ? " " : "counters ", h[i]);
+            std::fprintf(stderr, "\n");
+        }
     }
 }
 

@@ -56,6 +56,7 @@ struct SeedArgs {
     uint32_t n;
     const uint4* kmer;          // k-mer table (DeviceIndex::kmer), nullptr = start every item at the root
     uint32_t kmerK;
+    uint32_t kmerPos;           // the table holds SA[lb] of single-row entries: their tasks carry text positions
     const uint32_t* kmerStart;  // per search: pattern offset of its error-free first kmerK steps, ~0u = n/a
     uint4* seeds;
     uint32_t* seedItem;
@@ -81,8 +82,9 @@ struct TextSlot {
     const uint4* tasks;      // text tasks (row, |t|, pattern, meta | search << 24)
     uint32_t* queues;        // striped counters: [256, 512) the seed tasks, [512, 768) the FM phase's
     uint4* hits;
-    uint32_t* rank;          // rows ranked where the hits are written (as SearchArgs)
+    uint32_t* rank;          // (the FM phase's ranks; text hits take theirs in kLocate)
     uint32_t* qcnt;
+    uint32_t* tcnt;          // per-query text hit counts (non-returning adds; kLocate ranks them)
     uint32_t* small;         // -, hitCount, flags, filled, taskCount, ...
 };
 // One batch of a pass (its patterns [q0, q0 + npat) of the staged ones).
@@ -91,8 +93,15 @@ struct TextBatch {
     uint32_t npat;
     uint32_t slot;
 };
+// work counters of count mode (sahara_stats): [0..15] as SearchArgs::counters
+// lists them, [16] text tasks that came with their text position (kTaskPos),
+// [17..19] text-kernel cycles idle / in grab / whole wave lives
+constexpr uint32_t kCounters = 40;
 // a published task count (kPublish): bit 31 set once the count is final for its phase
 constexpr uint32_t kTaskReady = 0x80000000u;
+// a task record whose x is already a text position (a k-mer seed with one
+// occurrence: DeviceIndex::kmerPos), not an SA row: bit 31 of its y (|t|)
+constexpr uint32_t kTaskPos = 0x80000000u;
 
 struct TextArgs {
     const uint32_t* sa;      // full SA: task records carry SA rows, the kernel reads their text positions
@@ -108,11 +117,14 @@ struct TextArgs {
     const TextBatch* batches;  // b1 + 1 entries (the last one is never a batch of the launch)
     const TextSlot* slots;
     uint32_t b0, b1;
-    uint32_t* bflags;        // per batch 4 words: seed tasks | kTaskReady, all tasks | kTaskReady,
-                             // workgroups past the batch, -; zero before the launch
+    uint32_t* bflags;        // per batch flagStride words (textFlagWords): the seed tasks' count and then
+                             // all tasks' count | kTaskReady, each once per workgroup 16 words apart
+                             // (textFlag), then the workgroups past the batch; zero before the launch
+    uint32_t flagStride;
     uint32_t* hostDone;      // pinned host memory, per batch: 1 once its text phase is done
     const uint32_t* ctl;     // [0] != 0: the host aborts the pass
     uint64_t timeoutTicks;   // an idle wave gives up after waiting this long (wall clock ticks)
+    uint64_t pollGap;        // a workgroup polls an unpublished task count at most once per this many ticks
     uint32_t taskCap;
     uint32_t hitCap;
     unsigned long long* counters;
@@ -131,6 +143,7 @@ struct LocateArgs {
     uint64_t nhits;
     const uint64_t* qoff;          // per-query row segments (querySegments)
     const uint32_t* rank;          // per cursor: slot of its first row in the segment (querySegments)
+    uint32_t* tcnt;                // per query: its text hits still to place (the segment's tail); zero on return
     const OccLine* occF;
     uint32_t C[8];
     const uint32_t* samples;
@@ -151,8 +164,13 @@ int textShapeOf(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);
-// *flag = min(*count, cap) | kTaskReady on stream st (the text phase's hand-off)
-void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, hipStream_t st);
+// flag[16 w] = min(*count, cap) | kTaskReady for w < nwg, on stream st (the
+// text phase's hand-off: one copy per text workgroup)
+void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, uint32_t nwg, hipStream_t st);
+// the text phase's hand-off words per batch for a launch of nwg workgroups,
+// and where batch b's phase ph (0: seed tasks, 1: all) copies begin
+inline size_t textFlagWords(uint32_t nwg) { return 2 * (size_t)nwg * 16 + 32; }
+inline size_t textFlag(uint64_t b, uint32_t ph, uint32_t nwg) { return b * textFlagWords(nwg) + (size_t)ph * nwg * 16; }
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st);
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst
@@ -188,9 +206,11 @@ void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, ui
 // radix sort).
 uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
 // qcnt: the batch's per-query row counts, which the search kernels add up
-// as they write the hits (SearchArgs::qcnt); all zero on return
-void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
-                   uint32_t* huge, uint32_t* nhuge, hipStream_t st);
+// as they write the hits (SearchArgs::qcnt); all zero on return. tcnt: the
+// per-query text hit counts (TextSlot::tcnt), read only: a query's segment
+// holds qcnt + tcnt rows, its text hits the last tcnt (placed by kLocate)
+void querySegments(uint32_t* qcnt, const uint32_t* tcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
+                   uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
 size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
 // long segments (> 64 rows, listed in big) are sorted in LDS, huge ones

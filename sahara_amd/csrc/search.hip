@@ -261,7 +261,7 @@ __device__ __forceinline__ uint32_t seedCode(const SeedArgs& a, uint32_t i) {
 // translation, not bandwidth, bounds these random lookups: tools/gather_bench).
 // Must be called by all lanes of the wave.
 template <int SIGMA>
-__device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& keep) {
+__device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& keep, uint32_t& textPos) {
     keep = i < a.nitems;
     const uint32_t code = seedCode<SIGMA>(a, i);
     const bool need = keep && code != ~0u;
@@ -278,6 +278,7 @@ __device__ __forceinline__ uint4 seedOf(const SeedArgs& a, uint32_t i, bool& kee
     const uint2 gE = make_uint2(pairSwap(rE.x), pairSwap(rE.y));     // even <- bytes 8-15 of its entry
     const uint2 gO = make_uint2(pairSwap(rO.x), pairSwap(rO.y));     // odd <- bytes 0-7 of its entry
     const uint4 t = odd ? make_uint4(gO.x, gO.y, rO.x, rO.y) : make_uint4(rE.x, rE.y, gE.x, gE.y);
+    textPos = t.w;  // SA[lb] when the k-mer occurs once (DeviceIndex::kmerPos)
     if (!need) return make_uint4(0u, 0u, a.n, kDeltaZero);
     keep = t.z != 0u;
     return make_uint4(t.x, t.y, t.z, packMeta(a.kmerK, 0u, OP_MS, OP_MS));
@@ -296,10 +297,11 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
     uint64_t cTasks = 0;
     for (uint32_t base = a.itemBegin + blockIdx.x * 1024u; base < a.nitems; base += gridDim.x * 1024u) {  // block-uniform
         uint4 cur[4];
+        uint32_t tpos[4];
         bool keep[4], task[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k]);
+            cur[k] = seedOf<SIGMA>(a, base + k * 256u + threadIdx.x, keep[k], tpos[k]);
             task[k] = keep[k] && a.toText && cur[k].z == 1u && (cur[k].w & 0xFFFFu) < a.m;
             keep[k] = keep[k] && !task[k];
         }
@@ -330,11 +332,14 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
                 a.seeds[at] = cur[k];
                 a.seedItem[at] = item;
             }
-            if (task[k]) {  // (row, |t| = kmerK, pattern, node meta | search << 24)
+            if (task[k]) {  // (row, |t| = kmerK, pattern, node meta | search << 24), or with
+                            // the text position instead of the row (kTaskPos)
                 const uint32_t at = tslot + (uint32_t)__popcll(mt[k] & ltMask);
                 const uint32_t pid = item / a.nsearch, sIdx = item - pid * a.nsearch;
                 if (at < a.taskCap)
-                    a.tasks[at] = make_uint4(cur[k].x, cur[k].w & 0xFFFFu, pid, (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
+                    a.tasks[at] = make_uint4(a.kmerPos ? tpos[k] : cur[k].x,
+                                             (cur[k].w & 0xFFFFu) | (a.kmerPos ? kTaskPos : 0u), pid,
+                                             (cur[k].w & 0x00FFFFFFu) | (sIdx << 24));
                 else
                     atomicOr(a.flags, 8u);
                 ++cTasks;
@@ -344,7 +349,10 @@ __global__ __launch_bounds__(256) void kSeedItems(SeedArgs a) {
         }
         __syncthreads();  // wcount / blockBase reused next round
     }
-    if (a.counters && cTasks) atomicAdd(a.counters + 6, (unsigned long long)cTasks);
+    if (a.counters && cTasks) {
+        atomicAdd(a.counters + 6, (unsigned long long)cTasks);
+        if (a.kmerPos) atomicAdd(a.counters + 16, (unsigned long long)cTasks);
+    }
 }
 
 // =========================================================== phase 1: FM ====
@@ -781,9 +789,12 @@ __host__ __device__ constexpr TextShape textShape(int shape) {
 // One launch serves the batches [b0, b1) of a pass, so the text phase has no
 // launch boundary (and no grid drain and refill) between batches. A batch's
 // task list fills in two steps: the tasks kSeedItems writes (their count
-// published in bflags[4b] by kPublish on the seed stream), then the tasks the
-// FM phase appends (the final count in bflags[4b + 1], published after
-// kSearchFM). A wave's queue walks the batches in order, phase by phase, taking
+// published by kPublish on the seed stream: textFlag(b, 0)), then the tasks
+// the FM phase appends (the final count, textFlag(b, 1), published after
+// kSearchFM; each count is written once per workgroup, 64 B apart, so that
+// every workgroup polls a line of its own: a few hundred pollers of one word
+// slowed every kernel beside them 2-3x). A wave's queue walks the batches in
+// order, phase by phase, taking
 // 64-task chunks from the phase's striped counters. The lanes of one wave hold
 // tasks of at most two consecutive batches (a lane's batch parity: `lpar`),
 // each with its own hit range: the queue moves on from batch qb only once the
@@ -792,7 +803,7 @@ __host__ __device__ constexpr TextShape textShape(int shape) {
 // Retiring batch b (the wave holds nothing of it and its queue has moved past
 // it): the wave closes its hit range, stores its deferred ranks and releases
 // its writes (agent scope), then arrives at the workgroup's counter of b in
-// LDS; the workgroup's last wave adds one to bflags[4b + 2], and the workgroup
+// LDS; the workgroup's last wave adds one to the batch's arrival counter, and the workgroup
 // whose add completes the grid tells the host (hostDone[b] = 1, a system-scope
 // store to pinned memory), which starts the batch's locate chain and later
 // reuses the batch's slot: every wave has passed the batch by then, so none
@@ -813,18 +824,57 @@ typedef __attribute__((address_space(1))) uint32_t GlobalU32;
 #else
 #define GLOB(T, p) ((T*)(p))
 #endif
+// A 16-B record through a global pointer: uint4 is a class type whose copy
+// goes through a generic reference (a flat load again), a native vector is not
+typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 loadGlobal4(const uint4* p) {
+    const U32x4 v = *GLOB(const U32x4, p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ uint32_t pollWord(const uint32_t* p) {  // relaxed, agent scope: an sc1 load
     return __hip_atomic_load((GlobalU32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// What the text kernel hands to the locate chain while it keeps running (hit
+// records, ranks) is stored write-through (sc1: relaxed agent-scope stores),
+// so that a wave only waits for its stores (vmcnt) before it reports a batch
+// done: a release fence there (buffer_wbl2) wrote back the whole L2 of its
+// XCD at every wave's every batch, dirty lines of every other kernel included,
+// and slowed everything beside the text phase 3-10x.
+typedef __attribute__((address_space(1))) uint64_t GlobalU64;
+#ifdef SAHARA_V_PLAIN
+__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) { *GLOB(uint32_t, p) = v; }
+__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) { *GLOB(uint4, p) = v; }
+#else
+__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((GlobalU32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) {
+    GlobalU64* q = (GlobalU64*)p;
+    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
 
 template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
 __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t arrive[8];  // waves of this workgroup past batch b, at b % 8
+    // published task counts this workgroup has seen ([b % 8][phase], tagged
+    // with b), and when one of its waves last polled one: a wave that finds
+    // its phase unpublished here polls global memory only if no wave of the
+    // workgroup did in the last kPollGap (a few hundred pollers of one word
+    // otherwise slow every kernel beside them)
+    __shared__ uint32_t pubTag[8][2], pubVal[8][2];
+    __shared__ uint64_t lastPoll;
+    __shared__ uint32_t abortSeen;  // the host's abort, as wave 0 of the workgroup last polled it
     uint2* SC = reinterpret_cast<uint2*>(lds);
     uint32_t* slot = lds + a.tableWords;  // >= kTextTableMin: the window's block -1 stays in LDS
     for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = a.table[i];
-    if (threadIdx.x < 8) arrive[threadIdx.x] = 0;
+    if (threadIdx.x < 8) {
+        arrive[threadIdx.x] = 0;
+        pubTag[threadIdx.x][0] = pubTag[threadIdx.x][1] = ~0u;
+    }
+    if (threadIdx.x == 0) lastPoll = 0, abortSeen = 0;
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -841,12 +891,37 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
     const uint32_t m = a.m;
     const uint32_t patBytes = patBlocks * 16u;
-    // patterns of batch b (pattern ids in task records are batch-local)
-    auto patBufOf = [&](uint32_t b) {
-        const TextBatch& B = a.batches[b];
-        return bufferOf(a.pats3 + B.q0 * patBlocks, B.npat * patBytes);
+    // patterns of the batches the wave holds, by batch parity (pattern ids in
+    // task records are batch-local): read from the batch table when the queue
+    // reaches a batch, so that a chunk switch does not wait for the table
+    const uint4 *patP0 = nullptr, *patP1 = nullptr;
+    uint32_t patN0 = 0, patN1 = 0;
+    auto loadPats = [&](uint32_t b) __attribute__((always_inline)) {
+        const TextBatch B = a.batches[b];
+        if (b & 1u) { patP1 = a.pats3 + B.q0 * patBlocks; patN1 = B.npat * patBytes; }
+        else { patP0 = a.pats3 + B.q0 * patBlocks; patN0 = B.npat * patBytes; }
     };
-    auto slotOf = [&](uint32_t b) -> const TextSlot& { return a.slots[a.batches[b].slot]; };
+    loadPats(a.b0);
+    auto patBufOf = [&](uint32_t b) __attribute__((always_inline)) {
+        return (b & 1u) ? bufferOf(patP1, patN1) : bufferOf(patP0, patN0);
+    };
+    // the slot buffers of the (at most two) batches the wave holds, by batch
+    // parity: loaded when the queue reaches a batch, so emission and retire
+    // read registers, not the tables
+    TextSlot slotP0 = a.slots[a.batches[a.b0].slot], slotP1 = slotP0;  // (the other parity: when qb moves)
+    // field by field, so that the structs stay in registers (a reference
+    // chosen at run time would put them in scratch memory)
+    auto slotFor = [&](uint32_t p) __attribute__((always_inline)) {
+        TextSlot r;
+        r.tasks = p ? slotP1.tasks : slotP0.tasks;
+        r.queues = p ? slotP1.queues : slotP0.queues;
+        r.hits = p ? slotP1.hits : slotP0.hits;
+        r.rank = p ? slotP1.rank : slotP0.rank;
+        r.qcnt = p ? slotP1.qcnt : slotP0.qcnt;
+        r.tcnt = p ? slotP1.tcnt : slotP0.tcnt;
+        r.small = p ? slotP1.small : slotP0.small;
+        return r;
+    };
 
     // ---- the wave's place in the pass (wave-uniform)
     uint32_t qb = a.b0, qph = 0, lo = a.b0;  // the queue's batch and phase; the oldest batch the wave holds
@@ -856,8 +931,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint32_t* qCtr = nullptr;                 // the phase's striped counters (StripedQueue, unrolled
     uint32_t qN = 0, qStripe = 0, qTries = 0; // into plain values: they stay in registers)
     const uint4* qTasks = nullptr;
-    // the batch of parity p among the (at most two) the wave holds
-    auto batchOf = [&](uint32_t p) { return (lo & 1u) == p ? lo : qb; };
 
     uint32_t sp = 0, pid = 0, wb = 0, sBase = 0, lpar = 0;
     bool have = false, bad = false;
@@ -875,7 +948,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     bool nextRaw = false;
     auto resolveNext = [&]() {
         if (nextRaw) {  // wave-uniform
-            if (nBase + lane < nEnd) nextRec.x = a.sa[nextRec.x];
+            if (nBase + lane < nEnd && !(nextRec.y & kTaskPos)) nextRec.x = a.sa[nextRec.x];
             nextRaw = false;
         }
     };
@@ -887,12 +960,30 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             if (qb >= a.b1) return 2u;
             if (!qReady) {
                 uint32_t f = 0;
-                if (lane == 0) f = pollWord(a.bflags + 4u * qb + qph);
+                if (lane == 0) {
+                    const uint32_t r = qb & 7u;
+                    if (pubTag[r][qph] == qb) {
+                        f = pubVal[r][qph];
+                    } else {
+                        const uint64_t now = wall_clock64();
+                        if (now - lastPoll >= a.pollGap) {
+                            lastPoll = now;
+                            f = pollWord(a.bflags + (size_t)qb * a.flagStride + (qph * gridDim.x + blockIdx.x) * 16u);
+                            if (f & kTaskReady) {
+                                pubVal[r][qph] = f;
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                                pubTag[r][qph] = qb;
+                            }
+                        }
+                    }
+                }
                 f = __builtin_amdgcn_readfirstlane(f);
                 if (!(f & kTaskReady)) return 0u;
+#ifndef SAHARA_V_NOACQ
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // then the task records
+#endif
                 const uint32_t cnt = min(f & ~kTaskReady, a.taskCap);
-                const TextSlot& Sl = slotOf(qb);
+                const TextSlot Sl = slotFor(qb & 1u);
                 if (qph == 0) qSnap = cnt;
                 qLo = qph == 0 ? 0u : min(qSnap, cnt);
                 qCtr = Sl.queues + 256u * (1u + qph);
@@ -927,7 +1018,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 nEnd = qLo + e;
                 nBat = qb;
                 nextRec = make_uint4(0, 0, 0, 0);
-                if (nBase + lane < nEnd) nextRec = uint4(*GLOB(const uint4, qTasks + nBase + lane));
+                if (nBase + lane < nEnd) nextRec = loadGlobal4(qTasks + nBase + lane);
                 haveNext = true;
                 nextRaw = true;
                 return 1u;
@@ -941,22 +1032,28 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             ++qb;
             qph = 0;
             qReady = false;
+            if (qb < a.b1) {
+                loadPats(qb);
+                const TextSlot t = a.slots[a.batches[qb].slot];
+                if (qb & 1u) {
+                    slotP1.tasks = t.tasks; slotP1.queues = t.queues; slotP1.hits = t.hits;
+                    slotP1.rank = t.rank; slotP1.qcnt = t.qcnt; slotP1.tcnt = t.tcnt; slotP1.small = t.small;
+                } else {
+                    slotP0.tasks = t.tasks; slotP0.queues = t.queues; slotP0.hits = t.hits;
+                    slotP0.rank = t.rank; slotP0.qcnt = t.qcnt; slotP0.tcnt = t.tcnt; slotP0.small = t.small;
+                }
+            }
         }
     };
-    // This wave is past batch b: hit range closed, ranks stored, writes
+    // This wave is past batch b: hit range closed, writes
     // released, arrival counted. Wave-uniform, all lanes active.
-    uint32_t rankSlot = ~0u, rankVal = 0, rankPar = 0;  // the lane's last hit whose rank is not stored yet
     auto retire = [&](uint32_t b) __attribute__((always_inline)) {
         const uint32_t p = b & 1u;
-        const TextSlot& Sl = slotOf(b);
-        if (rankSlot != ~0u && rankPar == p) {
-            *GLOB(uint32_t, Sl.rank + rankSlot) = rankVal;
-            rankSlot = ~0u;
-        }
+        const TextSlot Sl = slotFor(p);
         // the unused tail of the hit range: empty records (len 0) for the locate scan
         const uint32_t hn = p ? hn1 : hn0, he = p ? he1 : he0;
         for (uint32_t i = hn + lane; i < he; i += 64)
-            if (i < a.hitCap) *GLOB(uint4, Sl.hits + i) = make_uint4(0u, 0u, 0u, 0u);
+            if (i < a.hitCap) storeThrough(Sl.hits + i, make_uint4(0u, 0u, 0u, 0u));
         if (p) hn1 = he1 = 0;
         else hn0 = he0 = 0;
         const uint32_t fl = p ? filled1 : filled0;
@@ -965,15 +1062,18 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         else filled0 = 0;
         if (__any(bad) && lane == 0)
             __hip_atomic_fetch_or(GLOB(uint32_t, Sl.small + 2), 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // the wave's hits, ranks and counts reach memory before it arrives
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // the wave's hits and ranks (stored write-through) and counts reach
+        // memory before it arrives
+#ifndef SAHARA_V_NORETWAIT
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         if (lane == 0) {
             const uint32_t k = __hip_atomic_fetch_add(arrive + (b & 7u), 1u, __ATOMIC_ACQ_REL,
                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             if (k + 1u == blockDim.x / 64u) {  // the workgroup's last wave
                 arrive[b & 7u] = 0;
-                const uint32_t g = __hip_atomic_fetch_add((GlobalU32*)(a.bflags + 4u * b + 2u), 1u,
+                const uint32_t g = __hip_atomic_fetch_add((GlobalU32*)(a.bflags + (size_t)b * a.flagStride +
+                                                                       2u * gridDim.x * 16u), 1u,
                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (g + 1u == gridDim.x) __hip_atomic_store(a.hostDone + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
@@ -985,7 +1085,9 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     bool waiting = false;
     uint2 cur = make_uint2(0, 0);
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
-    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
+    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0, cyIdle = 0, cyGrab = 0, cyStart = 0, cySteal = 0,
+             cyRetire = 0, cyResolve = 0, cySwitch = 0, nGrab = 0, cyShfl = 0, cyTail = 0, cyTop = 0;
+    const uint64_t tBorn = COUNT ? clock64() : 0;
 
     for (;;) {
         // Starting a task costs a global round trip (window + pattern) that
@@ -997,24 +1099,31 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         const bool busy = idleMask != ~0ull;
         const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
         uint64_t pending = refill ? idleMask : 0ull;
-        if (pending) resolveNext();
-        bool dry = false;  // no task in hand for an idle lane
-        // (re)fill the prefetched chunk: at most two chunks serve one refill
-        // (64 tasks each, <= 64 idle lanes), so one grab before and one after
-        // the lane loop keep a chunk prefetched; a busy wave polls an
-        // unpublished phase every few iterations only
-        auto prefetch = [&]() __attribute__((always_inline)) {
-            if (haveNext) return;
-            if (busy && pollSkip) --pollSkip;
-            else if (grab() != 1u) pollSkip = 8;
-        };
-        if (pending) prefetch();
-        while (pending) {  // wave-uniform
+        if (COUNT) { const uint64_t r0 = clock64(); cyTop += r0 - t0; if (pending) resolveNext(); cyResolve += clock64() - r0; }
+        else if (pending) resolveNext();
+        bool dry = false, tried = false;  // no task in hand for an idle lane; grab() tried this refill
+        for (;;) {  // wave-uniform
+            // (re)fill the prefetched chunk: at most two chunks serve one
+            // refill (64 tasks each, <= 64 idle lanes). One call site, so
+            // that the prefetched records have one home register; a busy wave
+            // polls an unpublished phase every few iterations only
+            if (!haveNext && !tried && (pending || refill)) {
+                tried = true;
+                if (busy && pollSkip) {
+                    --pollSkip;
+                } else {
+                    const uint64_t g0 = COUNT ? clock64() : 0;
+                    if (grab() != 1u) pollSkip = 8;
+                    if (COUNT) { cyGrab += clock64() - g0; ++nGrab; }
+                }
+            }
+            if (!pending) break;
             if (qNext >= qEnd) {  // switch to the prefetched chunk
                 if (!haveNext) {
                     dry = true;
                     break;
                 }
+                const uint64_t w0 = COUNT ? clock64() : 0;
                 resolveNext();
                 qBase = nBase;
                 qNext = nBase;
@@ -1023,8 +1132,11 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 cBat = nBat;
                 patBuf = patBufOf(cBat);
                 haveNext = false;
-                if (qNext >= qEnd) continue;
+                tried = false;
+                if (COUNT) cySwitch += clock64() - w0;
+                continue;
             }
+            const uint64_t h0 = COUNT ? clock64() : 0;
             const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
             const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
             const bool mine = ((pending >> lane) & 1ull) && rank < take;
@@ -1032,6 +1144,8 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const uint32_t srcLane = (qNext - qBase + rank) & 63u;
             const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
                                        __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
+            const uint64_t s0 = COUNT ? clock64() : 0;
+            if (COUNT) cyShfl += s0 - h0;
             if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
                 // ---- start a task (x = its text position): copy the pattern
                 // and the text window its subtree can reach
@@ -1052,13 +1166,14 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     wb &= ~31u;
                     copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBytes, patBlocks);
                 }
-                cur = make_uint2((x - wb) | ((x + t.y - wb) << 16), meta);
+                cur = make_uint2((x - wb) | ((x + (t.y & 0xFFFFu) - wb) << 16), meta);
                 have = true;
             }
             pending &= ~__ballot(mine);
             qNext += take;
+            if (COUNT) cyStart += clock64() - s0;
         }
-        if (refill) prefetch();
+        const uint64_t e0 = COUNT ? clock64() : 0;
         if (!dry) dry = qNext >= qEnd && !haveNext;
         // ---- retire the older batch once the wave holds nothing of it
         bool retired = false;
@@ -1067,7 +1182,9 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             const bool held = __any((have || sp > 0u) && lpar == p) || (cBat == lo && qNext < qEnd) ||
                               (haveNext && nBat == lo);
             if (!held) {
+                const uint64_t r0 = COUNT ? clock64() : 0;
                 retire(lo);
+                if (COUNT) cyRetire += clock64() - r0;
                 ++lo;
                 retired = true;
             }
@@ -1080,6 +1197,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         // pattern copied slot to slot in LDS, and the task state (pattern id,
         // window start, scheme row, batch parity) by shuffle. The DFS of the
         // entry is the same whichever lane runs it, so the hits are too.
+        const uint64_t st0 = COUNT ? clock64() : 0;
         if (a.stealAt && dry) {
             const bool thief = !have && sp == 0u;
             const uint64_t I = __ballot(thief);
@@ -1123,6 +1241,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 }
             }
         }
+        if (COUNT) { const uint64_t e1 = clock64(); cySteal += e1 - st0; cyTail += e1 - e0; }
         if (!__any(have || sp > 0)) {
             if (lo >= a.b1) break;  // every batch of the pass retired
             if (retired) continue;  // the queue may move on now
@@ -1132,13 +1251,26 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 waiting = true;
                 waitStart = wall_clock64();
             }
-            __builtin_amdgcn_s_sleep(20);  // ~0.5 us
-            if ((++idleSpins & 15u) == 0u) {
+            __builtin_amdgcn_s_sleep(60);  // ~1.6 us
+            if ((++idleSpins & 63u) == 0u) {
                 uint32_t abort = 0;
-                if (lane == 0) abort = pollWord(a.ctl);
-                if (__builtin_amdgcn_readfirstlane(abort) || wall_clock64() - waitStart > a.timeoutTicks) break;
+                if (threadIdx.x == 0) abortSeen = pollWord(a.ctl);
+                if (lane == 0) abort = abortSeen;
+                if (__builtin_amdgcn_readfirstlane(abort)) break;
+                if (wall_clock64() - waitStart > a.timeoutTicks) {
+                    // what the wave waited for (counters [26..29], read by the
+                    // host when the pass falls back: SAHARA_DEBUG_TEXT)
+                    if (lane == 0) {
+                        atomicAdd(a.counters + 26, 1ull);
+                        atomicMax(a.counters + 27, (unsigned long long)(qb * 2u + qph) << 32 | (qReady ? 1u : 0u));
+                        atomicMin(a.counters + 28, (unsigned long long)(qb * 2u + qph) << 32 | lo);
+                        atomicMax(a.counters + 29, (unsigned long long)pubVal[qb & 7u][qph] << 32 | pubTag[qb & 7u][qph]);
+                    }
+                    break;
+                }
             }
             pollSkip = 0;
+            if (COUNT) cyIdle += clock64() - t0;
             continue;
         }
         waiting = false;
@@ -1338,48 +1470,52 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             t0 = t1;
         }
         {
-            // leaves -> the hit buffer of their batch (one slot range per
-            // batch parity). The hit's row is ranked in its query's segment
-            // (qcnt); the atomic's result is stored at the lane's next
-            // emission, so its round trip overlaps the micro-steps between.
-            uint32_t* rk0 = slotOf(batchOf(0u)).rank;
-            uint32_t* rk1 = slotOf(batchOf(1u)).rank;
-            auto emit = [&](uint32_t p, uint32_t& hn, uint32_t& he) __attribute__((always_inline)) {
+            // leaves -> the hit buffer of their batch: a slot per leaf lane
+            // from the wave's range of its batch parity, one store site, and
+            // a count on the query (tcnt) by an atomic whose result is not
+            // used. No value returns into the wave: a returning atomic (the
+            // hit's rank, as the FM phase does it) left a register pending
+            // across the micro-steps, which the compiler then waited for in
+            // every one of them (4.5x the text time, r5); kLocate ranks text
+            // hits instead, at the tail of their query's segment
+            uint32_t s = ~0u;
+            auto take = [&](uint32_t p, uint32_t& hn, uint32_t& he, uint32_t* counter) __attribute__((always_inline)) {
                 const bool want = leaf && lpar == p;
                 const uint64_t wm = __ballot(want);
                 if (!wm) return;
-                const TextSlot& Sl = slotOf(batchOf(p));
-                // SlotRange::take on (hn, he)
                 const uint32_t cnt = (uint32_t)__popcll(wm), rank = (uint32_t)__popcll(wm & ltMask);
                 const uint32_t avail = he - hn;
                 uint32_t base = 0;
                 if (cnt > avail) {
                     if (lane == 0)
-                        base = __hip_atomic_fetch_add(GLOB(uint32_t, Sl.small + 1), kHitChunk, __ATOMIC_RELAXED,
+                        base = __hip_atomic_fetch_add(GLOB(uint32_t, counter), kHitChunk, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);
                     base = __builtin_amdgcn_readfirstlane(base);
                 }
-                const uint32_t s = rank < avail ? hn + rank : base + (rank - avail);
+                if (want) s = rank < avail ? hn + rank : base + (rank - avail);
                 if (cnt > avail) { hn = base + (cnt - avail); he = base + kHitChunk; }
                 else hn += cnt;
-                if (want) {
+            };
+            if (__any(leaf)) {
+                take(0u, hn0, he0, slotP0.small + 1);
+                take(1u, hn1, he1, slotP1.small + 1);
+                if (leaf) {
+                    const bool p1 = lpar != 0u;
                     if (s < a.hitCap) {
-                        *GLOB(uint4, Sl.hits + s) = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
-                        if (rankSlot != ~0u) *GLOB(uint32_t, (rankPar ? rk1 : rk0) + rankSlot) = rankVal;
-                        rankVal = __hip_atomic_fetch_add(GLOB(uint32_t, Sl.qcnt + pid), 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                        rankSlot = s;
-                        rankPar = p;
+                        storeThrough((p1 ? slotP1.hits : slotP0.hits) + s,
+                                     make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown));
+#ifndef SAHARA_V_NOTCNT
+                        (void)__hip_atomic_fetch_add(GLOB(uint32_t, (p1 ? slotP1.tcnt : slotP0.tcnt) + pid), 1u,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
                     } else {
-                        __hip_atomic_fetch_or(GLOB(uint32_t, Sl.small + 2), 2u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_fetch_or(GLOB(uint32_t, (p1 ? slotP1.small : slotP0.small) + 2), 2u,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    if (p) ++filled1;
+                    if (p1) ++filled1;
                     else ++filled0;
                 }
-            };
-            emit(0u, hn0, he0);
-            emit(1u, hn1, he1);
+            }
         }
         if (COUNT) cyEmit += clock64() - t0;
     }
@@ -1392,19 +1528,34 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             atomicAdd(a.counters + 11, (unsigned long long)cyRefill);
             atomicAdd(a.counters + 12, (unsigned long long)cyStep);
             atomicAdd(a.counters + 13, (unsigned long long)cyEmit);
+            atomicAdd(a.counters + 17, (unsigned long long)cyIdle);
+            atomicAdd(a.counters + 18, (unsigned long long)cyGrab);
+            atomicAdd(a.counters + 19, (unsigned long long)(clock64() - tBorn));
+            atomicAdd(a.counters + 20, (unsigned long long)cyStart);
+            atomicAdd(a.counters + 21, (unsigned long long)cySteal);
+            atomicAdd(a.counters + 22, (unsigned long long)cyRetire);
+            atomicAdd(a.counters + 23, (unsigned long long)cyResolve);
+            atomicAdd(a.counters + 24, (unsigned long long)cySwitch);
+            atomicAdd(a.counters + 25, (unsigned long long)nGrab);
+            atomicAdd(a.counters + 30, (unsigned long long)cyShfl);
+            atomicAdd(a.counters + 31, (unsigned long long)cyTail);
+            atomicAdd(a.counters + 32, (unsigned long long)cyTop);
         }
         atomicAdd(a.counters + 14, (unsigned long long)cCmp);
         atomicAdd(a.counters + 15, (unsigned long long)cSteps);
     }
 }
 
-// A producer stream's step of the text phase's hand-off: *flag = the task
-// count (capped) | kTaskReady, stored sc1 (relaxed, agent scope). The tasks
-// were written by the kernels before this one on its stream, whose end
-// released them; the text kernel polls the flag, then acquires.
-__global__ void kPublish(const uint32_t* count, uint32_t cap, uint32_t* flag) {
+// A producer stream's step of the text phase's hand-off: flag[16 w] = the
+// task count (capped) | kTaskReady for each of the text launch's nwg
+// workgroups w, stored sc1 (relaxed, agent scope). The tasks were written by
+// the kernels before this one on its stream, whose end released them; a text
+// workgroup polls its own copy, then acquires.
+__global__ void kPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, uint32_t nwg) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwg) return;
     const uint32_t v = min(*count, cap) | kTaskReady;
-    __hip_atomic_store((GlobalU32*)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((GlobalU32*)(flag + 16u * w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ================================================================ locate ====
@@ -1448,12 +1599,13 @@ __device__ __forceinline__ uint64_t blockExclusiveScan(uint64_t v, uint64_t& tot
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(256) void kTileSums(const uint32_t* __restrict__ cnt, uint32_t n,
+__global__ __launch_bounds__(256) void kTileSums(const uint32_t* __restrict__ cnt,
+                                                const uint32_t* __restrict__ tcnt, uint32_t n,
                                                 uint64_t* __restrict__ partial) {
     __shared__ uint64_t wsum[4];
     const uint32_t base = blockIdx.x * kScanTile;
     uint64_t acc = 0;
-    for (uint32_t i = threadIdx.x; i < kScanTile && base + i < n; i += 256) acc += cnt[base + i];
+    for (uint32_t i = threadIdx.x; i < kScanTile && base + i < n; i += 256) acc += cnt[base + i] + tcnt[base + i];
     for (uint32_t off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
     if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = acc;
     __syncthreads();
@@ -1473,7 +1625,8 @@ __global__ __launch_bounds__(256) void kScanPartials(uint64_t* __restrict__ part
     }
 }
 
-__global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, uint32_t n,
+__global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tcnt,
+                                                 uint32_t n,
                                                  const uint64_t* __restrict__ partial, uint64_t* __restrict__ off,
                                                  uint32_t* __restrict__ list, uint32_t* __restrict__ nlist,
                                                  uint32_t* __restrict__ huge, uint32_t* __restrict__ nhuge) {
@@ -1486,8 +1639,9 @@ __global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, ui
     uint64_t carry = partial[blockIdx.x];
     for (uint32_t c = 0; c < kScanTile; c += 256) {  // uniform trip count: block scans inside
         const uint32_t i = base + c + threadIdx.x;
-        const uint32_t v = i < n ? cnt[i] : 0u;
-        if (v) cnt[i] = 0u;  // zero again for the next batch
+        const uint32_t f = i < n ? cnt[i] : 0u;
+        if (f) cnt[i] = 0u;  // zero again for the next batch (tcnt: kLocate counts it down)
+        const uint32_t v = f + (i < n ? tcnt[i] : 0u);
         uint64_t tot;
         const uint64_t ex = blockExclusiveScan(v, tot, wsum);
         if (i < n) off[i] = carry + ex;
@@ -1518,12 +1672,16 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
          h += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 hit = a.hits[h];
         if (hit.z == 0) continue;  // reserved hole
-        const uint64_t out = a.qoff[hit.x] + a.rank[h];
         const uint64_t e = hit.w & 0xFu;
-        if (hit.w & kPosKnown) {  // resolved by the text phase
-            a.keys[out] = ((uint64_t)hit.y << 4) | e;
+        if (hit.w & kPosKnown) {  // resolved by the text phase: the segment's tail, counted down
+#ifdef SAHARA_V_NOTCNT
+            continue;  // (timing variant: text hits not counted, not located)
+#endif
+            const uint32_t left = atomicSub(a.tcnt + hit.x, 1u);
+            a.keys[a.qoff[hit.x + 1] - left] = ((uint64_t)hit.y << 4) | e;
             continue;
         }
+        const uint64_t out = a.qoff[hit.x] + a.rank[h];
         if (a.useSA) {  // full SA resident: one read per row
             for (uint32_t j = 0; j < hit.z; ++j) a.keys[out + j] = ((uint64_t)a.sa[hit.y + j] << 4) | e;
             continue;
@@ -1980,8 +2138,8 @@ void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32
     SH_HIP(hipGetLastError());
 }
 
-void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, hipStream_t st) {
-    hipLaunchKernelGGL(kPublish, dim3(1), dim3(64), 0, st, count, cap, flag);
+void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, uint32_t nwg, hipStream_t st) {
+    hipLaunchKernelGGL(kPublish, dim3((nwg + 255) / 256), dim3(256), 0, st, count, cap, flag, nwg);
     SH_HIP(hipGetLastError());
 }
 
@@ -2308,13 +2466,14 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
     SH_HIP(hipGetLastError());
 }
 
-void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
-                   uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
-    // qcnt[nq] stays 0, so qoff[nq] = total rows
+void querySegments(uint32_t* qcnt, const uint32_t* tcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
+                   uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
+    // qcnt[nq] and tcnt[nq] stay 0, so qoff[nq] = total rows
     const uint32_t n = nq + 1, tiles = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, n, partial);
+    hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, tcnt, n, partial);
     hipLaunchKernelGGL(kScanPartials, dim3(1), dim3(256), 0, st, partial, tiles);
-    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, n, partial, qoff, big, nbig, huge, nhuge);
+    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, tcnt, n, partial, qoff, big, nbig, huge,
+                       nhuge);
     SH_HIP(hipGetLastError());
 }
 
