@@ -221,19 +221,24 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // the text phase addresses text and a batch's patterns with 32-bit buffer offsets
     const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
+    const int textShape = textShapeOf(winBlocks, c->patBlocks, exactWindow);
+    const char* olEnv = std::getenv("SAHARA_TEXT_ONE_LAUNCH");
+    const bool wantOneLaunch = !serial && olEnv && std::atoi(olEnv) == 1;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
-        tbpc = textBlocksPerCU(sigma, c->edit, textLds);
+        tbpc = textBlocksPerCU(sigma, c->edit, count, textShape, textLds, wantOneLaunch);
     // overlapped with the FM phase, three text workgroups per CU beside its one
     // (four would fit: r2 v8 measured text 4 against 3 in alternating pairs,
     // C3 914-943M vs 880-952M on one box and 873-914M vs 953-956M on another,
     // C2 950-1013M vs 956-1026M: the sign flips with the box)
     if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
-    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, textLds), std::atoi(e)));
-    // (pipelined) the text launch waits for the seed and FM kernels, which
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, count, textShape, textLds, wantOneLaunch), std::atoi(e)));
+    // (one launch) the text launch waits for the seed and FM kernels, which
     // must fit beside its workgroups (count mode's kernels hold more VGPRs)
-    if (!serial && tbpc > 0)
-        tbpc = textBlocksBeside(sigma, c->edit, count, textShapeOf(winBlocks, c->patBlocks, exactWindow), textLds, lds,
-                                tbpc);
+    if (wantOneLaunch && tbpc > 0)
+        tbpc = textBlocksBeside(sigma, c->edit, count, textShape, textLds, lds, tbpc);
+    if (std::getenv("SAHARA_DUMP_COUNTERS"))
+        std::fprintf(stderr, "text geometry: shape %d lds %zu blocks/CU %d (alone %d) serial %d\n", textShape, textLds, tbpc,
+                     textBlocksPerCU(sigma, c->edit, count, textShape, textLds, wantOneLaunch), (int)serial);
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     // (pipelined) the first batch's text phase starts on its seed tasks while
     // its FM phase runs; a device-resident lone batch does not: its FM phase
@@ -250,15 +255,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool chunkSeeds = c->streaming && !serial && split && !(csEnv && std::atoi(csEnv) == 0);
     const bool early = !serial && split && (batchesHere > 1 || chunkSeeds);
     const bool chunked0 = early && chunkSeeds;
-    // (pipelined) the text phase of the whole pass is one launch that takes
-    // each batch's tasks as the seed and FM streams publish them (search.hip
-    // kSearchText), so no launch boundary falls between batches: C3's call had
-    // 11% of its time between the per-batch text launches, waiting for CU slots
-    // (profiles/r04_head_c3_timeline_split.txt). SAHARA_TEXT_ONE_LAUNCH=0: one
-    // launch per batch (the same kernel over [b, b + 1)).
-    const char* olEnv = std::getenv("SAHARA_TEXT_ONE_LAUNCH");
-    const bool persist = split && !serial;
-    const bool oneLaunch = persist && !(olEnv && std::atoi(olEnv) == 0);
+    // (pipelined, SAHARA_TEXT_ONE_LAUNCH=1) the text phase of the whole pass
+    // as one launch that takes each batch's tasks as the seed and FM streams
+    // publish them (search.hip kSearchText), so no launch boundary falls
+    // between batches. Measured slower than one launch per batch
+    // (kSearchTextBatch, the default): DESIGN.md §9.
+    const bool oneLaunch = split && wantOneLaunch;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
@@ -334,23 +336,30 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     SH_HIP(hipStreamSynchronize(c->stC));
     SH_HIP(hipStreamSynchronize(c->stD));
     c->mark("pass synced", 0);
-    if (count) SH_HIP(hipMemsetAsync(c->counters.ptr, 0, kCounters * sizeof(unsigned long long), sA));
-    // the text launch's timeout report (search.hip kSearchText): count, max, min, max
-    SH_HIP(hipMemsetAsync(c->counters.ptr + 26, 0, 2 * sizeof(unsigned long long), sA));
-    SH_HIP(hipMemsetAsync(c->counters.ptr + 28, 0xFF, sizeof(unsigned long long), sA));
-    SH_HIP(hipMemsetAsync(c->counters.ptr + 29, 0, sizeof(unsigned long long), sA));
+    const bool probe = std::getenv("SAHARA_DUMP_COUNTERS") != nullptr;  // (profiling hook)
+    if (count || probe) {
+        SH_HIP(hipMemsetAsync(c->counters.ptr, 0, kCounters * sizeof(unsigned long long), sA));
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 33, 0xFF, sizeof(unsigned long long), sA));  // (minima)
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 37, 0xFF, sizeof(unsigned long long), sA));
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 38, 0xFF, sizeof(unsigned long long), sA));
+    }
+    if (oneLaunch) {  // the text launch's timeout report (search.hip kSearchText): count, max, min, max
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 26, 0, 2 * sizeof(unsigned long long), sA));
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 28, 0xFF, sizeof(unsigned long long), sA));
+        SH_HIP(hipMemsetAsync(c->counters.ptr + 29, 0, sizeof(unsigned long long), sA));
+    }
     c->nout = 0;
     c->sinkDone = 0;
     c->sinkOk = c->sink != nullptr || c->blockRecs != nullptr;
     c->batchQ0.clear();
     c->batchEnd.clear();
-    // The text phase's hand-off state: per batch 4 words (zero), the batch
-    // table, the host's done words; every slot's buffers are sized before the
-    // launch, so their addresses hold for the pass (the slot table).
+    // The one text launch's hand-off state: per batch 4 words (zero), the
+    // batch table, the host's done words; every slot's buffers are sized
+    // before the launch, so their addresses hold for the pass (the slot table).
     const size_t usedSlots = (size_t)std::min<uint64_t>(nbatch, Ctx::kSlots);
     uint64_t maxItems = 0;
     for (uint64_t b = 0; b < nbatch; ++b) maxItems = std::max(maxItems, (bstart[b + 1] - bstart[b]) * c->nsearch);
-    for (size_t i = 0; i < usedSlots; ++i) {
+    for (size_t i = 0; i < (oneLaunch ? usedSlots : 0); ++i) {
         Ctx::Slot& sl = c->slot[i];
         sl.hits.reserve((size_t)c->hitCap + 1);
         sl.rank.reserve((size_t)c->hitCap + 1);
@@ -366,7 +375,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         }
         SH_HIP(hipMemcpyAsync(c->slotTab.ptr, c->slotHost, Ctx::kSlots * sizeof(TextSlot), hipMemcpyHostToDevice, s));
     };
-    if (split) {
+    if (oneLaunch) {
         if (c->batchHostCap < nbatch + 1) {
             if (c->batchHost) SH_HIP(hipHostFree(c->batchHost));
             c->batchHost = nullptr;
@@ -406,6 +415,16 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     };
     for (auto& sl : c->slot) resetSlot(sl, sA);
 
+    // the batch's seed tasks are all written (stream sD): the one-launch text
+    // phase may start on them (published), the first batch's per-batch text
+    // phase launches on them (the count snapshot in small[5]) before its FM
+    // phase ends
+    auto seedTasksDone = [&](uint64_t b, Ctx::Slot& sl) {
+        if (oneLaunch)
+            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sD);
+        else
+            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+    };
     auto issueFM = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
@@ -413,9 +432,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         sl.rank.reserve((size_t)c->hitCap + 1);
         sl.tasks.reserve((size_t)c->taskCap);
         SH_HIP(hipStreamWaitEvent(sA, sl.free, 0));  // the slot's previous batch is fully consumed
-        if (serial && split)  // a re-run of the batch publishes its tasks again
-            SH_HIP(hipMemsetAsync(c->bflags.ptr + textFlag(b, 0, textBlocks), 0,
-                                  textFlagWords(textBlocks) * sizeof(uint32_t), sA));
         SearchArgs a{};
         a.occF = c->I.occF.ptr;
         a.occR = c->I.occR.ptr;
@@ -498,7 +514,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             ensureUploaded(c, p1, sD);
             SH_HIP(hipEventRecord(sl.fmStart, sD));
             seeds(0, (uint32_t)(p1 * c->nsearch));
-            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sD);
+            seedTasksDone(b, sl);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
             ensureUploaded(c, bstart[b + 1], sD);
             SH_HIP(hipEventRecord(sl.seedMid, sD));  // the second part's seeds start (after the upload's wait)
@@ -512,16 +528,15 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // the seed tasks end here: the text phase may start on them (a
             // lone device-resident batch's text phase waits for its FM phase:
             // published after it below)
-            if (split && (early || serial))
-                launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sD);
+            if (split && early) seedTasksDone(b, sl);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
         }
         SH_HIP(hipEventRecord(sl.seedDone, sD));
         SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
         SH_HIP(hipEventRecord(sl.fmBegin, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
-        if (split) {  // the batch's task list is final
-            if (!early && !serial)
+        if (split && oneLaunch) {  // the batch's task list is final
+            if (!early)
                 launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sA);
             launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 1, textBlocks), textBlocks, sA);
         }
@@ -539,6 +554,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // the kernel's wall clock (s_memrealtime) counts at 100 MHz on gfx950
     // (MI355X_MICROARCH.md); the device attribute reported another rate
     constexpr uint64_t wallKHz = 100000;
+    // in-wave work stealing while no task is in hand, once SAHARA_STEAL_AT
+    // lanes of a wave are idle (0: off). Measured in one process, alternating:
+    // C5 80.4M (off) -> 124.3M (1) / 129.5M (8) reads/s, lanes busy 0.656 ->
+    // 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
+    uint32_t stealAt = 8;
+    if (const char* e = std::getenv("SAHARA_STEAL_AT")) stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
     auto launchTextRange = [&](uint64_t b0, uint64_t b1) {
         TextArgs t{};
         t.sa = c->I.saFull.ptr;
@@ -561,6 +582,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // then redoes the pass batch by batch): no legitimate wait is that long
         t.timeoutTicks = wallKHz * 2000;
         t.pollGap = std::max<uint64_t>(1, wallKHz * 2 / 1000);  // 2 us
+        t.probe = probe ? 1u : 0u;
         t.taskCap = c->taskCap;
         t.hitCap = c->hitCap;
         t.counters = c->counters.ptr;
@@ -570,12 +592,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         t.tableWords = tableWords;
         t.steps = c->textSteps;
         t.refillAt = c->refillAt;
-        // in-wave work stealing while no task is in hand, once SAHARA_STEAL_AT
-        // lanes of a wave are idle (0: off). Measured in one process,
-        // alternating: C5 80.4M (off) -> 124.3M (1) / 129.5M (8) reads/s,
-        // lanes busy 0.656 -> 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
-        t.stealAt = 8;
-        if (const char* e = std::getenv("SAHARA_STEAL_AT")) t.stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
+        t.stealAt = stealAt;
         launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
     };
     auto issueText = [&](uint64_t b) {
@@ -590,14 +607,53 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             ++S.text_launches;
             return;
         }
-        SH_HIP(hipStreamWaitEvent(sB, early && b == 0 ? sl.seedDone0 : sl.fmDone, 0));
-        if (serial && split) {  // a re-run may have grown the slot's buffers
-            SH_HIP(hipStreamSynchronize(sB));
-            writeSlotTable(sB);
-        }
+        // one launch per batch (kSearchTextBatch) after its FM phase; the
+        // first batch of an early pass in two: its seed tasks while its FM
+        // phase runs, then the tasks the FM phase appended after them
+        const bool split0 = early && b == 0;
+        SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone0 : sl.fmDone, 0));
         SH_HIP(hipEventRecord(sl.textStart, sB));
         if (split) {
-            launchTextRange(b, b + 1);
+            const uint64_t q0 = bstart[b];
+            TextBatchArgs t{};
+            t.sa = c->I.saFull.ptr;
+            t.text3 = c->I.text3.ptr;
+            t.pats3 = c->pats3.ptr + q0 * c->patBlocks;
+            t.patBlocks = c->patBlocks;
+            t.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
+            t.pats3Bytes = (uint32_t)std::min<uint64_t>((bstart[b + 1] - q0) * c->patBlocks * 16, 0xFFFFFF00ull);
+            t.m = c->m;
+            t.nsearch = c->nsearch;
+            t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
+            t.tasks = sl.tasks.ptr;
+            t.taskCount = sl.small.ptr + 4;
+            t.taskCap = c->taskCap;
+            t.work = sl.queues.ptr + 256;
+            t.hits = sl.hits.ptr;
+            t.hitCap = c->hitCap;
+            t.hitCount = sl.small.ptr + 1;
+            t.filled = sl.small.ptr + 3;
+            t.flags = sl.small.ptr + 2;
+            t.counters = c->counters.ptr;
+            t.winBlocks = winBlocks;
+            t.exactWindow = exactWindow ? 1u : 0u;
+            t.stackCap = textStack;
+            t.tableWords = tableWords;
+            t.steps = c->textSteps;
+            t.refillAt = c->refillAt;
+            t.stealAt = stealAt;
+            t.qcnt = sl.qcnt.ptr;
+            t.rank = sl.rank.ptr;
+            if (split0) {
+                t.taskCount = sl.small.ptr + 5;
+                launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);
+                SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+                t.taskBegin = sl.small.ptr + 5;
+                t.taskCount = sl.small.ptr + 4;
+                t.work = sl.queues.ptr + 512;
+                ++S.text_launches;
+            }
+            launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);
             ++S.text_launches;
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));
@@ -719,7 +775,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         la.nhits = nh;
         la.qoff = c->qoff.ptr;
         la.rank = sl.rank.ptr;
-        la.tcnt = tcntOf(sl);
+        la.tcnt = oneLaunch ? tcntOf(sl) : nullptr;  // (one launch: text hits counted, not ranked)
         la.occF = c->I.occF.ptr;
         for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
         la.samples = c->I.samples.ptr;
@@ -929,6 +985,20 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         }
         overflow = false;
         SH_HIP(hipStreamSynchronize(c->stF));
+    }
+    if (probe && !count) {
+        unsigned long long h[kCounters];
+        SH_HIP(hipMemcpy(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "text wave lives (first launch, us): last start %.1f first end %.1f last end %.1f mean %.1f; "
+                     "tasks all taken seen first %.1f last %.1f by %llu waves, which ran on %.1f on average\n",
+                     (h[34] - h[33]) / 100.0, (h[37] - h[33]) / 100.0, (h[35] - h[33]) / 100.0,
+                     h[36] / 100.0 / std::max<double>(1, S.text_grid * 4.0), (h[38] - h[33]) / 100.0,
+                     (h[39] - h[33]) / 100.0, h[31], h[30] / 100.0 / std::max<double>(1, (double)h[31]));
+        std::fprintf(stderr, "text iterations before / after: %llu (busy lanes %.1f) / %llu (busy lanes %.1f); sleeps %llu steals %llu\n", h[40],
+                     h[41] / std::max(1.0, (double)h[40]), h[42], h[43] / std::max(1.0, (double)h[42]), h[44], h[45]);
+        std::fprintf(stderr, "text wall per iteration (us) before: refill %.2f steps+emit %.2f; after: refill %.2f steps+emit %.2f\n",
+                     h[46] / 100.0 / std::max(1.0, (double)h[40]), h[47] / 100.0 / std::max(1.0, (double)h[40]),
+                     h[48] / 100.0 / std::max(1.0, (double)h[42]), h[49] / 100.0 / std::max(1.0, (double)h[42]));
     }
     if (count) {
         unsigned long long h[kCounters];

@@ -96,12 +96,47 @@ struct TextBatch {
 // work counters of count mode (sahara_stats): [0..15] as SearchArgs::counters
 // lists them, [16] text tasks that came with their text position (kTaskPos),
 // [17..19] text-kernel cycles idle / in grab / whole wave lives
-constexpr uint32_t kCounters = 40;
+constexpr uint32_t kCounters = 56;
 // a published task count (kPublish): bit 31 set once the count is final for its phase
 constexpr uint32_t kTaskReady = 0x80000000u;
 // a task record whose x is already a text position (a k-mer seed with one
 // occurrence: DeviceIndex::kmerPos), not an SA row: bit 31 of its y (|t|)
 constexpr uint32_t kTaskPos = 0x80000000u;
+
+// One launch of the text phase over one batch's tasks [*taskBegin, *taskCount)
+// (kSearchTextBatch)
+struct TextBatchArgs {
+    const uint32_t* sa;      // full SA: task records carry SA rows (unless kTaskPos), the kernel reads their positions
+    const uint4* text3;      // text as 3-bit-plane blocks of 32 symbols (device_index.h)
+    const uint4* pats3;      // the batch's patterns as 3-bit-plane blocks, patBlocks per pattern
+    uint32_t patBlocks;
+    uint32_t text3Bytes;     // bytes of text3 / of the batch's pats3 (buffer-load bounds; < 4 GiB)
+    uint32_t pats3Bytes;
+    uint32_t m;
+    uint32_t nsearch;
+    const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
+    const uint4* tasks;
+    const uint32_t* taskCount;  // tasks written by the seed / FM kernels (device-side: no host round trip)
+    const uint32_t* taskBegin;  // first task of this launch (device-side; nullptr: 0)
+    uint32_t taskCap;
+    uint32_t* work;          // the launch's striped queue counters (zero)
+    uint4* hits;
+    uint32_t hitCap;
+    uint32_t* hitCount;
+    uint32_t* filled;
+    uint32_t* flags;
+    unsigned long long* counters;
+    uint32_t winBlocks;      // window blocks per lane (32 symbols each)
+    uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
+    uint32_t stackCap;       // text DFS stack entries per lane
+    uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)
+    uint32_t steps;          // node expansions per lane between wave-level bookkeeping
+    uint32_t refillAt;       // refill idle lanes once this many are idle
+    uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
+                             // lane of their wave (with its window and pattern) once this many are idle (0: off)
+    uint32_t* qcnt;          // as SearchArgs: rows ranked where the hits are written (the FM phase's counts)
+    uint32_t* rank;
+};
 
 struct TextArgs {
     const uint32_t* sa;      // full SA: task records carry SA rows, the kernel reads their text positions
@@ -125,6 +160,7 @@ struct TextArgs {
     const uint32_t* ctl;     // [0] != 0: the host aborts the pass
     uint64_t timeoutTicks;   // an idle wave gives up after waiting this long (wall clock ticks)
     uint64_t pollGap;        // a workgroup polls an unpublished task count at most once per this many ticks
+    uint32_t probe;          // (profiling) the first launch's wave lives on the wall clock into counters [33..37]
     uint32_t taskCap;
     uint32_t hitCap;
     unsigned long long* counters;
@@ -143,7 +179,8 @@ struct LocateArgs {
     uint64_t nhits;
     const uint64_t* qoff;          // per-query row segments (querySegments)
     const uint32_t* rank;          // per cursor: slot of its first row in the segment (querySegments)
-    uint32_t* tcnt;                // per query: its text hits still to place (the segment's tail); zero on return
+    uint32_t* tcnt;                // (one text launch) per query: its text hits still to place (the segment's
+                                   // tail), zero on return; nullptr: text hits ranked like FM cursors (rank)
     const OccLine* occF;
     uint32_t C[8];
     const uint32_t* samples;
@@ -156,11 +193,14 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
+int textBlocksPerCU(uint32_t sigma, bool edit, bool count, int shape, size_t lds, bool persistent);
 // text workgroups per CU (<= want) that leave room for an FM workgroup and a
 // locate-chain workgroup beside them (shape: the compile-time text shape, 0-2)
 int textBlocksBeside(uint32_t sigma, bool edit, bool count, int shape, size_t textLds, size_t fmLds, int want);
 int textShapeOf(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow);
+// the text phase of one batch (kSearchTextBatch): the product path
+void launchTextBatch(const TextBatchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
+                     hipStream_t st);
 void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                 hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);

@@ -57,6 +57,39 @@ namespace sahara {
 namespace {
 
 // Swap a dword with the neighbour lane of the pair (DPP quad_perm [1,0,3,2]).
+typedef __attribute__((address_space(1))) uint32_t GlobalU32;
+// Pointers that come from memory (the slot table), from integers (Occ line
+// addresses) or that may point to LDS or global memory (a stack level) are
+// generic: accesses through them are flat instructions, which also count
+// against the LDS counter and make every LDS wait wait for them (and a flat
+// access of LDS is slower than a ds_ one). Where they address global memory,
+// say so. (The host pass of this file parses kernel bodies too, where class
+// types in an address space do not convert: there the cast is a plain one.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GLOB(T, p) ((__attribute__((address_space(1))) T*)(p))
+#else
+#define GLOB(T, p) ((T*)(p))
+#endif
+// A 16-B record through a global pointer: uint4 is a class type whose copy
+// goes through a generic reference (a flat access again), a native vector is not
+typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 loadGlobal4(const uint4* p) {
+    const U32x4 v = *GLOB(const U32x4, p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// a wave-uniform 64-bit value made scalar (readfirstlane returns an int: its
+// low half must not be sign-extended into the high one)
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void storeGlobal4(uint4* p, const uint4& v) {
+    U32x4 w;
+    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+    *GLOB(U32x4, p) = w;
+}
+
 __device__ __forceinline__ uint32_t pairSwap(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
 }
@@ -82,12 +115,21 @@ __device__ __forceinline__ void fetchLinePair(uint64_t own, bool need, bool odd,
     const uint32_t half = odd ? 16u : 0u;
     uint4 r1 = make_uint4(0, 0, 0, 0), r2 = r1, r3 = r1, r4 = r1;
     if (needE) {
+#ifdef SAHARA_X_OCC_FLAT
         r1 = *reinterpret_cast<const uint4*>(addrE + half);
         r2 = *reinterpret_cast<const uint4*>(addrE + 32 + half);
     }
     if (needO) {
         r3 = *reinterpret_cast<const uint4*>(addrO + half);
         r4 = *reinterpret_cast<const uint4*>(addrO + 32 + half);
+#else
+        r1 = loadGlobal4(reinterpret_cast<const uint4*>(addrE + half));
+        r2 = loadGlobal4(reinterpret_cast<const uint4*>(addrE + 32 + half));
+    }
+    if (needO) {
+        r3 = loadGlobal4(reinterpret_cast<const uint4*>(addrO + half));
+        r4 = loadGlobal4(reinterpret_cast<const uint4*>(addrO + 32 + half));
+#endif
     }
     // even: r1 = E0, r2 = E2, r3 = O0, r4 = O2 ; odd: r1 = E1, r2 = E3, r3 = O1, r4 = O3
     const uint4 g1 = pairSwap4(odd ? r1 : r3);  // even <- E1, odd <- O0
@@ -388,12 +430,22 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     const uint32_t L = a.stackLevels;
     auto stackGet = [&](uint32_t d) -> uint4 {
         d = d >= L ? d - L : d;
+#ifdef SAHARA_X_FMSTACK_GLOBAL
+        if (d < ldsDepth) return lstk[d * 256u + threadIdx.x];
+        return loadGlobal4(stk + (size_t)(d - ldsDepth) * T);
+#else
         return d < ldsDepth ? lstk[d * 256u + threadIdx.x] : stk[(size_t)(d - ldsDepth) * T];
+#endif
     };
     auto stackPut = [&](uint32_t d, const uint4& v) {
         d = d >= L ? d - L : d;
+#ifdef SAHARA_X_FMSTACK_GLOBAL
+        if (d < ldsDepth) lstk[d * 256u + threadIdx.x] = v;
+        else storeGlobal4(stk + (size_t)(d - ldsDepth) * T, v);
+#else
         if (d < ldsDepth) lstk[d * 256u + threadIdx.x] = v;
         else stk[(size_t)(d - ldsDepth) * T] = v;
+#endif
     };
     // seeds (kSeedItems: starting cursor + item) arrive in chunks of 64, one
     // record per lane, prefetched a chunk ahead so a refill costs no memory trip
@@ -493,8 +545,8 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
                 if (takes) {
                     const uint32_t dt = (threadIdx.x & ~63u) | donor;
                     const uint32_t lv = dBot;  // < L
-                    cur = lv < ldsDepth ? lstk[lv * 256u + dt]
-                                        : a.stack[(size_t)(lv - ldsDepth) * T + (gtid & ~63u) + donor];
+                    if (lv < ldsDepth) cur = lstk[lv * 256u + dt];
+                    else cur = loadGlobal4(a.stack + (size_t)(lv - ldsDepth) * T + (gtid & ~63u) + donor);
                     pid = dPid;
                     sIdx = dS;
                     have = true;
@@ -784,6 +836,450 @@ struct TextShape { uint32_t win, pat; bool exact; };
 __host__ __device__ constexpr TextShape textShape(int shape) {
     return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
+
+typedef __attribute__((address_space(1))) uint64_t GlobalU64;
+#ifdef SAHARA_V_PLAIN
+__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) { *GLOB(uint32_t, p) = v; }
+__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) { *GLOB(uint4, p) = v; }
+#else
+__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((GlobalU32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) {
+    GlobalU64* q = (GlobalU64*)p;
+    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+
+// ---- kSearchTextBatch: the text phase of one batch per launch (the product
+// path). Its tasks [*taskBegin, *taskCount) of the slot's list come from a
+// striped queue; a lane takes a task (text position, or SA row read here),
+// copies the window and pattern to LDS and runs the subtree's DFS against the
+// text; leaves are hits (qid, text position, e | kPosKnown) counted per query
+// in tcnt (kLocate places them). The persistent kSearchText below serves all
+// batches of a pass from one launch (SAHARA_TEXT_ONE_LAUNCH=1): measured
+// slower, kept as an option.
+template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
+__global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
+    extern __shared__ uint32_t lds[];
+    uint2* SC = reinterpret_cast<uint2*>(lds);
+    uint32_t* slot = lds + a.tableWords;  // >= kTextTableMin: the window's block -1 stays in LDS
+    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = a.table[i];
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t ltMask = (1ull << lane) - 1ull;
+    constexpr TextShape kShape = textShape(SHAPE);
+    const uint32_t winBlocks = SHAPE ? kShape.win : a.winBlocks, patBlocks = SHAPE ? kShape.pat : a.patBlocks;
+    const bool exactWindow = SHAPE ? kShape.exact : a.exactWindow != 0u;
+    uint32_t* W = slot + threadIdx.x;
+    uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
+    uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
+    auto stackGet = [&](uint32_t d) -> uint2 { return S[d * 256u]; };
+    auto stackPut = [&](uint32_t d, const uint2& v) { S[d * 256u] = v; };
+    const uint32_t winLen = winBlocks * 32u;
+    const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
+    const __amdgpu_buffer_rsrc_t patBuf = bufferOf(a.pats3, a.pats3Bytes);
+    const uint32_t m = a.m;
+    // this launch's tasks: [tBase, taskCount) of the batch's list
+    const uint32_t tEnd = min(*a.taskCount, a.taskCap);
+    const uint32_t tBase = a.taskBegin ? min(*a.taskBegin, tEnd) : 0u;
+    const uint32_t ntasks = tEnd - tBase;
+    const uint4* tasks = a.tasks + tBase;
+
+    uint32_t sp = 0, pid = 0, wb = 0, sBase = 0;
+    bool have = false, exhausted = false, bad = false;
+    uint32_t qNext = 0, qEnd = 0, filled = 0;
+    bool qDone = false;
+    // task chunks: the current one's records (one per lane) and the next one's,
+    // prefetched a chunk ahead so a refill needs no dependent task read
+    uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
+    uint32_t nBase = 0, nEnd = 0, qBase = 0;
+    bool haveNext = false;
+    // The prefetched chunk's records still hold SA rows. Their text positions
+    // are read at the next refill, beside its window loads (one round trip for
+    // both), or at the latest when the chunk becomes current.
+    bool nextRaw = false;
+    auto resolveNext = [&]() {
+        if (nextRaw) {  // wave-uniform
+            if (nBase + lane < nEnd && !(nextRec.y & kTaskPos)) nextRec.x = a.sa[nextRec.x];
+            nextRaw = false;
+        }
+    };
+    StripedQueue queue(a.work, ntasks);
+    {
+        uint32_t b = 0, e = 0;
+        if (queue.next(lane, kTaskChunk, b, e)) {
+            nBase = b;
+            nEnd = e;
+            if (b + lane < e) nextRec = tasks[b + lane];
+            haveNext = true;
+            nextRaw = true;
+        } else {
+            qDone = true;
+        }
+    }
+    SlotRange hitSlots;
+    uint32_t rankSlot = ~0u, rankVal = 0;  // the lane's last hit whose rank is not stored yet
+    uint2 cur = make_uint2(0, 0);
+    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
+    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
+
+    for (;;) {
+        // Starting a task costs a global round trip (window + pattern) that
+        // stalls the whole wave, so idle lanes are refilled in batches: once
+        // refillAt lanes are idle (or nothing else is left).
+        if (COUNT) t0 = clock64();
+        const bool idle = !have && sp == 0 && !exhausted;
+        const uint64_t idleMask = __ballot(idle);
+        const bool busy = __any(have || sp > 0);
+        const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
+        const bool need = refill && idle;
+        uint64_t pending = refill ? idleMask : 0ull;
+        if (pending) resolveNext();
+        while (pending) {  // wave-uniform
+            if (qNext >= qEnd) {
+                // switch to the prefetched chunk, prefetch the one after it
+                if (!haveNext) break;
+                resolveNext();
+                qBase = nBase;
+                qNext = nBase;
+                qEnd = nEnd;
+                curRec = nextRec;
+                haveNext = false;
+                if (!qDone) {
+                    uint32_t b = 0, e = 0;
+                    if (!queue.next(lane, kTaskChunk, b, e)) {
+                        qDone = true;
+                    } else {
+                        nBase = b;
+                        nEnd = e;
+                        if (b + lane < e) nextRec = tasks[b + lane];
+                        haveNext = true;
+                        nextRaw = true;
+                    }
+                }
+                if (qNext >= qEnd) continue;
+            }
+            const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
+            const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
+            const bool mine = ((pending >> lane) & 1ull) && rank < take;
+            // the chunk's task records sit one per lane: fetch ours by shuffle
+            const uint32_t srcLane = (qNext - qBase + rank) & 63u;
+            const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
+                                       __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
+            if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
+                // ---- start a task (x = its text position): copy the pattern
+                // and the text window its subtree can reach
+                const uint32_t x = t.x;
+                pid = t.z;
+                sBase = (t.w >> 24) * m;
+                const uint32_t meta = t.w & 0x00FFFFFFu;
+                const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
+                const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
+                const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
+                const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
+                wb = x > left ? x - left : 0u;  // window start
+                if (exactWindow) {              // at wb: m + 2k symbols fit in winBlocks blocks
+                    copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
+                                      pid * patBlocks * 16u, patBlocks);
+                } else {                        // at the block start below wb (31 more symbols)
+                    wb &= ~31u;
+                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBlocks * 16u, patBlocks);
+                }
+                cur = make_uint2((x - wb) | ((x + (t.y & 0xFFFFu) - wb) << 16), meta);
+                have = true;
+            }
+            pending &= ~__ballot(mine);
+            qNext += take;
+        }
+        if (qDone && !haveNext && qNext >= qEnd && need && !have) exhausted = true;
+        // ---- work stealing inside the wave once the task queue is dry (wave-
+        // uniform: the queue state is the wave's). A launch ends on its longest
+        // subtrees, each on one lane while the others idle (C5: lanes busy
+        // 0.655 of the time); an idle lane takes the bottom (shallowest, so
+        // largest) stack entry of a busy lane, with that lane's window and
+        // pattern copied slot to slot in LDS, and the task state (pattern id,
+        // window start, scheme row) by shuffle. The DFS of the entry is the
+        // same whichever lane runs it, so the hits are too.
+        if (a.stealAt && qDone && !haveNext && qNext >= qEnd) {
+            const bool thief = !have && sp == 0u;
+            const uint64_t I = __ballot(thief);
+            const uint64_t D = __ballot(sp >= 2u || (sp == 1u && have));
+            const uint32_t nI = (uint32_t)__popcll(I), nD = (uint32_t)__popcll(D);
+            if (nI >= a.stealAt && nD) {  // wave-uniform
+                const uint32_t n = min(nI, nD);
+                const uint32_t r = (uint32_t)__popcll(I & ltMask);
+                // donor of thief rank r: the r-th set bit of D
+                uint32_t donor = 0, rr = r;
+                uint64_t dm = D;
+#pragma unroll
+                for (uint32_t w = 32; w; w >>= 1) {
+                    const uint32_t c = (uint32_t)__popcll(dm & ((1ull << w) - 1ull));
+                    if (rr >= c) { rr -= c; dm >>= w; donor += w; }
+                }
+                const bool takes = thief && r < n;
+                donor = takes ? donor : lane;
+                const uint32_t dPid = __shfl(pid, donor), dWb = __shfl(wb, donor), dBase = __shfl(sBase, donor);
+                const uint32_t dTid = (threadIdx.x & ~63u) | donor;
+                if (takes) {
+                    const uint32_t* src = slot + dTid;
+                    uint32_t* dst = slot + threadIdx.x;
+                    for (uint32_t k = 0; k < 3u * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
+                    const uint2 node = reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
+                    cur = node;
+                    pid = dPid;
+                    wb = dWb;
+                    sBase = dBase;
+                    have = true;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                // donors (rank < n) drop their bottom entry
+                const bool gives = ((D >> lane) & 1ull) && (uint32_t)__popcll(D & ltMask) < n;
+                if (gives) {
+                    for (uint32_t d = 1; d < sp; ++d) stackPut(d - 1u, stackGet(d));
+                    --sp;
+                }
+            }
+        }
+        if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
+        if (COUNT) {
+            const uint64_t act = __ballot(have || sp > 0);
+            if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
+            const uint64_t t1 = clock64();
+            cyRefill += t1 - t0;
+            t0 = t1;
+        }
+
+        // ---- up to a.steps micro-steps per lane; a lane that reaches a leaf
+        // holds it (stalls) until the emission below
+        bool leaf = false;
+        uint32_t leafStart = 0, leafE = 0;
+        for (uint32_t step = 0; step < a.steps; ++step) {
+            const bool pop = !have && !leaf && sp > 0;
+            const uint2 top = stackGet(pop ? sp - 1u : 0u);
+            if (pop) { cur = top; --sp; have = true; }
+            const bool live = have && !leaf;
+            if (!__any(live)) break;  // wave-uniform
+
+            const uint32_t pos = cur.y & 0xFFFFu;
+            const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
+            const uint32_t e = (cur.y >> 16) & 0xFu;
+            const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
+            const uint2 tab = SC[sBase + min(pos, m - 1u)];
+            const uint32_t t0 = tab.x;
+            const uint32_t q0 = t0 & 0xFFFFu, lb0 = (t0 >> 16) & 0xFu, ub0 = (t0 >> 20) & 0xFu;
+            const bool r0 = (t0 >> 24) & 1u;
+            const uint32_t run0 = t0 >> 25, same0 = (tab.y >> 24) & 0x7Fu;
+
+            // ---- pattern symbols from pi[pos] in this step's direction and
+            // the text symbols beyond the span on that side, both in chain
+            // order (symbol j of the chain in bit j); text past the window
+            // edge or before the text start reads as 0 and never matches.
+            // One read each at a side-dependent offset (a left run ends at the
+            // position and is bit-reversed), so the lanes of both sides share it
+            const Planes P16 = chain32(P, r0 ? q0 : q0 + 1u, r0);
+            const Planes T16 = chain32(W, r0 ? yo : xo, r0);
+            const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
+            const uint32_t VT = onesR(avail);
+            const uint32_t E0 = eqm(P16, T16) & VT;                 // p_j == t_j     (M chain, S runs)
+            const uint32_t ED = eqm(P16, shr1(T16)) & (VT >> 1);    // p_j == t_{j+1} (D runs)
+            const uint32_t EI = eqm(shr1(P16), T16) & VT;           // p_{j+1} == t_j (I runs)
+            const uint32_t TZ = (T16.b0 | T16.b1 | T16.b2) & VT;    // t_j is a symbol (not '$' / edge)
+
+            const bool atLeaf = live && pos == m;
+            const bool node = live && pos < m;
+            const bool forced = e == ub0;          // no error child here or in the rest of the run
+            const bool kidsF = e + 1u == ub0;      // the error children are forced nodes
+            const bool mOK = lb0 <= e && e <= ub0;
+            const bool misOK = lb0 <= e + 1u && e + 1u <= ub0;
+            const uint32_t side = r0 ? lastR : lastL;
+            // chain budget: a forced node matches up to kRun symbols; a node
+            // whose error children are forced walks up to kChain positions of
+            // its match chain (same direction, l and u), checking every error
+            // child's forced run on the way; any other node is expanded alone
+            const uint32_t B = forced ? min(run0, kRun)
+                                      : (kidsF ? max(1u, min(min(same0, run0 - 1u), kChain)) : 1u);
+            const uint32_t miss = ~E0 & kRunMask;
+            const uint32_t L = mOK ? min(B, miss ? (uint32_t)__builtin_ctz(miss) : kRun) : 0u;
+
+            // ---- error children of the chain nodes i < NN (node L = the mismatch)
+            const uint32_t NN = L < B ? L + 1u : B;
+            const uint32_t nodesM = node && !forced ? onesR(NN) : 0u;  // leaves / idle lanes: none
+            const uint32_t first = 1u;  // chain node 0 (= this node)
+            uint32_t Dm = EDIT ? (nodesM & TZ) : 0u;
+            if (pos == 0u || side == OP_I) Dm &= ~first;
+            uint32_t Im = EDIT && misOK ? nodesM : 0u;
+            if (side == OP_D) Im &= ~first;
+            // S at the first mismatch (not where M is merely disallowed: l > e)
+            bool Sx = node && !forced && L < B && misOK && ((TZ & ~E0) >> L) & 1u;
+            // forced runs: a child at e + 1 = u is forced for the rest of the run,
+            // and survives only if min(7, rest of the run) symbols match on its
+            // diagonal (positions past the run count as matches): R7x bit j =
+            // that check for a run starting at chain position j on diagonal x
+            const uint32_t bR = beyondR(run0), bR1 = beyondR(run0 - 1u);
+            const uint32_t R7E0 = run7(E0 | bR), R7ED = run7(ED | bR), R7EI = run7(EI | bR1);
+            if (kidsF) {
+                // D at i: p[i..] vs t[i+1..]; I at i: p[i+1..] vs t[i..]; S at L: p[L+1..] vs t[L+1..]
+                Dm &= R7ED;
+                Im &= R7EI;
+                Sx = Sx && ((R7E0 >> (L + 1u)) & 1u);
+            }
+            if (EDIT && node && e + 2u == ub0) {
+                // A node expanded alone whose error children are chain nodes:
+                // keep only the children whose subtree outlives their own first
+                // step. A child does if its match chain leaves the run or the
+                // 32 symbols read (chain length > kRun - 9), or one of its own
+                // error children (forced) passes the check above on its
+                // diagonal; no I right after D, no D right after I (policy P0).
+                // tests/text_model.py holds this to the plain DFS.
+                const uint32_t ED2 = eqm(P16, shr2(T16)) & (VT >> 2);   // p_j == t_{j+2}
+                const uint32_t EI2 = eqm(shr2(P16), T16) & VT;          // p_{j+2} == t_j
+                const uint32_t bR2 = run0 >= 2u ? beyondR(run0 - 2u) : kRunMask;
+                const uint32_t R7ED2 = run7(ED2 | bR), R7EI2 = run7(EI2 | bR2);
+                const uint32_t I2after = (R7E0 >> 1) & ~1u;  // bit j: I2 (back to diagonal 0) at chain node j > 0
+                constexpr uint32_t kLim = kRun - 9u;
+                if (Dm & first) {  // D child: p_j vs t_{j+1}
+                    const uint32_t LD = (uint32_t)__builtin_ctz(~ED);
+                    const bool keep = LD >= run0 || LD > kLim || ((R7ED >> (LD + 1u)) & 1u) ||
+                                      ((R7ED2 | I2after) & onesR(LD + 1u)) != 0u;
+                    if (!keep) Dm &= ~first;
+                }
+                if (Im & first) {  // I child: p_{x+1} vs t_x
+                    const uint32_t LI = ~EI ? (uint32_t)__builtin_ctz(~EI) : kRun;
+                    const bool keep = LI + 1u >= run0 || LI > kLim || ((R7EI >> (LI + 1u)) & 1u) ||
+                                      ((I2after | R7EI2) & onesR(LI + 1u)) != 0u;
+                    if (!keep) Im &= ~first;
+                }
+                if (Sx) {  // S child at the mismatch L = 0: p_x vs t_x, x >= 1
+                    const uint32_t rest = ~E0 & ~1u;
+                    const uint32_t LS = rest ? (uint32_t)__builtin_ctz(rest) : kRun;
+                    Sx = LS >= run0 || LS > kLim || ((R7E0 >> (LS + 1u)) & 1u) ||
+                         ((R7ED | R7EI) & ~1u & onesR(LS + 1u)) != 0u;
+                }
+            }
+            const bool contM = node && L >= B;  // the match chain continues at pos + B
+            uint32_t nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
+            // the lane continues with one child and stacks the others: a
+            // surviving error child first, the match chain below it
+            uint32_t Bc = B;
+            // Stack invariant (stackCap = 2k + 2): a node that stacks entries
+            // with e errors finds sp <= 2e + 2. One node expanded alone stacks
+            // <= 2; a chain may stack more only while the child it continues
+            // with (e + 1) still finds sp <= 2(e + 1) + 2.
+            if (nSurv && sp + nSurv + (contM ? 1u : 0u) - 1u > 2u * e + 4u) {
+                // not enough stack for this chain: expand its first node only
+                Bc = 1u;
+                Dm &= first;
+                Im &= first;
+                Sx = Sx && L == 0u;
+                nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
+            }
+            const bool contM1 = node && L >= Bc;
+            // cannot happen (the reserve rule above; tests/text_model.py): flagged, not handled
+            bad = bad || (node && nSurv && sp + nSurv + (contM1 ? 1u : 0u) - 1u > a.stackCap);
+
+            // ---- children as stack entries (x = span, y = meta). Per step:
+            // extending by n symbols adds n << 16 (right) or -n (left) to the
+            // span, one mad; a child's side memory is its operation on the
+            // extension side (MS once k forced matches follow it), the other
+            // side keeps its memory — except at pos 0, where the first
+            // operation sets both (for chain node i > 0 that was a match)
+            const int extMul = r0 ? 65536 : -1;
+            auto extend = [&](uint32_t span, uint32_t n) -> uint32_t { return span + (uint32_t)((int)n * extMul); };
+            const uint32_t shMine = r0 ? 22u : 20u, shOther = r0 ? 20u : 22u;
+            const uint32_t otherKept = pos ? (r0 ? lastL : lastR) : (uint32_t)OP_MS;
+            auto metaAt = [&](uint32_t i, uint32_t op, uint32_t k) -> uint32_t {
+                const uint32_t mine = k ? (uint32_t)OP_MS : op;
+                const uint32_t other = (pos == 0u && i == 0u) ? op : otherKept;
+                return (mine << shMine) | (other << shOther);
+            };
+            const uint32_t e1 = (e + 1u) << 16;
+            // forced matches after an error child whose run starts at chain node ii
+            const uint32_t kEnd = kidsF ? run0 : 0u;
+            const uint2 cM = make_uint2(extend(cur.x, Bc), (pos + Bc) | (e << 16) | metaAt(Bc, OP_MS, 0u));
+            if (nSurv) {  // the surviving error children; the last one stays in registers
+                uint32_t spw = sp;
+                uint2 pend = cM;
+                bool hasPend = contM1;
+                // one loop over all of them — D at chain node i (bit i), I at i
+                // (bit 32 + i), S at L (bit 63), in that order — so the wave
+                // runs max(nSurv) iterations rather than one loop per kind
+                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << 32) | (Sx ? 1ull << 63 : 0ull);
+                while (sv) {
+                    const uint32_t j = (uint32_t)__builtin_ctzll(sv);
+                    sv &= sv - 1ull;
+                    const bool isS = j == 63u, isD = j < 32u, isI = !isD && !isS;
+                    const uint32_t i = isS ? L : (j & 31u);
+                    const uint32_t ii = i + (isD ? 0u : 1u);  // chain node where its forced run starts
+                    const uint32_t k = ii < kEnd ? min(kEnd - ii, 7u) : 0u;
+                    const uint32_t op = isD ? (uint32_t)OP_D : (isI ? (uint32_t)OP_I : (uint32_t)OP_MS);
+                    const uint2 v = make_uint2(extend(cur.x, i + k + (isI ? 0u : 1u)), (pos + ii + k) | e1 | metaAt(i, op, k));
+                    if (hasPend) stackPut(min(spw++, a.stackCap - 1u), pend);
+                    pend = v;
+                    hasPend = true;
+                }
+                sp = min(spw, a.stackCap);
+                cur = pend;
+            } else if (node && contM1) {
+                cur = cM;
+            }
+
+            if (atLeaf) { leaf = true; leafStart = xo; leafE = e; }
+            have = live ? node && (nSurv || contM1) : have;
+            if (COUNT) {
+                cNodes += forced ? 0u : (node ? NN : 0u);
+                cCmp += (node && forced) ? 1u : 0u;
+                cSteps += node ? 1u : 0u;
+            }
+        }
+        if (COUNT) {
+            const uint64_t t1 = clock64();
+            cyStep += t1 - t0;
+            t0 = t1;
+        }
+        {
+            uint32_t s;
+            if (hitSlots.take(leaf, lane, ltMask, a.hitCount, s) && leaf) {
+                if (s < a.hitCap) {
+                    a.hits[s] = make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown);
+                    // the hit's row ranked in its query's segment (a.qcnt,
+                    // the FM phase's counts): the atomic's result is stored
+                    // at the lane's next emission, so that its round trip
+                    // overlaps the micro-steps in between (kLocate then
+                    // places the hit without an atomic of its own)
+                    if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
+                    rankVal = atomicAdd(a.qcnt + pid, 1u);
+                    rankSlot = s;
+                } else {
+                    atomicOr(a.flags, 2u);
+                }
+                ++filled;
+            }
+        }
+        if (COUNT) cyEmit += clock64() - t0;
+    }
+    hitSlots.close(lane, a.hits, a.hitCap);
+    if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
+    if (filled) atomicAdd(a.filled, filled);  // per-lane counts
+    if (__any(bad) && lane == 0) atomicOr(a.flags, 16u);
+    if (COUNT) {
+        atomicAdd(a.counters + 5, (unsigned long long)cNodes);
+        if (lane == 0) {
+            atomicAdd(a.counters + 8, (unsigned long long)tIter);
+            atomicAdd(a.counters + 9, (unsigned long long)tActive);
+            atomicAdd(a.counters + 10, (unsigned long long)tRefill);
+            atomicAdd(a.counters + 11, (unsigned long long)cyRefill);
+            atomicAdd(a.counters + 12, (unsigned long long)cyStep);
+            atomicAdd(a.counters + 13, (unsigned long long)cyEmit);
+        }
+        atomicAdd(a.counters + 14, (unsigned long long)cCmp);
+        atomicAdd(a.counters + 15, (unsigned long long)cSteps);
+    }
+}
+
 // ---- the text phase of a whole pass in one launch (r5)
 //
 // One launch serves the batches [b0, b1) of a pass, so the text phase has no
@@ -813,24 +1309,6 @@ __host__ __device__ constexpr TextShape textShape(int shape) {
 // sleeps; it ends when the host aborts the pass (ctl[0]) or after waiting
 // timeoutTicks (wall clock) — the host then finds the launch ended with a
 // batch not done and redoes the pass one batch at a time (pass.cpp).
-typedef __attribute__((address_space(1))) uint32_t GlobalU32;
-// Pointers that come from memory (the slot table) are generic: accesses through
-// them would be flat instructions, which also count against the LDS counter
-// and make every LDS wait wait for them. They address global memory, so say so.
-// (The host pass of this file parses kernel bodies too, where class types in
-// an address space do not convert: there the cast is a plain one.)
-#if defined(__HIP_DEVICE_COMPILE__)
-#define GLOB(T, p) ((__attribute__((address_space(1))) T*)(p))
-#else
-#define GLOB(T, p) ((T*)(p))
-#endif
-// A 16-B record through a global pointer: uint4 is a class type whose copy
-// goes through a generic reference (a flat load again), a native vector is not
-typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 loadGlobal4(const uint4* p) {
-    const U32x4 v = *GLOB(const U32x4, p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
 __device__ __forceinline__ uint32_t pollWord(const uint32_t* p) {  // relaxed, agent scope: an sc1 load
     return __hip_atomic_load((GlobalU32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -840,23 +1318,13 @@ __device__ __forceinline__ uint32_t pollWord(const uint32_t* p) {  // relaxed, a
 // done: a release fence there (buffer_wbl2) wrote back the whole L2 of its
 // XCD at every wave's every batch, dirty lines of every other kernel included,
 // and slowed everything beside the text phase 3-10x.
-typedef __attribute__((address_space(1))) uint64_t GlobalU64;
-#ifdef SAHARA_V_PLAIN
-__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) { *GLOB(uint32_t, p) = v; }
-__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) { *GLOB(uint4, p) = v; }
-#else
-__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) {
-    __hip_atomic_store((GlobalU32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) {
-    GlobalU64* q = (GlobalU64*)p;
-    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#endif
 
+// Four waves per SIMD (<= 128 VGPRs): four workgroups per CU alone, three
+// beside an FM workgroup. Left to itself the compiler took 142-166 VGPRs
+// (three and two); held to 128 it spills a few values of the refill path
+// (none in the micro-step loop). Count mode's instrumentation is not held.
 template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
-__global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : 4))) void kSearchText(TextArgs a) {
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t arrive[8];  // waves of this workgroup past batch b, at b % 8
     // published task counts this workgroup has seen ([b % 8][phase], tagged
@@ -896,14 +1364,25 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     // reaches a batch, so that a chunk switch does not wait for the table
     const uint4 *patP0 = nullptr, *patP1 = nullptr;
     uint32_t patN0 = 0, patN1 = 0;
+    // (wave-uniform values read from memory: made scalar, or the compiler
+    // guards every pattern load with a loop over the lanes' distinct buffers)
     auto loadPats = [&](uint32_t b) __attribute__((always_inline)) {
         const TextBatch B = a.batches[b];
-        if (b & 1u) { patP1 = a.pats3 + B.q0 * patBlocks; patN1 = B.npat * patBytes; }
-        else { patP0 = a.pats3 + B.q0 * patBlocks; patN0 = B.npat * patBytes; }
+        const uint64_t q0 = uniform64(B.q0);
+        const uint32_t n = __builtin_amdgcn_readfirstlane(B.npat) * patBytes;
+        if (b & 1u) { patP1 = a.pats3 + q0 * patBlocks; patN1 = n; }
+        else { patP0 = a.pats3 + q0 * patBlocks; patN0 = n; }
     };
     loadPats(a.b0);
+    // the pattern buffer of batch b, built from scalars where it is used: a
+    // buffer descriptor the compiler holds in vector registers (a value
+    // assigned on a path it cannot prove uniform) makes it wrap every load in
+    // a loop over the lanes' distinct descriptors
     auto patBufOf = [&](uint32_t b) __attribute__((always_inline)) {
-        return (b & 1u) ? bufferOf(patP1, patN1) : bufferOf(patP0, patN0);
+        const bool odd = (__builtin_amdgcn_readfirstlane(b) & 1u) != 0u;
+        const uint64_t ptr = (uint64_t)(odd ? patP1 : patP0);
+        const uint64_t p = uniform64(ptr);
+        return bufferOf(reinterpret_cast<const void*>(p), __builtin_amdgcn_readfirstlane(odd ? patN1 : patN0));
     };
     // the slot buffers of the (at most two) batches the wave holds, by batch
     // parity: loaded when the queue reaches a batch, so emission and retire
@@ -941,7 +1420,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
     uint32_t nBase = 0, nEnd = 0, qBase = 0, cBat = a.b0, nBat = a.b0;
     bool haveNext = false;
-    __amdgpu_buffer_rsrc_t patBuf = patBufOf(a.b0);
     // The prefetched chunk's records still hold SA rows. Their text positions
     // are read at the next refill, beside its window loads (one round trip for
     // both), or at the latest when the chunk becomes current.
@@ -1018,7 +1496,21 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 nEnd = qLo + e;
                 nBat = qb;
                 nextRec = make_uint4(0, 0, 0, 0);
-                if (nBase + lane < nEnd) nextRec = loadGlobal4(qTasks + nBase + lane);
+                if (nBase + lane < nEnd) {
+#if defined(SAHARA_X_LD_FLAT)
+                    nextRec = qTasks[nBase + lane];
+#elif defined(SAHARA_X_LD_BUF)
+                    const U32x4 v = __builtin_bit_cast(U32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                        bufferOf(qTasks, 0xFFFFFFF0u), (nBase + lane) * 16u, 0, 0));
+                    nextRec = make_uint4(v.x, v.y, v.z, v.w);
+#elif defined(SAHARA_X_LD_2X8)
+                    const uint64_t* q = reinterpret_cast<const uint64_t*>(qTasks + nBase + lane);
+                    const uint64_t lo8 = *GLOB(const uint64_t, q), hi8 = *GLOB(const uint64_t, q + 1);
+                    nextRec = make_uint4((uint32_t)lo8, (uint32_t)(lo8 >> 32), (uint32_t)hi8, (uint32_t)(hi8 >> 32));
+#else
+                    nextRec = loadGlobal4(qTasks + nBase + lane);
+#endif
+                }
                 haveNext = true;
                 nextRaw = true;
                 return 1u;
@@ -1088,8 +1580,13 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0, cyIdle = 0, cyGrab = 0, cyStart = 0, cySteal = 0,
              cyRetire = 0, cyResolve = 0, cySwitch = 0, nGrab = 0, cyShfl = 0, cyTail = 0, cyTop = 0;
     const uint64_t tBorn = COUNT ? clock64() : 0;
+    __shared__ uint64_t wBorn[4], wDrain[4];
+    uint32_t pIterPre = 0, pIterPost = 0, pActPre = 0, pActPost = 0, pSleeps = 0, pSteals = 0;
+    uint64_t pwPreA = 0, pwPreB = 0, pwPostA = 0, pwPostB = 0;
+    if (a.probe && lane == 0) wBorn[threadIdx.x >> 6] = wall_clock64(), wDrain[threadIdx.x >> 6] = 0;
 
     for (;;) {
+        const uint64_t pw0 = a.probe ? wall_clock64() : 0;
         // Starting a task costs a global round trip (window + pattern) that
         // stalls the whole wave, so idle lanes are refilled in batches: once
         // refillAt lanes are idle (or nothing else is left).
@@ -1113,7 +1610,10 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     --pollSkip;
                 } else {
                     const uint64_t g0 = COUNT ? clock64() : 0;
-                    if (grab() != 1u) pollSkip = 8;
+                    const uint32_t got = grab();
+                    if (got != 1u) pollSkip = 8;
+                    if (a.probe && got == 2u && lane == 0 && wDrain[threadIdx.x >> 6] == 0)
+                        wDrain[threadIdx.x >> 6] = wall_clock64();
                     if (COUNT) { cyGrab += clock64() - g0; ++nGrab; }
                 }
             }
@@ -1130,7 +1630,6 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 qEnd = nEnd;
                 curRec = nextRec;
                 cBat = nBat;
-                patBuf = patBufOf(cBat);
                 haveNext = false;
                 tried = false;
                 if (COUNT) cySwitch += clock64() - w0;
@@ -1146,6 +1645,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                                        __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
             const uint64_t s0 = COUNT ? clock64() : 0;
             if (COUNT) cyShfl += s0 - h0;
+            const __amdgpu_buffer_rsrc_t patBuf = patBufOf(cBat);
             if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
                 // ---- start a task (x = its text position): copy the pattern
                 // and the text window its subtree can reach
@@ -1198,7 +1698,11 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
         // window start, scheme row, batch parity) by shuffle. The DFS of the
         // entry is the same whichever lane runs it, so the hits are too.
         const uint64_t st0 = COUNT ? clock64() : 0;
+#ifdef SAHARA_X_NOSTEAL
+        if (false) {
+#else
         if (a.stealAt && dry) {
+#endif
             const bool thief = !have && sp == 0u;
             const uint64_t I = __ballot(thief);
             const uint64_t D = __ballot(sp >= 2u || (sp == 1u && have));
@@ -1214,6 +1718,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                     const uint32_t c = (uint32_t)__popcll(dm & ((1ull << w) - 1ull));
                     if (rr >= c) { rr -= c; dm >>= w; donor += w; }
                 }
+                if (a.probe) ++pSteals;
                 const bool takes = thief && r < n;
                 donor = takes ? donor : lane;
                 const uint32_t dPid = __shfl(pid, donor), dWb = __shfl(wb, donor), dBase = __shfl(sBase, donor);
@@ -1251,6 +1756,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
                 waiting = true;
                 waitStart = wall_clock64();
             }
+            if (a.probe) ++pSleeps;
             __builtin_amdgcn_s_sleep(60);  // ~1.6 us
             if ((++idleSpins & 63u) == 0u) {
                 uint32_t abort = 0;
@@ -1274,6 +1780,11 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             continue;
         }
         waiting = false;
+        if (a.probe) {  // iterations and busy lanes before / after the wave saw all tasks taken
+            const uint32_t act = (uint32_t)__popcll(__ballot(have || sp > 0));
+            const uint32_t post = wDrain[threadIdx.x >> 6] != 0 ? 1u : 0u;
+            if (post) { ++pIterPost; pActPost += act; } else { ++pIterPre; pActPre += act; }
+        }
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);
             if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
@@ -1282,6 +1793,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             t0 = t1;
         }
 
+        const uint64_t pw1 = a.probe ? wall_clock64() : 0;
         // ---- up to a.steps micro-steps per lane; a lane that reaches a leaf
         // holds it (stalls) until the emission below
         bool leaf = false;
@@ -1518,6 +2030,36 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             }
         }
         if (COUNT) cyEmit += clock64() - t0;
+        if (a.probe) {
+            const uint64_t pw2 = wall_clock64();
+            if (wDrain[threadIdx.x >> 6] != 0) { pwPostA += pw1 - pw0; pwPostB += pw2 - pw1; }
+            else { pwPreA += pw1 - pw0; pwPreB += pw2 - pw1; }
+        }
+    }
+    if (a.probe && a.b0 == 0 && lane == 0) {  // the first launch's wave lives on the wall clock
+        const uint64_t wEnd = wall_clock64(), w0 = wBorn[threadIdx.x >> 6];
+        atomicMin(a.counters + 33, (unsigned long long)w0);
+        atomicMax(a.counters + 34, (unsigned long long)w0);
+        atomicMax(a.counters + 35, (unsigned long long)wEnd);
+        atomicAdd(a.counters + 36, (unsigned long long)(wEnd - w0));
+        atomicMin(a.counters + 37, (unsigned long long)wEnd);
+        const uint64_t wd = wDrain[threadIdx.x >> 6];
+        if (wd) {  // the wave saw the pass's tasks all taken: when, and how long it ran on
+            atomicMin(a.counters + 38, (unsigned long long)wd);
+            atomicMax(a.counters + 39, (unsigned long long)wd);
+            atomicAdd(a.counters + 30, (unsigned long long)(wEnd - wd));
+            atomicAdd(a.counters + 31, 1ull);
+        }
+        atomicAdd(a.counters + 40, (unsigned long long)pIterPre);
+        atomicAdd(a.counters + 41, (unsigned long long)pActPre);
+        atomicAdd(a.counters + 42, (unsigned long long)pIterPost);
+        atomicAdd(a.counters + 43, (unsigned long long)pActPost);
+        atomicAdd(a.counters + 44, (unsigned long long)pSleeps);
+        atomicAdd(a.counters + 45, (unsigned long long)pSteals);
+        atomicAdd(a.counters + 46, (unsigned long long)pwPreA);
+        atomicAdd(a.counters + 47, (unsigned long long)pwPreB);
+        atomicAdd(a.counters + 48, (unsigned long long)pwPostA);
+        atomicAdd(a.counters + 49, (unsigned long long)pwPostB);
     }
     if (COUNT) {
         atomicAdd(a.counters + 5, (unsigned long long)cNodes);
@@ -1540,6 +2082,7 @@ __global__ __launch_bounds__(256) void kSearchText(TextArgs a) {
             atomicAdd(a.counters + 30, (unsigned long long)cyShfl);
             atomicAdd(a.counters + 31, (unsigned long long)cyTail);
             atomicAdd(a.counters + 32, (unsigned long long)cyTop);
+
         }
         atomicAdd(a.counters + 14, (unsigned long long)cCmp);
         atomicAdd(a.counters + 15, (unsigned long long)cSteps);
@@ -1673,15 +2216,16 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
         const uint4 hit = a.hits[h];
         if (hit.z == 0) continue;  // reserved hole
         const uint64_t e = hit.w & 0xFu;
-        if (hit.w & kPosKnown) {  // resolved by the text phase: the segment's tail, counted down
-#ifdef SAHARA_V_NOTCNT
-            continue;  // (timing variant: text hits not counted, not located)
-#endif
+        if ((hit.w & kPosKnown) && a.tcnt) {  // (one text launch) the segment's tail, counted down
             const uint32_t left = atomicSub(a.tcnt + hit.x, 1u);
             a.keys[a.qoff[hit.x + 1] - left] = ((uint64_t)hit.y << 4) | e;
             continue;
         }
         const uint64_t out = a.qoff[hit.x] + a.rank[h];
+        if (hit.w & kPosKnown) {  // resolved by the text phase, ranked where it was written
+            a.keys[out] = ((uint64_t)hit.y << 4) | e;
+            continue;
+        }
         if (a.useSA) {  // full SA resident: one read per row
             for (uint32_t j = 0; j < hit.z; ++j) a.keys[out + j] = ((uint64_t)a.sa[hit.y + j] << 4) | e;
             continue;
@@ -2045,6 +2589,18 @@ void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_
     }
 }
 
+template <int SIGMA, int SHAPE>
+const void* textKernelOf(bool edit, bool count) {
+    if (edit) return count ? (const void*)kSearchText<SIGMA, true, true, SHAPE> : (const void*)kSearchText<SIGMA, true, false, SHAPE>;
+    return count ? (const void*)kSearchText<SIGMA, false, true, SHAPE> : (const void*)kSearchText<SIGMA, false, false, SHAPE>;
+}
+
+template <int SIGMA>
+const void* textKernelOfShape(bool edit, bool count, int shape) {
+    return shape == 1 ? textKernelOf<SIGMA, 1>(edit, count)
+                      : shape == 2 ? textKernelOf<SIGMA, 2>(edit, count) : textKernelOf<SIGMA, 0>(edit, count);
+}
+
 template <int SIGMA>
 void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
     const int shape = textShapeOf(a.winBlocks, a.patBlocks, a.exactWindow != 0u);
@@ -2073,11 +2629,27 @@ int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
     return b < 1 ? 1 : b;
 }
 
-int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
+template <int SIGMA>
+const void* textBatchKernelOf(bool edit, bool count, int shape) {
+#define SH_TB(S)                                                                                         \
+    if (shape == S)                                                                                      \
+        return edit ? (count ? (const void*)kSearchTextBatch<SIGMA, true, true, S>                       \
+                             : (const void*)kSearchTextBatch<SIGMA, true, false, S>)                     \
+                    : (count ? (const void*)kSearchTextBatch<SIGMA, false, true, S>                      \
+                             : (const void*)kSearchTextBatch<SIGMA, false, false, S>);
+    SH_TB(1)
+    SH_TB(2)
+    SH_TB(0)
+#undef SH_TB
+    return nullptr;
+}
+
+int textBlocksPerCU(uint32_t sigma, bool edit, bool count, int shape, size_t lds, bool persistent) {
+    // (the variant that is launched: its registers differ by shape and count mode)
     int b = 0;
-    const void* f;
-    if (sigma == 5) f = edit ? (const void*)kSearchText<5, true, false> : (const void*)kSearchText<5, false, false>;
-    else            f = edit ? (const void*)kSearchText<6, true, false> : (const void*)kSearchText<6, false, false>;
+    const void* f = persistent
+                        ? (sigma == 5 ? textKernelOfShape<5>(edit, count, shape) : textKernelOfShape<6>(edit, count, shape))
+                        : (sigma == 5 ? textBatchKernelOf<5>(edit, count, shape) : textBatchKernelOf<6>(edit, count, shape));
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b;
 }
@@ -2089,22 +2661,7 @@ int textBlocksPerCU(uint32_t sigma, bool edit, size_t lds) {
 // and a 16 KB locate-chain workgroup (kSortBigLds, kScanTiles).
 int textBlocksBeside(uint32_t sigma, bool edit, bool count, int shape, size_t textLds, size_t fmLds, int want) {
     auto textFn = [&]() -> const void* {
-#define SH_TEXT_FN(S)                                                                                     \
-    if (shape == S) {                                                                                     \
-        if (sigma == 5)                                                                                   \
-            return edit ? (count ? (const void*)kSearchText<5, true, true, S> : (const void*)kSearchText<5, true, false, S>)    \
-                        : (count ? (const void*)kSearchText<5, false, true, S> : (const void*)kSearchText<5, false, false, S>); \
-        return edit ? (count ? (const void*)kSearchText<6, true, true, S> : (const void*)kSearchText<6, true, false, S>)        \
-                    : (count ? (const void*)kSearchText<6, false, true, S> : (const void*)kSearchText<6, false, false, S>);     \
-    }
-        SH_TEXT_FN(1)
-        SH_TEXT_FN(2)
-#undef SH_TEXT_FN
-        if (sigma == 5)
-            return edit ? (count ? (const void*)kSearchText<5, true, true, 0> : (const void*)kSearchText<5, true, false, 0>)
-                        : (count ? (const void*)kSearchText<5, false, true, 0> : (const void*)kSearchText<5, false, false, 0>);
-        return edit ? (count ? (const void*)kSearchText<6, true, true, 0> : (const void*)kSearchText<6, true, false, 0>)
-                    : (count ? (const void*)kSearchText<6, false, true, 0> : (const void*)kSearchText<6, false, false, 0>);
+        return sigma == 5 ? textKernelOfShape<5>(edit, count, shape) : textKernelOfShape<6>(edit, count, shape);
     };
     const void* fm;
     if (sigma == 5)
@@ -2128,6 +2685,32 @@ void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, ui
                   hipStream_t st) {
     if (sigma == 5) launchFMT<5>(a, edit, count, dim3(blocks), lds, st);
     else            launchFMT<6>(a, edit, count, dim3(blocks), lds, st);
+    SH_HIP(hipGetLastError());
+}
+
+template <int SIGMA, int SHAPE>
+void launchTextBatchShaped(const TextBatchArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
+    if (edit) {
+        if (count) hipLaunchKernelGGL((kSearchTextBatch<SIGMA, true, true, SHAPE>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchTextBatch<SIGMA, true, false, SHAPE>), grid, dim3(256), lds, st, a);
+    } else {
+        if (count) hipLaunchKernelGGL((kSearchTextBatch<SIGMA, false, true, SHAPE>), grid, dim3(256), lds, st, a);
+        else       hipLaunchKernelGGL((kSearchTextBatch<SIGMA, false, false, SHAPE>), grid, dim3(256), lds, st, a);
+    }
+}
+
+template <int SIGMA>
+void launchTextBatchT(const TextBatchArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
+    const int shape = textShapeOf(a.winBlocks, a.patBlocks, a.exactWindow != 0u);
+    if (shape == 1) launchTextBatchShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
+    else if (shape == 2) launchTextBatchShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
+    else launchTextBatchShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
+}
+
+void launchTextBatch(const TextBatchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
+                     hipStream_t st) {
+    if (sigma == 5) launchTextBatchT<5>(a, edit, count, dim3(blocks), lds, st);
+    else            launchTextBatchT<6>(a, edit, count, dim3(blocks), lds, st);
     SH_HIP(hipGetLastError());
 }
 

@@ -2,7 +2,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for L in "$@"; do
-  n=$(basename $L .so)
-  SAHARA_HIP_LIB=$PWD/$L timeout -k 10 200 python -u tools/ab_inproc.py --rounds 1 --steps 5 serial=SAHARA_PIPELINE=0 pipe=SAHARA_PIPELINE=1 > gpurun_out/tim_$n.txt 2>&1 || { tail gpurun_out/tim_$n.txt; exit 1; }
-  grep "^round" gpurun_out/tim_$n.txt | sed "s/^/$n /"
+  n=$(echo "$L" | tr '/' '_' | sed 's/\.so$//')
+  f=gpurun_out/tim_$n.txt
+  SAHARA_HIP_LIB=$PWD/$L timeout -k 10 200 python -u tools/ab_inproc.py --rounds 1 --steps 5 ${TIMING_SETTINGS:-serial=SAHARA_PIPELINE=0 pipe=SAHARA_PIPELINE=1} > $f 2>&1 || { tail $f; exit 1; }
+  grep -h "^round" $f | sed "s#^#$n #"
 done
