@@ -343,7 +343,7 @@ def main():
         text_ms_step = text_ms / args.steps
         kern = {"kSearchFM": {"ms": round(search_ms_step, 2), "bytes": search_bytes,
                               "GBs": round(search_bytes / (search_ms_step / 1e3) / 1e9, 1)},
-                "kSearchText": {"ms": round(text_ms_step, 2), "bytes": text_bytes,
+                "kSearchTextBatch": {"ms": round(text_ms_step, 2), "bytes": text_bytes,
                                 "GBs": round(text_bytes / max(text_ms_step, 1e-6) * 1e3 / 1e9, 1)}}
         dom = max(kern, key=lambda n: kern[n]["ms"])
         # launches per step of the dominant kernel (the first batch's text
@@ -364,8 +364,8 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                     "algorithmic_bytes_per_launch": round(kern[dom]["bytes"] / per_launch),
                     "units_per_launch": round(reads_per_launch), "launch_ms": round(launch_ms, 3),
-                    "note": ("kSearchText is VALU/LDS-issue bound (DESIGN.md §3.4): its HBM fraction is small by "
-                             "construction") if dom == "kSearchText" else "memory-latency bound (DESIGN.md §3.2)",
+                    "note": ("kSearchTextBatch is VALU/LDS-issue bound (DESIGN.md §3.4): its HBM fraction is small by "
+                             "construction") if dom == "kSearchTextBatch" else "memory-latency bound (DESIGN.md §3.2)",
                     "survey_8d": {"B_read": round(b_read, 1),
                                   "reference_equivalent_GBs": round(b_read * reads_per_s / 1e9, 1),
                                   "reference_equivalent_frac": round(b_read * reads_per_s / 1e9 / HBM_PEAK_GBS, 3),
@@ -378,7 +378,7 @@ def main():
                 roofline["traffic"] = tr["bytes_per_launch"]
                 roofline["traffic_GBs"] = tr["traffic_GBs"]
                 roofline["traffic_source"] = os.path.relpath(tj, ROOT)
-        # the bound that applies to kSearchText: VALU issue. Its instruction
+        # the bound that applies to kSearchTextBatch: VALU issue. Its instruction
         # count per launch comes from the committed SQ counter pass of the
         # same build and workload (tools/pmc_text.sh -> profiles/pmc_<config>.json)
         pj = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
@@ -441,7 +441,7 @@ def main():
     # the timed calls' own launches, timed with HIP events on their streams
     # (comparable with a rocprofv3 kernel trace of this same command)
     extra["timed_launches"] = {
-        "kSearchText": {"launches_per_step": text_launches / args.steps,
+        "kSearchTextBatch": {"launches_per_step": text_launches / args.steps,
                         "avg_launch_ms": round(text_ms / max(1, text_launches), 4)},
         "kSearchFM": {"launches_per_step": launches / args.steps,
                       "avg_launch_ms": round(search_ms / max(1, launches), 4)}}

@@ -218,7 +218,7 @@ Ctx* newCtx(int device) {
     });
     for (auto& sl : c->slot) {
         for (hipEvent_t* e : {&sl.fmStart, &sl.seedDone, &sl.seedDone0, &sl.seedMid, &sl.fmBegin, &sl.fmDone,
-                              &sl.textStart, &sl.textDone, &sl.free})
+                              &sl.textStart, &sl.textDone, &sl.free, &sl.textMid0, &sl.textMid1})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);
         sl.queues.reserve(768);

@@ -355,9 +355,13 @@ struct Ctx {
         // its launch(es): seeds fmStart..seedDone (sD), FM fmBegin..fmDone
         // (sA), text textStart..textDone (sB, one launch per batch; with one
         // launch per pass, Ctx::txStart..txEnd); seedDone0: the batch's first
-        // seed tasks are published
+        // seed tasks are written (published)
         hipEvent_t fmStart = nullptr, seedDone = nullptr, seedDone0 = nullptr, seedMid = nullptr, fmBegin = nullptr,
                    fmDone = nullptr, textStart = nullptr, textDone = nullptr, free = nullptr;
+        // the first batch of an early pass launches its text phase twice:
+        // textStart..textMid0, then textMid1..textDone (not the wait between)
+        hipEvent_t textMid0 = nullptr, textMid1 = nullptr;
+        bool twoText = false;
         bool seedsInParts = false;        // seeds in two launches: fmStart..seedDone0, seedMid..seedDone
     } slot[kSlots];
     hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
@@ -534,7 +538,7 @@ struct Ctx {
         if (stF) (void)hipStreamDestroy(stF);
         for (auto& sl : slot)
             for (hipEvent_t e : {sl.fmStart, sl.seedDone, sl.seedDone0, sl.seedMid, sl.fmBegin, sl.fmDone, sl.textStart,
-                                 sl.textDone, sl.free})
+                                 sl.textDone, sl.free, sl.textMid0, sl.textMid1})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
         if (batchHost) (void)hipHostFree(batchHost);

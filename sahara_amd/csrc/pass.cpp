@@ -611,6 +611,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // first batch of an early pass in two: its seed tasks while its FM
         // phase runs, then the tasks the FM phase appended after them
         const bool split0 = early && b == 0;
+        sl.twoText = split && split0;
         SH_HIP(hipStreamWaitEvent(sB, split0 ? sl.seedDone0 : sl.fmDone, 0));
         SH_HIP(hipEventRecord(sl.textStart, sB));
         if (split) {
@@ -647,7 +648,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             if (split0) {
                 t.taskCount = sl.small.ptr + 5;
                 launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);
+                SH_HIP(hipEventRecord(sl.textMid0, sB));
                 SH_HIP(hipStreamWaitEvent(sB, sl.fmDone, 0));
+                SH_HIP(hipEventRecord(sl.textMid1, sB));
                 t.taskBegin = sl.small.ptr + 5;
                 t.taskCount = sl.small.ptr + 4;
                 t.work = sl.queues.ptr + 512;
@@ -727,7 +730,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventElapsedTime(&ms, sl.fmBegin, sl.fmDone));
         S.search_ms += ms;
         if (!oneLaunch) {  // (one launch: its span, after the pass)
-            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+            if (sl.twoText) {  // the two launches, not the wait for the FM phase between them
+                SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMid0));
+                S.text_ms += ms;
+                SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textDone));
+            } else {
+                SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
+            }
             S.text_ms += ms;
         }
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
