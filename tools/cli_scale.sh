@@ -26,6 +26,15 @@ step read_simulator timeout -k 10 600 "$R/bin/sahara" read_simulator -i "$W/ref.
     > "$OUT/read_simulator.txt" 2> "$OUT/read_simulator.err" || { echo "read_simulator failed"; tail -5 "$OUT/read_simulator.err"; exit 1; }
 step search env SAHARA_TIMING=1 timeout -k 10 600 "$R/bin/sahara" search -q "$W/reads.fa" -i "$W/ref.fa.idx" -e 2 -o "$W/out.txt" \
     > "$OUT/search.txt" 2> "$OUT/search.err" || { echo "search failed"; tail -5 "$OUT/search.err"; exit 1; }
+md5sum < "$W/out.txt" > "$OUT/out_md5.txt"
+# (optional) another build's CLI on the same files: its stats and output bytes
+if [ -n "$CLI_B" ]; then
+  step search_b env SAHARA_TIMING=1 timeout -k 10 600 "$R/$CLI_B" search -q "$W/reads.fa" -i "$W/ref.fa.idx" -e 2 -o "$W/out_b.txt" \
+      > "$OUT/search_b.txt" 2> "$OUT/search_b.err" || { echo "search_b failed"; tail -5 "$OUT/search_b.err"; exit 1; }
+  md5sum < "$W/out_b.txt" >> "$OUT/out_md5.txt"
+  step search_again env SAHARA_TIMING=1 timeout -k 10 600 "$R/bin/sahara" search -q "$W/reads.fa" -i "$W/ref.fa.idx" -e 2 -o "$W/out.txt" \
+      > "$OUT/search_again.txt" 2> "$OUT/search_again.err" || { echo "search again failed"; exit 1; }
+fi
 ls -la "$W" > "$OUT/files.txt"
 head -3 "$W/out.txt" > "$OUT/out_head.txt"; wc -l < "$W/out.txt" >> "$OUT/out_head.txt"
 echo done
