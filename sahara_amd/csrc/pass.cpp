@@ -509,16 +509,21 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         if (chunked0 && b == 0) {
             // (streamed, early text) the first chunk's seeds as soon as it is
             // up; the text phase starts on their tasks while the rest of the
-            // batch uploads, seeds and runs its FM phase
-            const uint64_t p1 = std::min<uint64_t>(bstart[1], c->up.rc ? 2 * c->up.chunk : c->up.chunk);
+            // batch uploads; the other chunks' seeds as each arrives (a lone
+            // batch is four chunks: staging.cpp), then the FM phase
+            const uint64_t step = c->up.rc ? 2 * c->up.chunk : c->up.chunk;
+            const uint64_t p1 = std::min<uint64_t>(bstart[1], step);
             ensureUploaded(c, p1, sD);
             SH_HIP(hipEventRecord(sl.fmStart, sD));
             seeds(0, (uint32_t)(p1 * c->nsearch));
             seedTasksDone(b, sl);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
-            ensureUploaded(c, bstart[b + 1], sD);
-            SH_HIP(hipEventRecord(sl.seedMid, sD));  // the second part's seeds start (after the upload's wait)
-            seeds((uint32_t)(p1 * c->nsearch), a.nitems);
+            SH_HIP(hipEventRecord(sl.seedMid, sD));  // (the later parts' seeds and the upload waits between them)
+            for (uint64_t p0 = p1; p0 < bstart[1]; p0 += step) {
+                const uint64_t pe = std::min<uint64_t>(bstart[1], p0 + step);
+                ensureUploaded(c, pe, sD);
+                seeds((uint32_t)(p0 * c->nsearch), (uint32_t)(pe * c->nsearch));
+            }
             sl.seedsInParts = true;
         } else {
             sl.seedsInParts = false;

@@ -740,6 +740,10 @@ void stageStreamed(Ctx* c, const uint8_t* src, uint64_t rows, bool rc, uint64_t 
     if (const char* e = std::getenv("SAHARA_UPLOAD_CHUNK")) chunkPats = std::max<uint64_t>(2, std::atoll(e));
     uint64_t chunk = rc ? chunkPats / 2 : chunkPats;
     if (U.bits != 8) chunk = std::min<uint64_t>(chunk, Ctx::kRingSlot * 2 / m);
+    // a call of fewer than four chunks is cut in four, so that its first
+    // batch's seeds and text phase start on a quarter of the upload (C2: 1M
+    // reads, one batch; pass.cpp seeds the first batch chunk by chunk)
+    chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (rows + 3) / 4));
     // chunk * m a multiple of 32 symbols: every chunk's region of the staging
     // buffers (s0 / 2 bytes at 2 or 4 bits, s0 at 8) then starts 16-B aligned
     // for kPackFrom2's word loads (C5: m = 250)

@@ -165,12 +165,14 @@ def test_packed_from_fasta_and_dna4(gpu_device, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"SAHARA_CHUNK_SEEDS": "0"}, {"SAHARA_BATCH": "997"},
-                                 {"SAHARA_CHUNK_SEEDS": "0", "SAHARA_BATCH": "997"}])
+                                 {"SAHARA_CHUNK_SEEDS": "0", "SAHARA_BATCH": "997"},
+                                 {"SAHARA_UPLOAD_CHUNK": str(1 << 20)}])
 def test_packed_first_batch_seeds_in_parts(gpu_device, monkeypatch, env):
     """The first batch's text phase started on its seed tasks (also for a lone
-    batch), its seeds in two parts: the first chunk's as soon as it is up,
-    the rest after (small chunks, so the split falls inside the batch); and
-    with one seed launch per batch (SAHARA_CHUNK_SEEDS=0)."""
+    batch), its seeds in parts, chunk by chunk as each is up (small chunks:
+    16 parts; the default chunk size on a call this small: four, as a lone
+    C2 batch is cut, staging.cpp); and with one seed launch per batch
+    (SAHARA_CHUNK_SEEDS=0)."""
     monkeypatch.setenv("SAHARA_UPLOAD_CHUNK", "150")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
