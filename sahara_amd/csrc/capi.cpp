@@ -178,13 +178,19 @@ Ctx* newCtx(int device) {
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    // the text stream gets a hardware queue of its own (a stream with a CU
-    // mask is never given a shared queue): its one launch per pass waits for
-    // the seed and FM kernels, which must not queue behind it
+    // With one text launch per pass (SAHARA_TEXT_ONE_LAUNCH=1 when the context
+    // is created) the text stream gets a hardware queue of its own (a stream
+    // with a CU mask is never given a shared queue): that launch waits for the
+    // seed and FM kernels, which must not queue behind it. Not otherwise: with
+    // a CU-masked stream in the process the memory-bound kernels on the other
+    // streams ran 1.4-1.8x longer, even alone (C3 kernel trace, one stream:
+    // kPackFrom2 67 -> 37 us, kSortDecode 86 -> 51 us, kLocate 71 -> 49 us)
     {
         std::vector<uint32_t> mask((size_t)(c->numCU + 31) / 32, 0xFFFFFFFFu);
-        const char* oq = std::getenv("SAHARA_TEXT_OWN_QUEUE");  // 0: a plain stream (A/B)
-        if (!(oq && std::atoi(oq) == 0) &&
+        const char* ol = std::getenv("SAHARA_TEXT_ONE_LAUNCH");
+        const char* oq = std::getenv("SAHARA_TEXT_OWN_QUEUE");  // 0 / 1: force (A/B)
+        const bool own = oq ? std::atoi(oq) != 0 : (ol && std::atoi(ol) == 1);
+        if (own &&
             hipExtStreamCreateWithCUMask(&c->stB, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
             c->textOwnQueue = true;
         } else {

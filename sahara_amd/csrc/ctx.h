@@ -362,7 +362,8 @@ struct Ctx {
         // textStart..textMid0, then textMid1..textDone (not the wait between)
         hipEvent_t textMid0 = nullptr, textMid1 = nullptr;
         bool twoText = false;
-        bool seedsInParts = false;        // seeds in two launches: fmStart..seedDone0, seedMid..seedDone
+        bool seedsInParts = false;        // seeds in parts: fmStart..seedDone0, then Ctx::partEv's pairs
+        uint32_t seedParts = 0;           // (the later parts: Ctx::partEv[2 i], [2 i + 1] around part i)
     } slot[kSlots];
     hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
     // The text phase of a pipelined pass is one launch (search.hip kSearchText)
@@ -381,6 +382,7 @@ struct Ctx {
     size_t hostDoneCap = 0;
     uint32_t* ctlHost = nullptr;          // pinned: the abort word's source (1)
     hipEvent_t txStart = nullptr, txEnd = nullptr;  // around the pass's text launch
+    std::vector<hipEvent_t> partEv;  // around the first batch's later seed launches (created on demand)
     bool textOwnQueue = false;            // stB was created with its own hardware queue
     uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
     // two pinned staging chunks for handing hits to pageable host memory: the
@@ -522,6 +524,7 @@ struct Ctx {
         if (ringInit.joinable()) ringInit.join();
         expander.reset();
         for (hipEvent_t e : downEv) (void)hipEventDestroy(e);
+        for (hipEvent_t e : partEv) (void)hipEventDestroy(e);
         if (downRing) (void)hipHostFree(downRing);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);

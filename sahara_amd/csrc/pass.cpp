@@ -518,12 +518,21 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             seeds(0, (uint32_t)(p1 * c->nsearch));
             seedTasksDone(b, sl);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
-            SH_HIP(hipEventRecord(sl.seedMid, sD));  // (the later parts' seeds and the upload waits between them)
-            for (uint64_t p0 = p1; p0 < bstart[1]; p0 += step) {
+            // each later part's seed launch timed on its own (not the upload waits between)
+            uint32_t part = 0;
+            for (uint64_t p0 = p1; p0 < bstart[1]; p0 += step, ++part) {
                 const uint64_t pe = std::min<uint64_t>(bstart[1], p0 + step);
                 ensureUploaded(c, pe, sD);
+                while (c->partEv.size() < 2 * (size_t)(part + 1)) {
+                    hipEvent_t e;
+                    SH_HIP(hipEventCreate(&e));
+                    c->partEv.push_back(e);
+                }
+                SH_HIP(hipEventRecord(c->partEv[2 * part], sD));
                 seeds((uint32_t)(p0 * c->nsearch), (uint32_t)(pe * c->nsearch));
+                SH_HIP(hipEventRecord(c->partEv[2 * part + 1], sD));
             }
+            sl.seedParts = part;
             sl.seedsInParts = true;
         } else {
             sl.seedsInParts = false;
@@ -724,10 +733,12 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         c->mark("text done", b);
         const uint32_t* hs = c->pinned + b * 16;
         float ms = 0;
-        if (sl.seedsInParts) {  // the two seed launches, not the upload wait between them
+        if (sl.seedsInParts) {  // the seed launches, not the upload waits between them
             SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone0));
-            S.seed_ms += ms;
-            SH_HIP(hipEventElapsedTime(&ms, sl.seedMid, sl.seedDone));
+            for (uint32_t i = 0; i < sl.seedParts; ++i) {
+                S.seed_ms += ms;
+                SH_HIP(hipEventElapsedTime(&ms, c->partEv[2 * i], c->partEv[2 * i + 1]));
+            }
         } else {
             SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone));
         }
