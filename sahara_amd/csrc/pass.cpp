@@ -9,6 +9,8 @@
 #include <exception>
 #include <thread>
 
+#include <sys/prctl.h>
+
 #include "ctx.h"
 
 namespace sahara {
@@ -685,6 +687,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool sleepy = c->streaming && !serial;
     uint32_t pollUs = 20;
     if (const char* e = std::getenv("SAHARA_POLL_US")) pollUs = (uint32_t)std::max(0, std::atoi(e));
+    unsigned long timerSlackNs = 1000;  // the finisher's timer slack (0: the process default)
+    if (const char* e = std::getenv("SAHARA_TIMER_SLACK_NS")) timerSlackNs = (unsigned long)std::max(0L, std::atol(e));
     // (one launch) the launch marks batch b done in pinned host memory; false
     // if the launch ended without marking it (a wave gave up: the pass is redone)
     bool textFailed = false;
@@ -912,6 +916,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         std::exception_ptr finErr;
         std::thread finisher([&] {
             c->place.bind();
+            // its polls sleep 20 us (SAHARA_POLL_US); Linux stretches a sleep
+            // by the thread's timer slack (50 us by default), which a lone
+            // batch's locate chain waited for twice (C2: ~70 us per wait)
+            if (timerSlackNs) prctl(PR_SET_TIMERSLACK, timerSlackNs, 0, 0, 0);
             try {
                 SH_HIP(hipSetDevice(c->device));
                 bool pending = false;  // finishCheck owed for batch `owed`
