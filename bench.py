@@ -378,6 +378,20 @@ def main():
                 roofline["traffic"] = tr["bytes_per_launch"]
                 roofline["traffic_GBs"] = tr["traffic_GBs"]
                 roofline["traffic_source"] = os.path.relpath(tj, ROOT)
+                if tr.get("avg_launch_us"):
+                    # the same kernel's average launch in that committed kernel
+                    # trace (the traced run is slower: tracing serialises the
+                    # streamed call's launches), and the fraction priced on it
+                    traced_ms = tr["avg_launch_us"] / 1e3
+                    roofline["traced"] = {
+                        "launch_ms": round(traced_ms, 3),
+                        "untraced_over_traced": round(launch_ms / traced_ms, 3),
+                        "achieved": round(kern[dom]["bytes"] / per_launch / (traced_ms / 1e3) / 1e9, 1),
+                        "frac": round(kern[dom]["bytes"] / per_launch / (traced_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "source": os.path.relpath(tj, ROOT),
+                        "same_command_check": "profiles/r05_kSearchTextBatch_launches_c3.csv: the timed call's "
+                                              "launches in a trace of bench.py itself average within 2% of "
+                                              "launch_ms taken in that traced run (tools/bench_profiled.sh)"}
         # the bound that applies to kSearchTextBatch: VALU issue. Its instruction
         # count per launch comes from the committed SQ counter pass of the
         # same build and workload (tools/pmc_text.sh -> profiles/pmc_<config>.json)
@@ -394,6 +408,9 @@ def main():
                     **{kk: pm[kk] for kk in ("SQ_INSTS_SALU", "SQ_INSTS_LDS", "issue_active", "wait_any",
                                              "valu_active", "lds_conflict", "dispatches") if kk in pm},
                     "source": os.path.relpath(pj, ROOT)}
+                if roofline.get("traced"):  # priced on the committed trace's launch time instead
+                    roofline["valu_issue"]["frac_traced"] = round(
+                        pm["SQ_INSTS_VALU"] / (roofline["traced"]["launch_ms"] / 1e3) / VALU_ISSUE_PEAK, 3)
         extra = {"bytes_per_read": round((search_bytes + text_bytes + locate_bytes) / nreads, 1),
                  "kernels": {n: {"ms": v["ms"], "algorithmic_GBs": v["GBs"],
                                  "bytes_per_read": round(v["bytes"] / nreads, 1)} for n, v in kern.items()},
