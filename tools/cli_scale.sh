@@ -24,7 +24,7 @@ step make_ref_fasta timeout -k 10 300 python3 "$R/tools/make_ref_fasta.py" "$W/r
 step index timeout -k 10 600 "$R/bin/sahara" index "$W/ref.fa" > "$OUT/index.txt" 2> "$OUT/index.err" || { echo "index failed"; tail -5 "$OUT/index.err"; exit 1; }
 step read_simulator timeout -k 10 600 "$R/bin/sahara" read_simulator -i "$W/ref.fa" -o "$W/reads.fa" -n "$N" -l 100 -e 2 \
     > "$OUT/read_simulator.txt" 2> "$OUT/read_simulator.err" || { echo "read_simulator failed"; tail -5 "$OUT/read_simulator.err"; exit 1; }
-step search env SAHARA_TIMING=1 timeout -k 10 600 "$R/bin/sahara" search -q "$W/reads.fa" -i "$W/ref.fa.idx" -e 2 -o "$W/out.txt" \
+step search env SAHARA_TIMING=${SEARCH_TIMING:-1} timeout -k 10 600 "$R/bin/sahara" search -q "$W/reads.fa" -i "$W/ref.fa.idx" -e 2 -o "$W/out.txt" \
     > "$OUT/search.txt" 2> "$OUT/search.err" || { echo "search failed"; tail -5 "$OUT/search.err"; exit 1; }
 md5sum < "$W/out.txt" > "$OUT/out_md5.txt"
 # (optional) another build's CLI on the same files: its stats and output bytes
