@@ -1021,6 +1021,13 @@ int sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len) {
         if (c->hitCap == 0) c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         if (c->taskCap == 0) c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
         const uint64_t nb = std::min<uint64_t>((n_patterns + maxBatch - 1) / maxBatch, Ctx::kSlots);
+        // the locate chain's per-batch buffers (pass.cpp; the keys sized for a
+        // batch's rows at four per pattern, grown by the pass if short)
+        c->qoff.reserve(maxBatch + 1);
+        c->big.reserve(maxBatch);
+        c->huge.reserve(maxBatch);
+        c->partial.reserve(scanTiles((uint32_t)maxBatch));
+        c->k0.reserve(std::min<uint64_t>(n_patterns, maxBatch) * 4);
         for (uint64_t i = 0; i < nb; ++i) {
             Ctx::Slot& sl = c->slot[i];
             sl.hits.reserve((size_t)c->hitCap + 1);
@@ -1034,6 +1041,7 @@ int sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len) {
             c->pats.reserve(n_patterns * patWords + 4);
             c->pats3.reserve(n_patterns * patBlocks);
             c->readRaw.reserve((n_patterns + 1) / 2 * len);
+            c->nibPats.reserve((n_patterns * len + 1) / 2 + 16);  // the streamed upload's staging (staging.cpp)
         }
     });
 }
