@@ -661,6 +661,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.stealAt = stealAt;
             t.qcnt = sl.qcnt.ptr;
             t.rank = sl.rank.ptr;
+            t.probe = probe ? 1u : 0u;
+            t.isFirst = b == 0 ? 1u : 0u;
             if (split0) {
                 t.taskCount = sl.small.ptr + 5;
                 launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);

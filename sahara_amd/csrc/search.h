@@ -136,6 +136,8 @@ struct TextBatchArgs {
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
     uint32_t* qcnt;          // as SearchArgs: rows ranked where the hits are written (the FM phase's counts)
     uint32_t* rank;
+    uint32_t probe;          // (profiling) wave lives on the wall clock into counters [30..49] ...
+    uint32_t isFirst;        // ... for the pass's first launch only
 };
 
 struct TextArgs {

@@ -925,8 +925,22 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
     uint2 cur = make_uint2(0, 0);
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
     uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
+    // (profiling, a.probe) the first batch's wave lives on the wall clock, as
+    // kSearchText's probe: the queue seen drained, iterations before / after
+    // Compiled in only with -DSAHARA_X_BATCH_PROBE (tools/build_variant.sh):
+    // it costs the product kernel 14 VGPRs and 12 SGPR spills.
+#ifdef SAHARA_X_BATCH_PROBE
+    constexpr bool kProbe = true;
+#else
+    constexpr bool kProbe = false;
+#endif
+    __shared__ uint64_t wBorn[4], wDrain[4];
+    if (kProbe && a.probe && lane == 0) wBorn[threadIdx.x >> 6] = wall_clock64(), wDrain[threadIdx.x >> 6] = 0;
+    uint32_t pIterPre = 0, pIterPost = 0, pActPre = 0, pActPost = 0;
+    uint64_t pwPreA = 0, pwPreB = 0, pwPostA = 0, pwPostB = 0, pw0 = 0, pw1 = 0;
 
     for (;;) {
+        if (kProbe && a.probe) pw0 = wall_clock64();
         // Starting a task costs a global round trip (window + pattern) that
         // stalls the whole wave, so idle lanes are refilled in batches: once
         // refillAt lanes are idle (or nothing else is left).
@@ -1045,6 +1059,12 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
             }
         }
         if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
+        if (kProbe && a.probe) {
+            if (qDone && lane == 0 && wDrain[threadIdx.x >> 6] == 0) wDrain[threadIdx.x >> 6] = wall_clock64();
+            const uint32_t act = (uint32_t)__popcll(__ballot(have || sp > 0));
+            if (qDone) { ++pIterPost; pActPost += act; } else { ++pIterPre; pActPre += act; }
+            pw1 = wall_clock64();
+        }
         if (COUNT) {
             const uint64_t act = __ballot(have || sp > 0);
             if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
@@ -1260,6 +1280,33 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
             }
         }
         if (COUNT) cyEmit += clock64() - t0;
+        if (kProbe && a.probe) {
+            const uint64_t pw2 = wall_clock64();
+            if (qDone) { pwPostA += pw1 - pw0; pwPostB += pw2 - pw1; }
+            else { pwPreA += pw1 - pw0; pwPreB += pw2 - pw1; }
+        }
+    }
+    if (kProbe && a.probe && a.isFirst && lane == 0) {
+        const uint64_t wEnd = wall_clock64(), w0 = wBorn[threadIdx.x >> 6], wd = wDrain[threadIdx.x >> 6];
+        atomicMin(a.counters + 33, (unsigned long long)w0);
+        atomicMax(a.counters + 34, (unsigned long long)w0);
+        atomicMax(a.counters + 35, (unsigned long long)wEnd);
+        atomicAdd(a.counters + 36, (unsigned long long)(wEnd - w0));
+        atomicMin(a.counters + 37, (unsigned long long)wEnd);
+        if (wd) {
+            atomicMin(a.counters + 38, (unsigned long long)wd);
+            atomicMax(a.counters + 39, (unsigned long long)wd);
+            atomicAdd(a.counters + 30, (unsigned long long)(wEnd - wd));
+            atomicAdd(a.counters + 31, 1ull);
+        }
+        atomicAdd(a.counters + 40, (unsigned long long)pIterPre);
+        atomicAdd(a.counters + 41, (unsigned long long)pActPre);
+        atomicAdd(a.counters + 42, (unsigned long long)pIterPost);
+        atomicAdd(a.counters + 43, (unsigned long long)pActPost);
+        atomicAdd(a.counters + 46, (unsigned long long)pwPreA);
+        atomicAdd(a.counters + 47, (unsigned long long)pwPreB);
+        atomicAdd(a.counters + 48, (unsigned long long)pwPostA);
+        atomicAdd(a.counters + 49, (unsigned long long)pwPostB);
     }
     hitSlots.close(lane, a.hits, a.hitCap);
     if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
