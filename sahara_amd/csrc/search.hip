@@ -155,7 +155,11 @@ __device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
 __device__ __forceinline__ uint32_t nib(uint32_t word, uint32_t i) { return (word >> ((i & 7u) * 4u)) & 0xFu; }
 
 constexpr uint32_t kSeedChunk = 64;   // seeds a wave takes per atomic
-constexpr uint32_t kTaskChunk = 64;   // text tasks a wave takes per atomic
+#ifndef SAHARA_X_TASK_CHUNK
+#define SAHARA_X_TASK_CHUNK 64
+#endif
+constexpr uint32_t kTaskChunk = SAHARA_X_TASK_CHUNK;  // text tasks a wave takes per atomic (<= 64)
+static_assert(kTaskChunk >= 1 && kTaskChunk <= 64, "a chunk's records sit one per lane");
 constexpr uint32_t kHitChunk = 64;    // hit / task slots a wave reserves per atomic
 
 // Per-wave slot reservation for append-only outputs (hits, tasks): ballot +
