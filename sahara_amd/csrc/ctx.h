@@ -306,6 +306,12 @@ private:
     std::exception_ptr err_;
 };
 
+// Text-phase scheduling defaults (SAHARA_TEXT_STEPS / SAHARA_REFILL_AT override
+// them per pass). Two micro-steps per iteration beat four by 5% on C3 and 2% on
+// C5, C2 within noise (profiles/r05_text_steps_ab.txt).
+constexpr uint32_t kTextStepsDefault = 2;
+constexpr uint32_t kRefillAtDefault = 8;
+
 struct Ctx {
     int device = 0;
     Placement place;                      // NUMA node of the device; the context's threads run there
@@ -336,8 +342,8 @@ struct Ctx {
     bool verify = true;
     bool locateSA = true;
     uint32_t split = 1;                   // text-phase threshold (rows per interval)
-    uint32_t textSteps = 4;               // text-phase micro-steps per lane per wave iteration
-    uint32_t refillAt = 8;                // text-phase batch refill threshold (idle lanes)
+    uint32_t textSteps = kTextStepsDefault;  // text-phase micro-steps per lane per wave iteration
+    uint32_t refillAt = kRefillAtDefault;    // text-phase batch refill threshold (idle lanes)
 
     // work buffers. Batches rotate over kSlots slots so that seeds and the FM
     // phase run batches ahead (streams `stD`, `st`) of the text phase (stream

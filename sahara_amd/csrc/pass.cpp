@@ -217,8 +217,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const uint32_t tableWords = std::max<uint32_t>(2 * c->nsearch * c->m, kTextTableMin);
     const size_t textLds = (size_t)tableWords * 4 + (size_t)256 * (3 * (winBlocks + c->patBlocks) + 2 * textStack) * 4;
     if (const char* e = std::getenv("SAHARA_SPLIT")) c->split = (uint32_t)std::max(0L, std::atol(e));
-    if (const char* e = std::getenv("SAHARA_TEXT_STEPS")) c->textSteps = (uint32_t)std::max(1L, std::atol(e));
-    if (const char* e = std::getenv("SAHARA_REFILL_AT")) c->refillAt = (uint32_t)std::min(64L, std::max(1L, std::atol(e)));
+    // read on every pass, so unsetting them restores the defaults (in-process A/Bs)
+    const char* eSteps = std::getenv("SAHARA_TEXT_STEPS");
+    const char* eRefill = std::getenv("SAHARA_REFILL_AT");
+    c->textSteps = eSteps ? (uint32_t)std::max(1L, std::atol(eSteps)) : kTextStepsDefault;
+    c->refillAt = eRefill ? (uint32_t)std::min(64L, std::max(1L, std::atol(eRefill))) : kRefillAtDefault;
     int tbpc = 0;
     // the text phase addresses text and a batch's patterns with 32-bit buffer offsets
     const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
