@@ -11,6 +11,12 @@ LIB      := $(LIBDIR)/libsahara_hip.so
 CLI      := bin/sahara
 HDRS     := $(wildcard $(CSRC)/*.h) include/sahara_hip.h
 
+# the build id compiled into the library (tools/build_id.py: a hash of the
+# sources); the header is rewritten only when the id changes
+BUILD_ID := $(shell python3 tools/build_id.py)
+$(shell mkdir -p $(OBJDIR) && echo '#define SAHARA_BUILD_ID "$(BUILD_ID)"' > $(OBJDIR)/build_id.h.new && \
+        (cmp -s $(OBJDIR)/build_id.h.new $(OBJDIR)/build_id.h || mv $(OBJDIR)/build_id.h.new $(OBJDIR)/build_id.h))
+
 OBJS := $(OBJDIR)/index_build.o $(OBJDIR)/search.o $(OBJDIR)/capi.o $(OBJDIR)/staging.o $(OBJDIR)/pass.o \
         $(OBJDIR)/host_util.o $(OBJDIR)/scheme.o
 
@@ -23,6 +29,9 @@ $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/capi.o: $(OBJDIR)/build_id.h
+$(OBJDIR)/capi.o: HIPFLAGS += -include $(OBJDIR)/build_id.h
 
 $(LIB): $(OBJS)
 	@mkdir -p $(LIBDIR)
@@ -54,6 +63,9 @@ $(ASANDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 $(ASANDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(ASANDIR)
 	$(HIPCC) $(HIPFLAGS) -O1 $(ASAN_HOST) -c $< -o $@
+
+$(ASANDIR)/capi.o: $(OBJDIR)/build_id.h
+$(ASANDIR)/capi.o: HIPFLAGS += -include $(OBJDIR)/build_id.h
 
 $(ASANDIR)/libsahara_hip.so: $(ASAN_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(ASAN_OBJS) -o $@ -lpthread

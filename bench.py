@@ -371,34 +371,44 @@ def main():
                                   "reference_equivalent_frac": round(b_read * reads_per_s / 1e9 / HBM_PEAK_GBS, 3),
                                   "basis": "the reference algorithm's Occ / LF / SA-sample lines + query bytes per "
                                            "read, counted in the reference-execution mode, x reads/s"}}
+        # Committed profiles carry the build id of the library they measured
+        # (tools/build_id.py); one of another build is reported as stale and
+        # nothing is priced on it.
+        build = sa.build_id()
         tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tj):
-            tr = json.load(open(tj)).get(dom)
-            if tr:  # HBM bytes per launch from the committed PMC pass (FETCH_SIZE, calibrated)
+            tall = json.load(open(tj))
+            tr = tall.get(dom)
+            if tr and tall.get("build_id") != build:
+                roofline["stale_traffic_profile"] = {"source": os.path.relpath(tj, ROOT),
+                                                     "build_id": tall.get("build_id"), "this_build": build}
+            elif tr:  # HBM bytes per launch from the committed PMC pass (FETCH_SIZE, calibrated)
                 roofline["traffic"] = tr["bytes_per_launch"]
                 roofline["traffic_GBs"] = tr["traffic_GBs"]
                 roofline["traffic_source"] = os.path.relpath(tj, ROOT)
                 if tr.get("avg_launch_us"):
                     # the same kernel's average launch in that committed kernel
-                    # trace (the traced run is slower: tracing serialises the
-                    # streamed call's launches), and the fraction priced on it
+                    # trace of this build (the traced run is slower: tracing
+                    # serialises the streamed call's launches), and the fraction
+                    # priced on it
                     traced_ms = tr["avg_launch_us"] / 1e3
                     roofline["traced"] = {
                         "launch_ms": round(traced_ms, 3),
-                        "untraced_over_traced": round(launch_ms / traced_ms, 3),
+                        "untraced_over_traced_same_build": round(launch_ms / traced_ms, 3),
                         "achieved": round(kern[dom]["bytes"] / per_launch / (traced_ms / 1e3) / 1e9, 1),
                         "frac": round(kern[dom]["bytes"] / per_launch / (traced_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "source": os.path.relpath(tj, ROOT),
-                        "same_command_check": "profiles/r05_kSearchTextBatch_launches_c3.csv: the timed call's "
-                                              "launches in a trace of bench.py itself average within 2% of "
-                                              "launch_ms taken in that traced run (tools/bench_profiled.sh)"}
+                        "source": os.path.relpath(tj, ROOT), "build_id": build}
         # the bound that applies to kSearchTextBatch: VALU issue. Its instruction
         # count per launch comes from the committed SQ counter pass of the
         # same build and workload (tools/pmc_text.sh -> profiles/pmc_<config>.json)
         pj = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(pj):
-            pm = json.load(open(pj)).get(dom)
-            if pm and pm.get("SQ_INSTS_VALU"):
+            pall = json.load(open(pj))
+            pm = pall.get(dom)
+            if pm and pall.get("build_id") != build:
+                roofline["stale_pmc_profile"] = {"source": os.path.relpath(pj, ROOT),
+                                                 "build_id": pall.get("build_id"), "this_build": build}
+            elif pm and pm.get("SQ_INSTS_VALU"):
                 roofline["valu_issue"] = {
                     "valu_per_launch": pm["SQ_INSTS_VALU"],
                     "frac": round(pm["SQ_INSTS_VALU"] / (launch_ms / 1e3) / VALU_ISSUE_PEAK, 3),
@@ -407,7 +417,7 @@ def main():
                              "cycles per instruction)",
                     **{kk: pm[kk] for kk in ("SQ_INSTS_SALU", "SQ_INSTS_LDS", "issue_active", "wait_any",
                                              "valu_active", "lds_conflict", "dispatches") if kk in pm},
-                    "source": os.path.relpath(pj, ROOT)}
+                    "source": os.path.relpath(pj, ROOT), "build_id": build}
                 if roofline.get("traced"):  # priced on the committed trace's launch time instead
                     roofline["valu_issue"]["frac_traced"] = round(
                         pm["SQ_INSTS_VALU"] / (roofline["traced"]["launch_ms"] / 1e3) / VALU_ISSUE_PEAK, 3)
@@ -437,7 +447,6 @@ def main():
                  "search_launches_per_step": launches // args.steps,
                  "text_launches_per_step": text_launches // args.steps,
                  "search_grid": cnt["search_grid"], "text_grid": cnt["text_grid"],
-                 "text_fallbacks_timed": step_stats.get("text_fallbacks", 0),
                  "pipelined": bool(cnt["pipelined"]),
                  "reference_algorithm": {"ext_lines_per_read": round(ref_cnt["ext_lines"] / nreads, 1),
                                          "lf_steps_per_read": round(ref_cnt["lf_steps"] / nreads, 2),
@@ -538,7 +547,7 @@ def main():
                    "reads_per_gpu": nreads, "read_len": rlen, "errors": k, "ref_len": ref_len,
                    "records": int(len(lens)), "generator": gen, "searches": int(scheme[0].shape[0]),
                    "parallelism": f"replicated-index x{world} (query shards)", "index_build_s": round(build_s, 1),
-                   "hits_total": total_hits, **extra},
+                   "hits_total": total_hits, "build_id": sa.build_id(), **extra},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

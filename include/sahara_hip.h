@@ -103,6 +103,10 @@ typedef struct sahara_stats {
 
 const char* sahara_gpu_last_error(void);
 int  sahara_gpu_device_count(void);
+/* The build id compiled into this library: the first 16 hex digits of the
+ * SHA-256 over its sources (tools/build_id.py). Profiles record it, so that
+ * a measurement can be matched to the build it measured. */
+const char* sahara_build_id(void);
 
 /* --- index residency (replaces the cereal load at search.cpp:162-169) --- */
 /* idx_image: the bytes of a `.idx` file as written by `sahara index`. */

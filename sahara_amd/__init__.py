@@ -89,6 +89,7 @@ class Stats(C.Structure):
 EXPORTED = {
     # name: (restype, argtypes)
     "sahara_gpu_last_error": (C.c_char_p, []),
+    "sahara_build_id": (C.c_char_p, []),
     "sahara_gpu_device_count": (C.c_int, []),
     "sahara_gpu_open": (C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "sahara_gpu_open_file": (C.c_int, [C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]),
@@ -178,6 +179,11 @@ def lib():
             fn.argtypes = args
         _LIB = L
     return _LIB
+
+
+def build_id():
+    """The library's build id (sahara_build_id: SHA-256 prefix of its sources, tools/build_id.py)."""
+    return lib().sahara_build_id().decode()
 
 
 def _check(rc):

@@ -225,6 +225,12 @@ struct HitPart {
 void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool emitErrors, unsigned nt) {
     const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd < 0) throw CliError("can not open output file " + path);
+    struct CloseFd {  // closed on every path out (formatting may throw, e.g. bad_alloc)
+        int fd;
+        bool closed = false;
+        int close() { closed = true; return ::close(fd); }
+        ~CloseFd() { if (!closed) (void)::close(fd); }
+    } closer{fd};
     struct Block {
         const HitPart* part;
         uint64_t lo, hi;
@@ -242,8 +248,23 @@ void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool 
         for (;;) {
             const size_t bi = next.fetch_add(1, std::memory_order_relaxed);
             if (bi >= blocks.size()) return;
+            // A block that fails to format still publishes its end (as an
+            // empty block), so that the blocks after it do not wait forever;
+            // the call then fails.
+            auto publishEmpty = [&] {
+                int64_t off = 0;
+                if (bi > 0)
+                    while ((off = ends[bi - 1].load(std::memory_order_acquire)) < 0) std::this_thread::yield();
+                ends[bi].store(off, std::memory_order_release);
+            };
             const Block& B = blocks[bi];
-            buf.resize((B.hi - B.lo) * 96);
+            try {
+                buf.resize((B.hi - B.lo) * 96);
+            } catch (...) {
+                failed.store(true);
+                publishEmpty();
+                continue;
+            }
             char* o = buf.data();
             char* e = o + buf.size();
             auto line = [&](uint64_t qid, uint64_t seq, uint64_t pos, uint32_t err) {
@@ -292,7 +313,7 @@ void writeHits(const std::string& path, const std::vector<HitPart>& parts, bool 
             }
         }
     });
-    if (::close(fd) != 0 || failed.load()) throw CliError("can not write output file " + path);
+    if (closer.close() != 0 || failed.load()) throw CliError("can not write output file " + path);
 }
 
 // A read-only mapping of a whole file (the .idx image every device loads).

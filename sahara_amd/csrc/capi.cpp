@@ -178,33 +178,14 @@ Ctx* newCtx(int device) {
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    // With one text launch per pass (SAHARA_TEXT_ONE_LAUNCH=1 when the context
-    // is created) the text stream gets a hardware queue of its own (a stream
-    // with a CU mask is never given a shared queue): that launch waits for the
-    // seed and FM kernels, which must not queue behind it. Not otherwise: with
-    // a CU-masked stream in the process the memory-bound kernels on the other
-    // streams ran 1.4-1.8x longer, even alone (C3 kernel trace, one stream:
-    // kPackFrom2 67 -> 37 us, kSortDecode 86 -> 51 us, kLocate 71 -> 49 us)
-    {
-        std::vector<uint32_t> mask((size_t)(c->numCU + 31) / 32, 0xFFFFFFFFu);
-        const char* ol = std::getenv("SAHARA_TEXT_ONE_LAUNCH");
-        const char* oq = std::getenv("SAHARA_TEXT_OWN_QUEUE");  // 0 / 1: force (A/B)
-        const bool own = oq ? std::atoi(oq) != 0 : (ol && std::atoi(ol) == 1);
-        if (own &&
-            hipExtStreamCreateWithCUMask(&c->stB, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
-            c->textOwnQueue = true;
-        } else {
-            (void)hipGetLastError();
-            SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
-        }
-    }
+    // (No stream gets a CU mask: with a CU-masked stream in the process the
+    // memory-bound kernels on the other streams ran 1.4-1.8x longer, r5.)
+    SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stD, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
     SH_HIP(hipStreamCreateWithFlags(&c->stF, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
-    SH_HIP(hipEventCreate(&c->txStart));
-    SH_HIP(hipEventCreate(&c->txEnd));
     for (auto& e : c->evSleep) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     for (auto& e : c->ringEv) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // the streamed upload's pinned ring, pinned while the caller builds or
@@ -270,6 +251,8 @@ Ctx* openImage(int device, const uint8_t* buf, size_t bytes) {
 extern "C" {
 
 const char* sahara_gpu_last_error(void) { return g_err.c_str(); }
+
+const char* sahara_build_id(void) { return SAHARA_BUILD_ID; }
 
 int sahara_gpu_device_count(void) {
     int n = 0;
@@ -1016,10 +999,10 @@ int sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len) {
         if (!c) return;  // (NULL context: the host part only, e.g. beside the index load)
         if (pinned) c->outRecs.reserve(capBytes / 8);
         c->out.reserve(est);
-        // the slots of a streamed pass (pass.cpp runPass: 2M-pattern batches)
+        // the slots of a streamed pass (pass.cpp runPass: 2M-pattern batches),
+        // sized as that pass sizes them
         const uint64_t maxBatch = 1ull << 21;
-        if (c->hitCap == 0) c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
-        if (c->taskCap == 0) c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        initWorkCaps(c, maxBatch);
         const uint64_t nb = std::min<uint64_t>((n_patterns + maxBatch - 1) / maxBatch, Ctx::kSlots);
         // the locate chain's per-batch buffers (pass.cpp; the keys sized for a
         // batch's rows at four per pattern, grown by the pass if short)
@@ -1033,7 +1016,7 @@ int sahara_gpu_prepare(void* ctx, uint64_t n_patterns, uint32_t len) {
             sl.hits.reserve((size_t)c->hitCap + 1);
             sl.rank.reserve((size_t)c->hitCap + 1);
             sl.tasks.reserve((size_t)c->taskCap);
-            sl.qcnt.reserve(2 * (maxBatch + 1));  // (FM counts, text counts: pass.cpp)
+            sl.qcnt.reserve(maxBatch + 1);  // per-query row counts (pass.cpp)
         }
         if (len) {
             const uint64_t patWords = (len + 7) / 8, patBlocks = (len + 31) / 32;

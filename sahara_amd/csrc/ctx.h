@@ -359,9 +359,8 @@ struct Ctx {
                                           // tasks [256, 512), the FM phase's [512, 768)
         // kernel spans, each recorded on the kernel's own stream right around
         // its launch(es): seeds fmStart..seedDone (sD), FM fmBegin..fmDone
-        // (sA), text textStart..textDone (sB, one launch per batch; with one
-        // launch per pass, Ctx::txStart..txEnd); seedDone0: the batch's first
-        // seed tasks are written (published)
+        // (sA), text textStart..textDone (sB); seedDone0: the batch's first
+        // seed tasks are written
         hipEvent_t fmStart = nullptr, seedDone = nullptr, seedDone0 = nullptr, seedMid = nullptr, fmBegin = nullptr,
                    fmDone = nullptr, textStart = nullptr, textDone = nullptr, free = nullptr;
         // the first batch of an early pass launches its text phase twice:
@@ -372,24 +371,7 @@ struct Ctx {
         uint32_t seedParts = 0;           // (the later parts: Ctx::partEv[2 i], [2 i + 1] around part i)
     } slot[kSlots];
     hipStream_t stB = nullptr, stC = nullptr, stD = nullptr;  // text, locate / sort, seeds
-    // The text phase of a pipelined pass is one launch (search.hip kSearchText)
-    // that takes each batch's tasks as the seed and FM streams publish them
-    // (bflags) and tells the finisher when a batch is done (hostDone, pinned).
-    // Its stream stB has a hardware queue of its own (created with a CU mask),
-    // so that no kernel it waits for can queue behind it.
-    DevBuf<uint32_t> bflags;              // per batch 4 words (TextArgs::bflags)
-    DevBuf<uint32_t> ctl;                 // [0]: abort the launch (set by an H2D copy on stE)
-    DevBuf<TextBatch> batchTab;
-    DevBuf<TextSlot> slotTab;
-    TextBatch* batchHost = nullptr;       // pinned staging of the tables
-    size_t batchHostCap = 0;
-    TextSlot* slotHost = nullptr;
-    uint32_t* hostDone = nullptr;         // pinned, per batch (TextArgs::hostDone)
-    size_t hostDoneCap = 0;
-    uint32_t* ctlHost = nullptr;          // pinned: the abort word's source (1)
-    hipEvent_t txStart = nullptr, txEnd = nullptr;  // around the pass's text launch
     std::vector<hipEvent_t> partEv;  // around the first batch's later seed launches (created on demand)
-    bool textOwnQueue = false;            // stB was created with its own hardware queue
     uint32_t* pinned = nullptr;           // host copies of the slots' small counters (8 u32 per batch)
     // two pinned staging chunks for handing hits to pageable host memory: the
     // DMA of one chunk overlaps the host copy out of the other (copyOut)
@@ -451,6 +433,10 @@ struct Ctx {
         std::vector<uint64_t> nFirst;
     } up;
     DevBuf<uint32_t> nList;
+    // the packed reads' N list last checked whole (strictly ascending): a
+    // stream processed shard by shard is checked once, not once per shard
+    const uint64_t* nPosChecked = nullptr;
+    uint64_t nCountChecked = 0;
     bool streaming = false;
     hipStream_t stE = nullptr, stF = nullptr;  // pattern upload; hit download (sink)
     // SAHARA_TIMING=2: timing events around each chunk's DMA (bytes, events)
@@ -550,12 +536,6 @@ struct Ctx {
                                  sl.textDone, sl.free, sl.textMid0, sl.textMid1})
                 if (e) (void)hipEventDestroy(e);
         if (pinned) (void)hipHostFree(pinned);
-        if (batchHost) (void)hipHostFree(batchHost);
-        if (slotHost) (void)hipHostFree(slotHost);
-        if (hostDone) (void)hipHostFree(hostDone);
-        if (ctlHost) (void)hipHostFree(ctlHost);
-        if (txStart) (void)hipEventDestroy(txStart);
-        if (txEnd) (void)hipEventDestroy(txEnd);
         if (nibHost) (void)hipHostFree(nibHost);
         for (void* p : outStage)
             if (p) (void)hipHostFree(p);
@@ -628,5 +608,6 @@ void run(Ctx* c, bool count);
 void runOne(Ctx* c, bool count);
 void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow);
 void growCap(uint32_t& cap, uint32_t seen);
+void initWorkCaps(Ctx* c, uint64_t maxBatch);
 
 }  // namespace sahara

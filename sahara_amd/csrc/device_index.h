@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -24,62 +25,39 @@ struct Error : std::runtime_error {
                                   "' at " __FILE__ ":" + std::to_string(__LINE__) + ": " #expr); \
     } while (0)
 
-// hipFree synchronizes the whole device. A pipelined pass's text launch waits
-// for work the host issues during the pass (search.hip kSearchText), so a
-// buffer that grows inside the pass (locate keys, the hit output) must not be
-// freed there: the free would wait for the launch and the launch for the host.
-// While any such pass runs, frees are deferred; the last pass to end does them.
-struct FreeDeferral {
-    std::mutex mu;
-    int active = 0;
-    std::vector<void*> list;
-};
-inline FreeDeferral& freeDeferral() {
-    static FreeDeferral* d = new FreeDeferral;  // never destroyed: frees may run after static destructors
-    return *d;
+// (test hook, SAHARA_TEST_HIGH_ADDR=1) every DevBuf starts at an address
+// whose low 32-bit word has bit 31 set, 2 GiB more allocated for the shift:
+// a kernel that rebuilds a 64-bit address from a sign-extended 32-bit half
+// (the round-5 fault) then faults or reads the wrong memory
+// in the GPU tests instead of depending on where the allocator puts things.
+inline bool highAddrHook() {
+    static const bool on = [] {
+        const char* e = std::getenv("SAHARA_TEST_HIGH_ADDR");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
 }
-inline void deviceFree(void* p) {
-    FreeDeferral& d = freeDeferral();
-    {
-        std::lock_guard<std::mutex> g(d.mu);
-        if (d.active) {
-            d.list.push_back(p);
-            return;
-        }
-    }
-    (void)hipFree(p);
-}
-struct DeferFrees {  // scope of a pass whose text launch outlives host calls
-    DeferFrees() {
-        FreeDeferral& d = freeDeferral();
-        std::lock_guard<std::mutex> g(d.mu);
-        ++d.active;
-    }
-    ~DeferFrees() {
-        FreeDeferral& d = freeDeferral();
-        std::vector<void*> drop;
-        {
-            std::lock_guard<std::mutex> g(d.mu);
-            if (--d.active == 0) drop.swap(d.list);
-        }
-        for (void* p : drop) (void)hipFree(p);
-    }
-    DeferFrees(const DeferFrees&) = delete;
-    DeferFrees& operator=(const DeferFrees&) = delete;
-};
 
 template <typename T>
 struct DevBuf {  // minimal owning device buffer that only ever grows
     T* ptr = nullptr;
     size_t cap = 0;
+    void* base = nullptr;  // the allocation (ptr, unless highAddrHook)
     void reserve(size_t n) {
         if (n <= cap) return;
         release();
-        if (n) SH_HIP(hipMalloc(&ptr, n * sizeof(T)));
+        if (n) {
+            const bool high = highAddrHook();
+            SH_HIP(hipMalloc(&base, n * sizeof(T) + (high ? (size_t)1 << 31 : 0)));
+            const uint32_t lo = (uint32_t)reinterpret_cast<uintptr_t>(base);
+            const size_t off = !high || (lo & 0x80000000u) ? 0 : (size_t)(0x80000000u - lo);
+            ptr = reinterpret_cast<T*>(static_cast<char*>(base) + off);
+        }
         cap = n;
     }
     void release() {
-        if (ptr) deviceFree(ptr);
+        if (base) (void)hipFree(base);
+        base = nullptr;
         ptr = nullptr;
         cap = 0;
     }
@@ -87,14 +65,16 @@ struct DevBuf {  // minimal owning device buffer that only ever grows
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), cap(o.cap) { o.ptr = nullptr; o.cap = 0; }
+    DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), cap(o.cap), base(o.base) { o.ptr = nullptr; o.cap = 0; o.base = nullptr; }
     DevBuf& operator=(DevBuf&& o) noexcept {
         if (this != &o) {
             release();
             ptr = o.ptr;
             cap = o.cap;
+            base = o.base;
             o.ptr = nullptr;
             o.cap = 0;
+            o.base = nullptr;
         }
         return *this;
     }
@@ -103,7 +83,7 @@ struct DevBuf {  // minimal owning device buffer that only ever grows
 // Text (and patterns) for the text phase as 3-bit-plane blocks: block i holds
 // symbols [32i, 32i+32) as {plane0, plane1, plane2, 0}, bit j of plane b =
 // bit b of symbol 32i+j. One 16-B load per 32 symbols, and per-symbol masks of
-// 32 symbols come out of 3 word operations (search.hip, kSearchText).
+// 32 symbols come out of 3 word operations (search.hip, kSearchTextBatch).
 constexpr uint64_t kTextPadBlocks = 4096;  // zero blocks after the text (text-phase windows)
 inline uint64_t text3Blocks(uint64_t n) { return (n + 31) / 32 + kTextPadBlocks; }
 

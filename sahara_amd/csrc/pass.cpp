@@ -18,7 +18,7 @@ namespace sahara {
 // One pass over the staged patterns in batches of <= 4M. Per batch:
 //   stream stD: chunk unpack (streamed upload), kSeedItems
 //   stream st : kSearchFM                    -> hits, tasks of its slot
-//   stream stB: kSearchText                  -> hits of its slot
+//   stream stB: kSearchTextBatch             -> hits of its slot
 //   stream stC: row counts + ranks, scan, locate, sort, decode
 //   stream stF: the batch's hits to the host sink (streamed calls)
 // Ctx::kSlots slots rotate, so the seeds and FM phase of later batches
@@ -82,7 +82,7 @@ void run(Ctx* c, bool count) {
                   &sahara_stats::conversions, &sahara_stats::fm_iterations, &sahara_stats::text_iterations,
                   &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
                   &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
-                  &sahara_stats::text_steps, &sahara_stats::text_launches, &sahara_stats::text_fallbacks,
+                  &sahara_stats::text_steps, &sahara_stats::text_launches,
                   &sahara_stats::text_pos_tasks, &sahara_stats::text_cycles_idle, &sahara_stats::text_cycles_grab,
                   &sahara_stats::text_cycles_life})
                 T.*f += S.*f;
@@ -121,14 +121,26 @@ void runOne(Ctx* c, bool count) {
     bool overflow = false;
     runPass(c, count, !c->pipeline, S, overflow);
     if (overflow) {
-        const uint64_t fallbacks = S.text_fallbacks;
         S = sahara_stats{};
-        S.text_fallbacks = fallbacks;
         runPass(c, count, true, S, overflow);
     }
     S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     S.stage_ms = c->stageMs;
     c->stats = S;
+}
+
+// The hit and task buffers' first sizes (SAHARA_HITCAP / SAHARA_TASKCAP in
+// tests), for batches of maxBatch patterns; a pass grows them on overflow.
+// sahara_gpu_prepare sizes them the same way.
+void initWorkCaps(Ctx* c, uint64_t maxBatch) {
+    if (c->hitCap == 0) {
+        c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (const char* e = std::getenv("SAHARA_HITCAP")) c->hitCap = (uint32_t)std::max(1L, std::atol(e));
+    }
+    if (c->taskCap == 0) {
+        c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
+        if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
+    }
 }
 
 void growCap(uint32_t& cap, uint32_t seen) {
@@ -227,23 +239,18 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool textFits = text3Blocks(c->I.n) * 16 <= 0xFFFFFF00ull &&
                           maxBatch * c->patBlocks * 16 <= 0xFFFFFF00ull;
     const int textShape = textShapeOf(winBlocks, c->patBlocks, exactWindow);
-    const char* olEnv = std::getenv("SAHARA_TEXT_ONE_LAUNCH");
-    const bool wantOneLaunch = !serial && olEnv && std::atoi(olEnv) == 1;
     if (c->verify && c->m <= 2047 && textLds <= 160 * 1024 && textFits)
-        tbpc = textBlocksPerCU(sigma, c->edit, count, textShape, textLds, wantOneLaunch);
+        tbpc = textBlocksPerCU(sigma, c->edit, count, textShape, textLds);
     // overlapped with the FM phase, three text workgroups per CU beside its one
     // (four would fit: r2 v8 measured text 4 against 3 in alternating pairs,
     // C3 914-943M vs 880-952M on one box and 873-914M vs 953-956M on another,
     // C2 950-1013M vs 956-1026M: the sign flips with the box)
     if (!serial && batchesHere > 1) tbpc = std::min(tbpc, 3);
-    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0) tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, count, textShape, textLds, wantOneLaunch), std::atoi(e)));
-    // (one launch) the text launch waits for the seed and FM kernels, which
-    // must fit beside its workgroups (count mode's kernels hold more VGPRs)
-    if (wantOneLaunch && tbpc > 0)
-        tbpc = textBlocksBeside(sigma, c->edit, count, textShape, textLds, lds, tbpc);
+    if (const char* e = std::getenv("SAHARA_TEXT_BPC"); e && tbpc > 0)
+        tbpc = std::max(1, std::min(textBlocksPerCU(sigma, c->edit, count, textShape, textLds), std::atoi(e)));
     if (std::getenv("SAHARA_DUMP_COUNTERS"))
         std::fprintf(stderr, "text geometry: shape %d lds %zu blocks/CU %d (alone %d) serial %d\n", textShape, textLds, tbpc,
-                     textBlocksPerCU(sigma, c->edit, count, textShape, textLds, wantOneLaunch), (int)serial);
+                     textBlocksPerCU(sigma, c->edit, count, textShape, textLds), (int)serial);
     const uint32_t split = tbpc > 0 ? c->split : 0u;
     // (pipelined) the first batch's text phase starts on its seed tasks while
     // its FM phase runs; a device-resident lone batch does not: its FM phase
@@ -260,24 +267,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const bool chunkSeeds = c->streaming && !serial && split && !(csEnv && std::atoi(csEnv) == 0);
     const bool early = !serial && split && (batchesHere > 1 || chunkSeeds);
     const bool chunked0 = early && chunkSeeds;
-    // (pipelined, SAHARA_TEXT_ONE_LAUNCH=1) the text phase of the whole pass
-    // as one launch that takes each batch's tasks as the seed and FM streams
-    // publish them (search.hip kSearchText), so no launch boundary falls
-    // between batches. Measured slower than one launch per batch
-    // (kSearchTextBatch, the default): DESIGN.md §9.
-    const bool oneLaunch = split && wantOneLaunch;
     const uint32_t textBlocks = (uint32_t)(c->numCU * std::max(tbpc, 1));
     S.text_grid = split ? textBlocks : 0u;
     S.pipelined = serial ? 0u : 1u;
 
-    if (c->hitCap == 0) {
-        c->hitCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
-        if (const char* e = std::getenv("SAHARA_HITCAP")) c->hitCap = (uint32_t)std::max(1L, std::atol(e));
-    }
-    if (c->taskCap == 0) {
-        c->taskCap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, 8 * maxBatch), 1u << 30);
-        if (const char* e = std::getenv("SAHARA_TASKCAP")) c->taskCap = (uint32_t)std::max(1L, std::atol(e));
-    }
+    initWorkCaps(c, maxBatch);
     // batch boundaries: equal batches of <= maxBatch patterns, or (pipelined,
     // SAHARA_RAMP / SAHARA_RAMP_END: lists of pattern counts, ',' or ':') given
     // first and last batches around equal middle ones
@@ -327,13 +321,10 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // chain (kCountRows) did it, beside the next batches' search, where the
     // chain lagged behind them: C3 805M -> 843M, C2 482M -> 503M, C5 94.2M ->
     // 95.6M reads/s (profiles/r04_emit_rank_ab.txt)
-    // Text hits are counted per query without a rank (TextSlot::tcnt, the
-    // second half of the slot's qcnt buffer) and placed by kLocate.
     for (auto& sl : c->slot) {
-        sl.qcnt.reserve(2 * (maxBatch + 1));
-        SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, 2 * (maxBatch + 1) * sizeof(uint32_t), c->st));
+        sl.qcnt.reserve(maxBatch + 1);
+        SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (maxBatch + 1) * sizeof(uint32_t), c->st));
     }
-    auto tcntOf = [&](Ctx::Slot& sl) { return sl.qcnt.ptr + maxBatch + 1; };
     hipStream_t sA = c->st, sB = serial ? c->st : c->stB, sC = serial ? c->st : c->stC, sD = serial ? c->st : c->stD;
     c->mark("pass", 0);
     SH_HIP(hipStreamSynchronize(c->st));
@@ -341,76 +332,19 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     SH_HIP(hipStreamSynchronize(c->stC));
     SH_HIP(hipStreamSynchronize(c->stD));
     c->mark("pass synced", 0);
-    const bool probe = std::getenv("SAHARA_DUMP_COUNTERS") != nullptr;  // (profiling hook)
-    if (count || probe) {
+    // (profiling hook, count mode) the first text launch's wave lives
+    const bool probe = count && std::getenv("SAHARA_DUMP_COUNTERS") != nullptr;
+    if (count) {
         SH_HIP(hipMemsetAsync(c->counters.ptr, 0, kCounters * sizeof(unsigned long long), sA));
         SH_HIP(hipMemsetAsync(c->counters.ptr + 33, 0xFF, sizeof(unsigned long long), sA));  // (minima)
         SH_HIP(hipMemsetAsync(c->counters.ptr + 37, 0xFF, sizeof(unsigned long long), sA));
         SH_HIP(hipMemsetAsync(c->counters.ptr + 38, 0xFF, sizeof(unsigned long long), sA));
-    }
-    if (oneLaunch) {  // the text launch's timeout report (search.hip kSearchText): count, max, min, max
-        SH_HIP(hipMemsetAsync(c->counters.ptr + 26, 0, 2 * sizeof(unsigned long long), sA));
-        SH_HIP(hipMemsetAsync(c->counters.ptr + 28, 0xFF, sizeof(unsigned long long), sA));
-        SH_HIP(hipMemsetAsync(c->counters.ptr + 29, 0, sizeof(unsigned long long), sA));
     }
     c->nout = 0;
     c->sinkDone = 0;
     c->sinkOk = c->sink != nullptr || c->blockRecs != nullptr;
     c->batchQ0.clear();
     c->batchEnd.clear();
-    // The one text launch's hand-off state: per batch 4 words (zero), the
-    // batch table, the host's done words; every slot's buffers are sized
-    // before the launch, so their addresses hold for the pass (the slot table).
-    const size_t usedSlots = (size_t)std::min<uint64_t>(nbatch, Ctx::kSlots);
-    uint64_t maxItems = 0;
-    for (uint64_t b = 0; b < nbatch; ++b) maxItems = std::max(maxItems, (bstart[b + 1] - bstart[b]) * c->nsearch);
-    for (size_t i = 0; i < (oneLaunch ? usedSlots : 0); ++i) {
-        Ctx::Slot& sl = c->slot[i];
-        sl.hits.reserve((size_t)c->hitCap + 1);
-        sl.rank.reserve((size_t)c->hitCap + 1);
-        sl.tasks.reserve((size_t)c->taskCap);
-        sl.seeds.reserve(maxItems);
-        sl.seedItem.reserve(maxItems);
-    }
-    auto writeSlotTable = [&](hipStream_t s) {
-        for (size_t i = 0; i < Ctx::kSlots; ++i) {
-            Ctx::Slot& sl = c->slot[i];
-            c->slotHost[i] = TextSlot{sl.tasks.ptr, sl.queues.ptr, sl.hits.ptr, sl.rank.ptr, sl.qcnt.ptr, tcntOf(sl),
-                                      sl.small.ptr};
-        }
-        SH_HIP(hipMemcpyAsync(c->slotTab.ptr, c->slotHost, Ctx::kSlots * sizeof(TextSlot), hipMemcpyHostToDevice, s));
-    };
-    if (oneLaunch) {
-        if (c->batchHostCap < nbatch + 1) {
-            if (c->batchHost) SH_HIP(hipHostFree(c->batchHost));
-            c->batchHost = nullptr;
-            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->batchHost), (nbatch + 1) * sizeof(TextBatch)));
-            c->batchHostCap = nbatch + 1;
-        }
-        if (c->hostDoneCap < nbatch) {
-            if (c->hostDone) SH_HIP(hipHostFree(c->hostDone));
-            c->hostDone = nullptr;
-            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hostDone), nbatch * sizeof(uint32_t)));
-            c->hostDoneCap = nbatch;
-        }
-        if (!c->slotHost) SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->slotHost), Ctx::kSlots * sizeof(TextSlot)));
-        if (!c->ctlHost) {
-            SH_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->ctlHost), 16));
-            c->ctlHost[0] = 1;
-        }
-        std::memset(c->hostDone, 0, nbatch * sizeof(uint32_t));
-        for (uint64_t b = 0; b <= nbatch; ++b)
-            c->batchHost[b] = b < nbatch ? TextBatch{bstart[b], (uint32_t)(bstart[b + 1] - bstart[b]), (uint32_t)(b % Ctx::kSlots)}
-                                         : TextBatch{bstart[nbatch], 0u, 0u};
-        c->bflags.reserve(nbatch * textFlagWords(textBlocks));
-        c->batchTab.reserve(nbatch + 1);
-        c->slotTab.reserve(Ctx::kSlots);
-        c->ctl.reserve(4);
-        SH_HIP(hipMemsetAsync(c->bflags.ptr, 0, nbatch * textFlagWords(textBlocks) * sizeof(uint32_t), sA));
-        SH_HIP(hipMemsetAsync(c->ctl.ptr, 0, 4 * sizeof(uint32_t), sA));
-        SH_HIP(hipMemcpyAsync(c->batchTab.ptr, c->batchHost, (nbatch + 1) * sizeof(TextBatch), hipMemcpyHostToDevice, sA));
-        writeSlotTable(sA);
-    }
     // a slot's counters and queues are zero when its `free` event fires:
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
@@ -420,15 +354,11 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     };
     for (auto& sl : c->slot) resetSlot(sl, sA);
 
-    // the batch's seed tasks are all written (stream sD): the one-launch text
-    // phase may start on them (published), the first batch's per-batch text
-    // phase launches on them (the count snapshot in small[5]) before its FM
-    // phase ends
-    auto seedTasksDone = [&](uint64_t b, Ctx::Slot& sl) {
-        if (oneLaunch)
-            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sD);
-        else
-            SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
+    // the batch's seed tasks are all written (stream sD): the first batch's
+    // text phase launches on them (the count snapshot in small[5]) before its
+    // FM phase ends
+    auto seedTasksDone = [&](Ctx::Slot& sl) {
+        SH_HIP(hipMemcpyAsync(sl.small.ptr + 5, sl.small.ptr + 4, 4, hipMemcpyDeviceToDevice, sD));
     };
     auto issueFM = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
@@ -521,7 +451,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             ensureUploaded(c, p1, sD);
             SH_HIP(hipEventRecord(sl.fmStart, sD));
             seeds(0, (uint32_t)(p1 * c->nsearch));
-            seedTasksDone(b, sl);
+            seedTasksDone(sl);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
             // each later part's seed launch timed on its own (not the upload waits between)
             uint32_t part = 0;
@@ -547,85 +477,24 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // the seed tasks end here: the text phase may start on them (a
             // lone device-resident batch's text phase waits for its FM phase:
             // published after it below)
-            if (split && early) seedTasksDone(b, sl);
+            if (split && early) seedTasksDone(sl);
             SH_HIP(hipEventRecord(sl.seedDone0, sD));
         }
         SH_HIP(hipEventRecord(sl.seedDone, sD));
         SH_HIP(hipStreamWaitEvent(sA, sl.seedDone, 0));
         SH_HIP(hipEventRecord(sl.fmBegin, sA));
         launchSearch(a, sigma, c->edit, count, b == 0 && !early ? firstBlocks : blocks, lds, sA);
-        if (split && oneLaunch) {  // the batch's task list is final
-            if (!early)
-                launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 0, textBlocks), textBlocks, sA);
-            launchPublish(sl.small.ptr + 4, c->taskCap, c->bflags.ptr + textFlag(b, 1, textBlocks), textBlocks, sA);
-        }
         SH_HIP(hipEventRecord(sl.fmDone, sA));
         ++S.search_launches;
     };
-    // The text phase. Pipelined: one launch for the whole pass, issued with
-    // batch 0 (after its first seed tasks are published, or after its FM
-    // phase for a lone device-resident batch, whose FM phase runs at full
-    // occupancy alone); every batch's tasks reach it through bflags, and the
-    // finisher learns a batch is done from hostDone. Serial (overflow re-runs,
-    // SAHARA_PIPELINE=0): one launch per batch after its FM phase, on the one
-    // stream. SAHARA_TEXT_ONE_LAUNCH=0: one launch per batch, pipelined.
-    bool textLaunched = false;
-    // the kernel's wall clock (s_memrealtime) counts at 100 MHz on gfx950
-    // (MI355X_MICROARCH.md); the device attribute reported another rate
-    constexpr uint64_t wallKHz = 100000;
     // in-wave work stealing while no task is in hand, once SAHARA_STEAL_AT
     // lanes of a wave are idle (0: off). Measured in one process, alternating:
     // C5 80.4M (off) -> 124.3M (1) / 129.5M (8) reads/s, lanes busy 0.656 ->
     // 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
     uint32_t stealAt = 8;
     if (const char* e = std::getenv("SAHARA_STEAL_AT")) stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-    auto launchTextRange = [&](uint64_t b0, uint64_t b1) {
-        TextArgs t{};
-        t.sa = c->I.saFull.ptr;
-        t.text3 = c->I.text3.ptr;
-        t.pats3 = c->pats3.ptr;
-        t.patBlocks = c->patBlocks;
-        t.text3Bytes = (uint32_t)std::min<uint64_t>(text3Blocks(c->I.n) * 16, 0xFFFFFF00ull);
-        t.m = c->m;
-        t.nsearch = c->nsearch;
-        t.table = reinterpret_cast<const uint2*>(c->cover.ptr);
-        t.batches = c->batchTab.ptr;
-        t.slots = c->slotTab.ptr;
-        t.b0 = (uint32_t)b0;
-        t.b1 = (uint32_t)b1;
-        t.bflags = c->bflags.ptr;
-        t.flagStride = (uint32_t)textFlagWords(textBlocks);
-        t.hostDone = c->hostDone;
-        t.ctl = c->ctl.ptr;
-        // an idle wave gives up after 2 s without published work (the host
-        // then redoes the pass batch by batch): no legitimate wait is that long
-        t.timeoutTicks = wallKHz * 2000;
-        t.pollGap = std::max<uint64_t>(1, wallKHz * 2 / 1000);  // 2 us
-        t.probe = probe ? 1u : 0u;
-        t.taskCap = c->taskCap;
-        t.hitCap = c->hitCap;
-        t.counters = c->counters.ptr;
-        t.winBlocks = winBlocks;
-        t.exactWindow = exactWindow ? 1u : 0u;
-        t.stackCap = textStack;
-        t.tableWords = tableWords;
-        t.steps = c->textSteps;
-        t.refillAt = c->refillAt;
-        t.stealAt = stealAt;
-        launchText(t, sigma, c->edit, count, textBlocks, textLds, sB);
-    };
     auto issueText = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
-        if (oneLaunch) {
-            if (b != 0) return;
-            SH_HIP(hipStreamWaitEvent(sB, early ? sl.seedDone0 : sl.fmDone, 0));
-            SH_HIP(hipEventRecord(c->txStart, sB));
-            launchTextRange(0, nbatch);
-            SH_HIP(hipEventRecord(c->txEnd, sB));
-            textLaunched = true;
-            ++S.text_launches;
-            return;
-        }
         // one launch per batch (kSearchTextBatch) after its FM phase; the
         // first batch of an early pass in two: its seed tasks while its FM
         // phase runs, then the tasks the FM phase appended after them
@@ -694,47 +563,13 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     if (const char* e = std::getenv("SAHARA_POLL_US")) pollUs = (uint32_t)std::max(0, std::atoi(e));
     unsigned long timerSlackNs = 1000;  // the finisher's timer slack (0: the process default)
     if (const char* e = std::getenv("SAHARA_TIMER_SLACK_NS")) timerSlackNs = (unsigned long)std::max(0L, std::atol(e));
-    // (one launch) the launch marks batch b done in pinned host memory; false
-    // if the launch ended without marking it (a wave gave up: the pass is redone)
-    bool textFailed = false;
-    auto waitTextDone = [&](uint64_t b) -> bool {
-        const volatile uint32_t* hd = c->hostDone + b;
-        for (uint32_t spin = 0;; ++spin) {
-            if (*hd) return true;
-            if (sleepy || (spin & 63u) == 0) {
-                const hipError_t r = hipEventQuery(c->txEnd);
-                if (r == hipSuccess) return *hd != 0;
-                if (r != hipErrorNotReady) SH_HIP(r);
-            }
-            if (sleepy && pollUs) std::this_thread::sleep_for(std::chrono::microseconds(pollUs));
-            else std::this_thread::yield();
-        }
-    };
     auto finish = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
         c->mark("finish", b);
         // the batch's counters, copied on sC (a copy on sB would wait for CU
         // slots between two text phases)
-        if (oneLaunch) {
-            if (!waitTextDone(b)) {
-                if (std::getenv("SAHARA_DEBUG_TEXT")) {
-                    unsigned long long h[kCounters];
-                    SH_HIP(hipMemcpy(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost));
-                    std::fprintf(stderr, "text launch gave up at batch %llu of %llu: timed-out waves %llu, "
-                                 "waited max (b*2+ph %llu, ready %llu) min (b*2+ph %llu, lo %llu), pub %llu/%llu; "
-                                 "host done:", (unsigned long long)b, (unsigned long long)nbatch, h[26], h[27] >> 32,
-                                 h[27] & 1, h[28] >> 32, h[28] & 0xFFFFFFFFull, h[29] >> 32, h[29] & 0xFFFFFFFFull);
-                    for (uint64_t i = 0; i < nbatch; ++i) std::fprintf(stderr, " %u", c->hostDone[i]);
-                    std::fprintf(stderr, "\n");
-                }
-                textFailed = true;
-                overflow = true;  // redone batch by batch
-                return false;
-            }
-        } else {
-            SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
-        }
+        SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
         SH_HIP(hipMemcpyAsync(c->pinned + b * 16, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
         SH_HIP(hipEventRecord(sleepy ? c->evSleep[0] : c->ev[6], sC));
         if (sleepy) waitSleepy(c->evSleep[0], pollUs);
@@ -754,16 +589,14 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         S.seed_ms += ms;
         SH_HIP(hipEventElapsedTime(&ms, sl.fmBegin, sl.fmDone));
         S.search_ms += ms;
-        if (!oneLaunch) {  // (one launch: its span, after the pass)
-            if (sl.twoText) {  // the two launches, not the wait for the FM phase between them
-                SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMid0));
-                S.text_ms += ms;
-                SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textDone));
-            } else {
-                SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
-            }
+        if (sl.twoText) {  // the two launches, not the wait for the FM phase between them
+            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textMid0));
             S.text_ms += ms;
+            SH_HIP(hipEventElapsedTime(&ms, sl.textMid1, sl.textDone));
+        } else {
+            SH_HIP(hipEventElapsedTime(&ms, sl.textStart, sl.textDone));
         }
+        S.text_ms += ms;
         if (hs[2] & 1u) throw Error("search stack overflow (internal bound violated)");
         if (hs[2] & 16u) throw Error("text phase: internal stack bound violated");
         if (hs[2] & (2u | 8u)) {  // hit or task buffer too small
@@ -773,7 +606,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             if (hs[2] & 2u) growCap(serial ? c->hitCap : seenHit, hs[1]);
             overflow = true;
             SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (nb + 1) * sizeof(uint32_t), sC));  // the re-run counts again
-            SH_HIP(hipMemsetAsync(tcntOf(sl), 0, (nb + 1) * sizeof(uint32_t), sC));
             resetSlot(sl, sC);
             return false;
         }
@@ -784,8 +616,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         SH_HIP(hipEventRecord(c->ev[2], sC));
         SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
         c->partial.reserve(scanTiles((uint32_t)nb));
-        querySegments(sl.qcnt.ptr, tcntOf(sl), (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4,
-                      c->huge.ptr, c->small.ptr + 5, sC);
+        querySegments(sl.qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4, c->huge.ptr,
+                      c->small.ptr + 5, sC);
         uint32_t* pr = c->pinned + b * 16;
         SH_HIP(hipMemcpyAsync(pr + 8, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
         SH_HIP(hipMemcpyAsync(pr + 10, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));  // long, huge segments
@@ -809,7 +641,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         la.nhits = nh;
         la.qoff = c->qoff.ptr;
         la.rank = sl.rank.ptr;
-        la.tcnt = oneLaunch ? tcntOf(sl) : nullptr;  // (one launch: text hits counted, not ranked)
         la.occF = c->I.occF.ptr;
         for (int i = 0; i < 8; ++i) la.C[i] = (uint32_t)c->I.C[i];
         la.samples = c->I.samples.ptr;
@@ -832,6 +663,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             SH_HIP(hipStreamSynchronize(c->stF));  // sink copies may still read the old buffer
             c->out.release();
             c->out.ptr = np;
+            c->out.base = np;
             c->out.cap = want;
         }
         sortDecode(c->k0.ptr, c->k1.ptr, rows, c->qoff.ptr, (uint32_t)nb, c->big.ptr, nbig, hugeList, nhuge, q0,
@@ -907,7 +739,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     };
 
     if (!serial) {
-        DeferFrees deferFrees;  // no device-wide sync while the text launch waits on this host
         // Two host threads. This one packs the queries of a streamed upload
         // and issues seeds, FM(b) and text(b) as soon as batch b's slot is
         // free; a finisher thread waits for each batch's text phase and
@@ -983,12 +814,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         cv.notify_all();
         finisher.join();
         c->mark("finisher joined", 0);
-        // a pass that stopped early: the text launch's waves end (they would
-        // otherwise wait for batches never issued until they time out)
-        if (textLaunched && (overflow || issueErr || finErr)) {
-            SH_HIP(hipMemcpyAsync(c->ctl.ptr, c->ctlHost, sizeof(uint32_t), hipMemcpyHostToDevice, c->stE));
-            SH_HIP(hipStreamSynchronize(c->stE));
-        }
         SH_HIP(hipStreamSynchronize(sA));
         SH_HIP(hipStreamSynchronize(sB));
         SH_HIP(hipStreamSynchronize(sC));
@@ -1000,12 +825,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         if (overflow) {
             c->taskCap = std::max(c->taskCap, seenTask);
             c->hitCap = std::max(c->hitCap, seenHit);
-            if (textFailed) ++S.text_fallbacks;
-        }
-        if (textLaunched && !overflow) {
-            float ms = 0;
-            SH_HIP(hipEventElapsedTime(&ms, c->txStart, c->txEnd));
-            S.text_ms += ms;
         }
         if (overflow) return;  // the caller redoes the pass serially with the grown buffers
     } else {
@@ -1024,7 +843,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         overflow = false;
         SH_HIP(hipStreamSynchronize(c->stF));
     }
-    if (probe && !count) {
+    if (probe) {
         unsigned long long h[kCounters];
         SH_HIP(hipMemcpy(h, c->counters.ptr, sizeof(h), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "text wave lives (first launch, us): last start %.1f first end %.1f last end %.1f mean %.1f; "
@@ -1032,8 +851,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                      (h[34] - h[33]) / 100.0, (h[37] - h[33]) / 100.0, (h[35] - h[33]) / 100.0,
                      h[36] / 100.0 / std::max<double>(1, S.text_grid * 4.0), (h[38] - h[33]) / 100.0,
                      (h[39] - h[33]) / 100.0, h[31], h[30] / 100.0 / std::max<double>(1, (double)h[31]));
-        std::fprintf(stderr, "text iterations before / after: %llu (busy lanes %.1f) / %llu (busy lanes %.1f); sleeps %llu steals %llu\n", h[40],
-                     h[41] / std::max(1.0, (double)h[40]), h[42], h[43] / std::max(1.0, (double)h[42]), h[44], h[45]);
+        std::fprintf(stderr, "text iterations before / after: %llu (busy lanes %.1f) / %llu (busy lanes %.1f); lanes stolen %llu\n",
+                     h[40], h[41] / std::max(1.0, (double)h[40]), h[42], h[43] / std::max(1.0, (double)h[42]), h[45]);
         std::fprintf(stderr, "text wall per iteration (us) before: refill %.2f steps+emit %.2f; after: refill %.2f steps+emit %.2f\n",
                      h[46] / 100.0 / std::max(1.0, (double)h[40]), h[47] / 100.0 / std::max(1.0, (double)h[40]),
                      h[48] / 100.0 / std::max(1.0, (double)h[42]), h[49] / 100.0 / std::max(1.0, (double)h[42]));

@@ -77,28 +77,10 @@ struct SeedArgs {
 // (left reads near the window start) stays inside the workgroup's LDS.
 constexpr uint32_t kTextTableMin = 3u * 256u;
 
-// One batch slot's buffers (Ctx::Slot) as the text phase sees them.
-struct TextSlot {
-    const uint4* tasks;      // text tasks (row, |t|, pattern, meta | search << 24)
-    uint32_t* queues;        // striped counters: [256, 512) the seed tasks, [512, 768) the FM phase's
-    uint4* hits;
-    uint32_t* rank;          // (the FM phase's ranks; text hits take theirs in kLocate)
-    uint32_t* qcnt;
-    uint32_t* tcnt;          // per-query text hit counts (non-returning adds; kLocate ranks them)
-    uint32_t* small;         // -, hitCount, flags, filled, taskCount, ...
-};
-// One batch of a pass (its patterns [q0, q0 + npat) of the staged ones).
-struct TextBatch {
-    uint64_t q0;
-    uint32_t npat;
-    uint32_t slot;
-};
 // work counters of count mode (sahara_stats): [0..15] as SearchArgs::counters
 // lists them, [16] text tasks that came with their text position (kTaskPos),
 // [17..19] text-kernel cycles idle / in grab / whole wave lives
 constexpr uint32_t kCounters = 56;
-// a published task count (kPublish): bit 31 set once the count is final for its phase
-constexpr uint32_t kTaskReady = 0x80000000u;
 // a task record whose x is already a text position (a k-mer seed with one
 // occurrence: DeviceIndex::kmerPos), not an SA row: bit 31 of its y (|t|)
 constexpr uint32_t kTaskPos = 0x80000000u;
@@ -136,44 +118,8 @@ struct TextBatchArgs {
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)
     uint32_t* qcnt;          // as SearchArgs: rows ranked where the hits are written (the FM phase's counts)
     uint32_t* rank;
-    uint32_t probe;          // (profiling) wave lives on the wall clock into counters [30..49] ...
+    uint32_t probe;          // (count mode) wave lives on the wall clock into counters [30..49] ...
     uint32_t isFirst;        // ... for the pass's first launch only
-};
-
-struct TextArgs {
-    const uint32_t* sa;      // full SA: task records carry SA rows, the kernel reads their text positions
-    const uint4* text3;      // text as 3-bit-plane blocks of 32 symbols (device_index.h)
-    const uint4* pats3;      // patterns of the pass as 3-bit-plane blocks, patBlocks per pattern
-    uint32_t patBlocks;
-    uint32_t text3Bytes;     // bytes of text3 (buffer-load bound; < 4 GiB; a batch's patterns likewise)
-    uint32_t m;
-    uint32_t nsearch;
-    const uint2* table;      // nsearch * m: {packScheme | run << 25, a | b << 12} (capi.cpp textTable)
-    // the batches [b0, b1) of the pass this launch serves (one launch per pass
-    // when pipelined, one per batch when serial; kSearchText's header comment)
-    const TextBatch* batches;  // b1 + 1 entries (the last one is never a batch of the launch)
-    const TextSlot* slots;
-    uint32_t b0, b1;
-    uint32_t* bflags;        // per batch flagStride words (textFlagWords): the seed tasks' count and then
-                             // all tasks' count | kTaskReady, each once per workgroup 16 words apart
-                             // (textFlag), then the workgroups past the batch; zero before the launch
-    uint32_t flagStride;
-    uint32_t* hostDone;      // pinned host memory, per batch: 1 once its text phase is done
-    const uint32_t* ctl;     // [0] != 0: the host aborts the pass
-    uint64_t timeoutTicks;   // an idle wave gives up after waiting this long (wall clock ticks)
-    uint64_t pollGap;        // a workgroup polls an unpublished task count at most once per this many ticks
-    uint32_t probe;          // (profiling) the first launch's wave lives on the wall clock into counters [33..37]
-    uint32_t taskCap;
-    uint32_t hitCap;
-    unsigned long long* counters;
-    uint32_t winBlocks;      // window blocks per lane (32 symbols each)
-    uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
-    uint32_t stackCap;       // text DFS stack entries per lane
-    uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)
-    uint32_t steps;          // node expansions per lane between wave-level bookkeeping
-    uint32_t refillAt;       // refill idle lanes once this many are idle
-    uint32_t stealAt;        // no task in hand: idle lanes take the bottom stack entry of a busy lane of
-                             // their wave (with its window and pattern) once this many are idle (0: off)
 };
 
 struct LocateArgs {
@@ -181,8 +127,6 @@ struct LocateArgs {
     uint64_t nhits;
     const uint64_t* qoff;          // per-query row segments (querySegments)
     const uint32_t* rank;          // per cursor: slot of its first row in the segment (querySegments)
-    uint32_t* tcnt;                // (one text launch) per query: its text hits still to place (the segment's
-                                   // tail), zero on return; nullptr: text hits ranked like FM cursors (rank)
     const OccLine* occF;
     uint32_t C[8];
     const uint32_t* samples;
@@ -195,24 +139,12 @@ struct LocateArgs {
 };
 
 int searchBlocksPerCU(uint32_t sigma, bool edit, size_t lds);
-int textBlocksPerCU(uint32_t sigma, bool edit, bool count, int shape, size_t lds, bool persistent);
-// text workgroups per CU (<= want) that leave room for an FM workgroup and a
-// locate-chain workgroup beside them (shape: the compile-time text shape, 0-2)
-int textBlocksBeside(uint32_t sigma, bool edit, bool count, int shape, size_t textLds, size_t fmLds, int want);
+int textBlocksPerCU(uint32_t sigma, bool edit, bool count, int shape, size_t lds);
 int textShapeOf(uint32_t winBlocks, uint32_t patBlocks, bool exactWindow);
-// the text phase of one batch (kSearchTextBatch): the product path
+// the text phase of one batch (kSearchTextBatch)
 void launchTextBatch(const TextBatchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
                      hipStream_t st);
-void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
-                hipStream_t st);
 void launchSeeds(const SeedArgs& a, uint32_t sigma, uint32_t blocks, hipStream_t st);
-// flag[16 w] = min(*count, cap) | kTaskReady for w < nwg, on stream st (the
-// text phase's hand-off: one copy per text workgroup)
-void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, uint32_t nwg, hipStream_t st);
-// the text phase's hand-off words per batch for a launch of nwg workgroups,
-// and where batch b's phase ph (0: seed tasks, 1: all) copies begin
-inline size_t textFlagWords(uint32_t nwg) { return 2 * (size_t)nwg * 16 + 32; }
-inline size_t textFlag(uint64_t b, uint32_t ph, uint32_t nwg) { return b * textFlagWords(nwg) + (size_t)ph * nwg * 16; }
 void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t patWords, uint32_t sigma,
                         uint32_t* dst, uint32_t* bad, hipStream_t st);
 // n symbols, two per byte of nib (low nibble first) -> one per byte of dst
@@ -248,11 +180,9 @@ void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, ui
 // radix sort).
 uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
 // qcnt: the batch's per-query row counts, which the search kernels add up
-// as they write the hits (SearchArgs::qcnt); all zero on return. tcnt: the
-// per-query text hit counts (TextSlot::tcnt), read only: a query's segment
-// holds qcnt + tcnt rows, its text hits the last tcnt (placed by kLocate)
-void querySegments(uint32_t* qcnt, const uint32_t* tcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
-                   uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st);
+// as they write the hits (SearchArgs::qcnt); all zero on return
+void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
+                   uint32_t* huge, uint32_t* nhuge, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
 size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
 // long segments (> 64 rows, listed in big) are sorted in LDS, huge ones

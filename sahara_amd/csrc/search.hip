@@ -16,7 +16,7 @@
 // interval holds at most `split` rows, the node is handed to phase 2 as one
 // *text task* per row instead of being ranked further.
 //
-// Phase 2, kSearchText: a text task is a node whose string t has a single
+// Phase 2, kSearchTextBatch: a text task is a node whose string t has a single
 // occurrence. Extending it by symbol c is non-empty iff c is the text's own
 // next symbol, so the rest of its subtree is the same DFS run against the
 // text. The lane copies the window of the 4-bit text that the subtree can
@@ -56,8 +56,6 @@
 namespace sahara {
 namespace {
 
-// Swap a dword with the neighbour lane of the pair (DPP quad_perm [1,0,3,2]).
-typedef __attribute__((address_space(1))) uint32_t GlobalU32;
 // Pointers that come from memory (the slot table), from integers (Occ line
 // addresses) or that may point to LDS or global memory (a stack level) are
 // generic: accesses through them are flat instructions, which also count
@@ -77,19 +75,8 @@ __device__ __forceinline__ uint4 loadGlobal4(const uint4* p) {
     const U32x4 v = *GLOB(const U32x4, p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-// a wave-uniform 64-bit value made scalar (readfirstlane returns an int: its
-// low half must not be sign-extended into the high one)
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ void storeGlobal4(uint4* p, const uint4& v) {
-    U32x4 w;
-    w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
-    *GLOB(U32x4, p) = w;
-}
 
+// Swap a dword with the neighbour lane of the pair (DPP quad_perm [1,0,3,2]).
 __device__ __forceinline__ uint32_t pairSwap(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
 }
@@ -115,21 +102,12 @@ __device__ __forceinline__ void fetchLinePair(uint64_t own, bool need, bool odd,
     const uint32_t half = odd ? 16u : 0u;
     uint4 r1 = make_uint4(0, 0, 0, 0), r2 = r1, r3 = r1, r4 = r1;
     if (needE) {
-#ifdef SAHARA_X_OCC_FLAT
-        r1 = *reinterpret_cast<const uint4*>(addrE + half);
-        r2 = *reinterpret_cast<const uint4*>(addrE + 32 + half);
-    }
-    if (needO) {
-        r3 = *reinterpret_cast<const uint4*>(addrO + half);
-        r4 = *reinterpret_cast<const uint4*>(addrO + 32 + half);
-#else
         r1 = loadGlobal4(reinterpret_cast<const uint4*>(addrE + half));
         r2 = loadGlobal4(reinterpret_cast<const uint4*>(addrE + 32 + half));
     }
     if (needO) {
         r3 = loadGlobal4(reinterpret_cast<const uint4*>(addrO + half));
         r4 = loadGlobal4(reinterpret_cast<const uint4*>(addrO + 32 + half));
-#endif
     }
     // even: r1 = E0, r2 = E2, r3 = O0, r4 = O2 ; odd: r1 = E1, r2 = E3, r3 = O1, r4 = O3
     const uint4 g1 = pairSwap4(odd ? r1 : r3);  // even <- E1, odd <- O0
@@ -155,10 +133,9 @@ __device__ __forceinline__ uint32_t pick5(const uint32_t v[5], uint32_t i) {
 __device__ __forceinline__ uint32_t nib(uint32_t word, uint32_t i) { return (word >> ((i & 7u) * 4u)) & 0xFu; }
 
 constexpr uint32_t kSeedChunk = 64;   // seeds a wave takes per atomic
-#ifndef SAHARA_X_TASK_CHUNK
-#define SAHARA_X_TASK_CHUNK 64
-#endif
-constexpr uint32_t kTaskChunk = SAHARA_X_TASK_CHUNK;  // text tasks a wave takes per atomic (<= 64)
+// text tasks a wave takes per atomic (<= 64; 64 / 32 / 16 measured 1088 / 1021 /
+// 891M reads/s at C3, profiles/r05_task_chunk_ab.txt)
+constexpr uint32_t kTaskChunk = 64;
 static_assert(kTaskChunk >= 1 && kTaskChunk <= 64, "a chunk's records sit one per lane");
 constexpr uint32_t kHitChunk = 64;    // hit / task slots a wave reserves per atomic
 
@@ -434,22 +411,12 @@ __global__ __launch_bounds__(256) void kSearchFM(SearchArgs a) {
     const uint32_t L = a.stackLevels;
     auto stackGet = [&](uint32_t d) -> uint4 {
         d = d >= L ? d - L : d;
-#ifdef SAHARA_X_FMSTACK_GLOBAL
-        if (d < ldsDepth) return lstk[d * 256u + threadIdx.x];
-        return loadGlobal4(stk + (size_t)(d - ldsDepth) * T);
-#else
         return d < ldsDepth ? lstk[d * 256u + threadIdx.x] : stk[(size_t)(d - ldsDepth) * T];
-#endif
     };
     auto stackPut = [&](uint32_t d, const uint4& v) {
         d = d >= L ? d - L : d;
-#ifdef SAHARA_X_FMSTACK_GLOBAL
-        if (d < ldsDepth) lstk[d * 256u + threadIdx.x] = v;
-        else storeGlobal4(stk + (size_t)(d - ldsDepth) * T, v);
-#else
         if (d < ldsDepth) lstk[d * 256u + threadIdx.x] = v;
         else stk[(size_t)(d - ldsDepth) * T] = v;
-#endif
     };
     // seeds (kSeedItems: starting cursor + item) arrive in chunks of 64, one
     // record per lane, prefetched a chunk ahead so a refill costs no memory trip
@@ -841,29 +808,15 @@ __host__ __device__ constexpr TextShape textShape(int shape) {
     return shape == 1 ? TextShape{4, 4, true} : shape == 2 ? TextShape{9, 8, false} : TextShape{0, 0, false};
 }
 
-typedef __attribute__((address_space(1))) uint64_t GlobalU64;
-#ifdef SAHARA_V_PLAIN
-__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) { *GLOB(uint32_t, p) = v; }
-__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) { *GLOB(uint4, p) = v; }
-#else
-__device__ __forceinline__ void storeThrough(uint32_t* p, uint32_t v) {
-    __hip_atomic_store((GlobalU32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void storeThrough(uint4* p, const uint4& v) {
-    GlobalU64* q = (GlobalU64*)p;
-    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#endif
 
-// ---- kSearchTextBatch: the text phase of one batch per launch (the product
-// path). Its tasks [*taskBegin, *taskCount) of the slot's list come from a
-// striped queue; a lane takes a task (text position, or SA row read here),
-// copies the window and pattern to LDS and runs the subtree's DFS against the
-// text; leaves are hits (qid, text position, e | kPosKnown) counted per query
-// in tcnt (kLocate places them). The persistent kSearchText below serves all
-// batches of a pass from one launch (SAHARA_TEXT_ONE_LAUNCH=1): measured
-// slower, kept as an option.
+// ---- kSearchTextBatch: the text phase of one batch per launch. Its tasks
+// [*taskBegin, *taskCount) of the slot's list come from a striped queue; a
+// lane takes a task (text position, or SA row read here), copies the window
+// and pattern to LDS and runs the subtree's DFS against the text; leaves are
+// hits (qid, text position, e | kPosKnown), each ranked in its query's
+// segment as it is written (kLocate places them). (Round 5's persistent
+// variant, one launch per pass, measured 2-3x slower and was removed in r6:
+// DESIGN.md §3.4.)
 template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
 __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
     extern __shared__ uint32_t lds[];
@@ -928,16 +881,11 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
     uint32_t rankSlot = ~0u, rankVal = 0;  // the lane's last hit whose rank is not stored yet
     uint2 cur = make_uint2(0, 0);
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
-    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0;
-    // (profiling, a.probe) the first batch's wave lives on the wall clock, as
-    // kSearchText's probe: the queue seen drained, iterations before / after
-    // Compiled in only with -DSAHARA_X_BATCH_PROBE (tools/build_variant.sh):
-    // it costs the product kernel 14 VGPRs and 12 SGPR spills.
-#ifdef SAHARA_X_BATCH_PROBE
-    constexpr bool kProbe = true;
-#else
-    constexpr bool kProbe = false;
-#endif
+    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0, cSteal = 0;
+    // (count mode, a.probe) the first launch's wave lives on the wall clock:
+    // the queue seen drained, iterations and busy lanes before / after it.
+    // Only in count mode: it costs the product kernel 14 VGPRs and 12 SGPR spills.
+    constexpr bool kProbe = COUNT;
     __shared__ uint64_t wBorn[4], wDrain[4];
     if (kProbe && a.probe && lane == 0) wBorn[threadIdx.x >> 6] = wall_clock64(), wDrain[threadIdx.x >> 6] = 0;
     uint32_t pIterPre = 0, pIterPost = 0, pActPre = 0, pActPost = 0;
@@ -1051,6 +999,7 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
                     wb = dWb;
                     sBase = dBase;
                     have = true;
+                    if (COUNT) ++cSteal;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -1328,828 +1277,8 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
         }
         atomicAdd(a.counters + 14, (unsigned long long)cCmp);
         atomicAdd(a.counters + 15, (unsigned long long)cSteps);
+        if (cSteal) atomicAdd(a.counters + 45, (unsigned long long)cSteal);
     }
-}
-
-// ---- the text phase of a whole pass in one launch (r5)
-//
-// One launch serves the batches [b0, b1) of a pass, so the text phase has no
-// launch boundary (and no grid drain and refill) between batches. A batch's
-// task list fills in two steps: the tasks kSeedItems writes (their count
-// published by kPublish on the seed stream: textFlag(b, 0)), then the tasks
-// the FM phase appends (the final count, textFlag(b, 1), published after
-// kSearchFM; each count is written once per workgroup, 64 B apart, so that
-// every workgroup polls a line of its own: a few hundred pollers of one word
-// slowed every kernel beside them 2-3x). A wave's queue walks the batches in
-// order, phase by phase, taking
-// 64-task chunks from the phase's striped counters. The lanes of one wave hold
-// tasks of at most two consecutive batches (a lane's batch parity: `lpar`),
-// each with its own hit range: the queue moves on from batch qb only once the
-// wave holds nothing of qb - 1 any more.
-//
-// Retiring batch b (the wave holds nothing of it and its queue has moved past
-// it): the wave closes its hit range, stores its deferred ranks and releases
-// its writes (agent scope), then arrives at the workgroup's counter of b in
-// LDS; the workgroup's last wave adds one to the batch's arrival counter, and the workgroup
-// whose add completes the grid tells the host (hostDone[b] = 1, a system-scope
-// store to pinned memory), which starts the batch's locate chain and later
-// reuses the batch's slot: every wave has passed the batch by then, so none
-// reads its task list or queue counters again. Waves may drift apart by up to
-// four batches (a slot is reused five batches on, after its batch is done), so
-// the LDS counters are a ring of eight. A wave with nothing to do and nothing published
-// sleeps; it ends when the host aborts the pass (ctl[0]) or after waiting
-// timeoutTicks (wall clock) — the host then finds the launch ended with a
-// batch not done and redoes the pass one batch at a time (pass.cpp).
-__device__ __forceinline__ uint32_t pollWord(const uint32_t* p) {  // relaxed, agent scope: an sc1 load
-    return __hip_atomic_load((GlobalU32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// What the text kernel hands to the locate chain while it keeps running (hit
-// records, ranks) is stored write-through (sc1: relaxed agent-scope stores),
-// so that a wave only waits for its stores (vmcnt) before it reports a batch
-// done: a release fence there (buffer_wbl2) wrote back the whole L2 of its
-// XCD at every wave's every batch, dirty lines of every other kernel included,
-// and slowed everything beside the text phase 3-10x.
-
-// Four waves per SIMD (<= 128 VGPRs): four workgroups per CU alone, three
-// beside an FM workgroup. Left to itself the compiler took 142-166 VGPRs
-// (three and two); held to 128 it spills a few values of the refill path
-// (none in the micro-step loop). Count mode's instrumentation is not held.
-template <int SIGMA, bool EDIT, bool COUNT, int SHAPE = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : 4))) void kSearchText(TextArgs a) {
-    extern __shared__ uint32_t lds[];
-    __shared__ uint32_t arrive[8];  // waves of this workgroup past batch b, at b % 8
-    // published task counts this workgroup has seen ([b % 8][phase], tagged
-    // with b), and when one of its waves last polled one: a wave that finds
-    // its phase unpublished here polls global memory only if no wave of the
-    // workgroup did in the last kPollGap (a few hundred pollers of one word
-    // otherwise slow every kernel beside them)
-    __shared__ uint32_t pubTag[8][2], pubVal[8][2];
-    __shared__ uint64_t lastPoll;
-    __shared__ uint32_t abortSeen;  // the host's abort, as wave 0 of the workgroup last polled it
-    uint2* SC = reinterpret_cast<uint2*>(lds);
-    uint32_t* slot = lds + a.tableWords;  // >= kTextTableMin: the window's block -1 stays in LDS
-    for (uint32_t i = threadIdx.x; i < a.nsearch * a.m; i += blockDim.x) SC[i] = a.table[i];
-    if (threadIdx.x < 8) {
-        arrive[threadIdx.x] = 0;
-        pubTag[threadIdx.x][0] = pubTag[threadIdx.x][1] = ~0u;
-    }
-    if (threadIdx.x == 0) lastPoll = 0, abortSeen = 0;
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t ltMask = (1ull << lane) - 1ull;
-    constexpr TextShape kShape = textShape(SHAPE);
-    const uint32_t winBlocks = SHAPE ? kShape.win : a.winBlocks, patBlocks = SHAPE ? kShape.pat : a.patBlocks;
-    const bool exactWindow = SHAPE ? kShape.exact : a.exactWindow != 0u;
-    uint32_t* W = slot + threadIdx.x;
-    uint32_t* P = slot + 3u * winBlocks * 256u + threadIdx.x;
-    uint2* S = reinterpret_cast<uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u) + threadIdx.x;
-    auto stackGet = [&](uint32_t d) -> uint2 { return S[d * 256u]; };
-    auto stackPut = [&](uint32_t d, const uint2& v) { S[d * 256u] = v; };
-    const uint32_t winLen = winBlocks * 32u;
-    const __amdgpu_buffer_rsrc_t textBuf = bufferOf(a.text3, a.text3Bytes);
-    const uint32_t m = a.m;
-    const uint32_t patBytes = patBlocks * 16u;
-    // patterns of the batches the wave holds, by batch parity (pattern ids in
-    // task records are batch-local): read from the batch table when the queue
-    // reaches a batch, so that a chunk switch does not wait for the table
-    const uint4 *patP0 = nullptr, *patP1 = nullptr;
-    uint32_t patN0 = 0, patN1 = 0;
-    // (wave-uniform values read from memory: made scalar, or the compiler
-    // guards every pattern load with a loop over the lanes' distinct buffers)
-    auto loadPats = [&](uint32_t b) __attribute__((always_inline)) {
-        const TextBatch B = a.batches[b];
-        const uint64_t q0 = uniform64(B.q0);
-        const uint32_t n = __builtin_amdgcn_readfirstlane(B.npat) * patBytes;
-        if (b & 1u) { patP1 = a.pats3 + q0 * patBlocks; patN1 = n; }
-        else { patP0 = a.pats3 + q0 * patBlocks; patN0 = n; }
-    };
-    loadPats(a.b0);
-    // the pattern buffer of batch b, built from scalars where it is used: a
-    // buffer descriptor the compiler holds in vector registers (a value
-    // assigned on a path it cannot prove uniform) makes it wrap every load in
-    // a loop over the lanes' distinct descriptors
-    auto patBufOf = [&](uint32_t b) __attribute__((always_inline)) {
-        const bool odd = (__builtin_amdgcn_readfirstlane(b) & 1u) != 0u;
-        const uint64_t ptr = (uint64_t)(odd ? patP1 : patP0);
-        const uint64_t p = uniform64(ptr);
-        return bufferOf(reinterpret_cast<const void*>(p), __builtin_amdgcn_readfirstlane(odd ? patN1 : patN0));
-    };
-    // the slot buffers of the (at most two) batches the wave holds, by batch
-    // parity: loaded when the queue reaches a batch, so emission and retire
-    // read registers, not the tables
-    TextSlot slotP0 = a.slots[a.batches[a.b0].slot], slotP1 = slotP0;  // (the other parity: when qb moves)
-    // field by field, so that the structs stay in registers (a reference
-    // chosen at run time would put them in scratch memory)
-    auto slotFor = [&](uint32_t p) __attribute__((always_inline)) {
-        TextSlot r;
-        r.tasks = p ? slotP1.tasks : slotP0.tasks;
-        r.queues = p ? slotP1.queues : slotP0.queues;
-        r.hits = p ? slotP1.hits : slotP0.hits;
-        r.rank = p ? slotP1.rank : slotP0.rank;
-        r.qcnt = p ? slotP1.qcnt : slotP0.qcnt;
-        r.tcnt = p ? slotP1.tcnt : slotP0.tcnt;
-        r.small = p ? slotP1.small : slotP0.small;
-        return r;
-    };
-
-    // ---- the wave's place in the pass (wave-uniform)
-    uint32_t qb = a.b0, qph = 0, lo = a.b0;  // the queue's batch and phase; the oldest batch the wave holds
-    bool qReady = false;                      // (qb, qph)'s range is published and `queue` covers it
-    uint32_t qLo = 0, qSnap = 0;              // first task of the phase; the seed tasks of qb
-    uint32_t hn0 = 0, he0 = 0, hn1 = 0, he1 = 0;  // hit slot range [next, end) of the batch of parity 0 / 1
-    uint32_t* qCtr = nullptr;                 // the phase's striped counters (StripedQueue, unrolled
-    uint32_t qN = 0, qStripe = 0, qTries = 0; // into plain values: they stay in registers)
-    const uint4* qTasks = nullptr;
-
-    uint32_t sp = 0, pid = 0, wb = 0, sBase = 0, lpar = 0;
-    bool have = false, bad = false;
-    uint32_t qNext = 0, qEnd = 0, filled0 = 0, filled1 = 0;
-    // task chunks: the current one's records (one per lane) and the next one's,
-    // prefetched a chunk ahead so a refill needs no dependent task read; each
-    // with its batch (cBat, nBat) and the current one's pattern buffer
-    uint4 curRec = make_uint4(0, 0, 0, 0), nextRec = curRec;
-    uint32_t nBase = 0, nEnd = 0, qBase = 0, cBat = a.b0, nBat = a.b0;
-    bool haveNext = false;
-    // The prefetched chunk's records still hold SA rows. Their text positions
-    // are read at the next refill, beside its window loads (one round trip for
-    // both), or at the latest when the chunk becomes current.
-    bool nextRaw = false;
-    auto resolveNext = [&]() {
-        if (nextRaw) {  // wave-uniform
-            if (nBase + lane < nEnd && !(nextRec.y & kTaskPos)) nextRec.x = a.sa[nextRec.x];
-            nextRaw = false;
-        }
-    };
-    // Next chunk into `next`: 1 got one; 0 none yet (nothing published, or the
-    // wave must retire batch qb - 1 first); 2 the pass's tasks are all taken.
-    // Wave-uniform.
-    auto grab = [&]() __attribute__((always_inline)) -> uint32_t {
-        for (;;) {
-            if (qb >= a.b1) return 2u;
-            if (!qReady) {
-                uint32_t f = 0;
-                if (lane == 0) {
-                    const uint32_t r = qb & 7u;
-                    if (pubTag[r][qph] == qb) {
-                        f = pubVal[r][qph];
-                    } else {
-                        const uint64_t now = wall_clock64();
-                        if (now - lastPoll >= a.pollGap) {
-                            lastPoll = now;
-                            f = pollWord(a.bflags + (size_t)qb * a.flagStride + (qph * gridDim.x + blockIdx.x) * 16u);
-                            if (f & kTaskReady) {
-                                pubVal[r][qph] = f;
-                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                                pubTag[r][qph] = qb;
-                            }
-                        }
-                    }
-                }
-                f = __builtin_amdgcn_readfirstlane(f);
-                if (!(f & kTaskReady)) return 0u;
-#ifndef SAHARA_V_NOACQ
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // then the task records
-#endif
-                const uint32_t cnt = min(f & ~kTaskReady, a.taskCap);
-                const TextSlot Sl = slotFor(qb & 1u);
-                if (qph == 0) qSnap = cnt;
-                qLo = qph == 0 ? 0u : min(qSnap, cnt);
-                qCtr = Sl.queues + 256u * (1u + qph);
-                qN = cnt - qLo;
-                qStripe = blockIdx.x % kStripes;
-                qTries = 0;
-                qTasks = Sl.tasks;
-                qReady = true;
-            }
-            uint32_t b = 0, e = 0;
-            bool got = false;
-            while (qTries < kStripes) {  // StripedQueue::next
-                const uint32_t s0 = (uint32_t)((uint64_t)qN * qStripe / kStripes);
-                const uint32_t s1 = (uint32_t)((uint64_t)qN * (qStripe + 1) / kStripes);
-                uint32_t off = 0;
-                if (lane == 0)
-                    off = s0 < s1 ? __hip_atomic_fetch_add(GLOB(uint32_t, qCtr + qStripe * kStripeStride), kTaskChunk,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0xFFFFFFFFu;
-                off = __builtin_amdgcn_readfirstlane(off);
-                if (off != 0xFFFFFFFFu && off < s1 - s0) {
-                    b = s0 + off;
-                    e = min(b + kTaskChunk, s1);
-                    got = true;
-                    break;
-                }
-                qStripe = (qStripe + 1) % kStripes;
-                ++qTries;
-            }
-            if (got) {
-                nBase = qLo + b;
-                nEnd = qLo + e;
-                nBat = qb;
-                nextRec = make_uint4(0, 0, 0, 0);
-                if (nBase + lane < nEnd) {
-#if defined(SAHARA_X_LD_FLAT)
-                    nextRec = qTasks[nBase + lane];
-#elif defined(SAHARA_X_LD_BUF)
-                    const U32x4 v = __builtin_bit_cast(U32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                        bufferOf(qTasks, 0xFFFFFFF0u), (nBase + lane) * 16u, 0, 0));
-                    nextRec = make_uint4(v.x, v.y, v.z, v.w);
-#elif defined(SAHARA_X_LD_2X8)
-                    const uint64_t* q = reinterpret_cast<const uint64_t*>(qTasks + nBase + lane);
-                    const uint64_t lo8 = *GLOB(const uint64_t, q), hi8 = *GLOB(const uint64_t, q + 1);
-                    nextRec = make_uint4((uint32_t)lo8, (uint32_t)(lo8 >> 32), (uint32_t)hi8, (uint32_t)(hi8 >> 32));
-#else
-                    nextRec = loadGlobal4(qTasks + nBase + lane);
-#endif
-                }
-                haveNext = true;
-                nextRaw = true;
-                return 1u;
-            }
-            if (qph == 0) {
-                qph = 1;
-                qReady = false;
-                continue;
-            }
-            if (lo != qb) return 0u;  // at most two batches in flight per wave
-            ++qb;
-            qph = 0;
-            qReady = false;
-            if (qb < a.b1) {
-                loadPats(qb);
-                const TextSlot t = a.slots[a.batches[qb].slot];
-                if (qb & 1u) {
-                    slotP1.tasks = t.tasks; slotP1.queues = t.queues; slotP1.hits = t.hits;
-                    slotP1.rank = t.rank; slotP1.qcnt = t.qcnt; slotP1.tcnt = t.tcnt; slotP1.small = t.small;
-                } else {
-                    slotP0.tasks = t.tasks; slotP0.queues = t.queues; slotP0.hits = t.hits;
-                    slotP0.rank = t.rank; slotP0.qcnt = t.qcnt; slotP0.tcnt = t.tcnt; slotP0.small = t.small;
-                }
-            }
-        }
-    };
-    // This wave is past batch b: hit range closed, writes
-    // released, arrival counted. Wave-uniform, all lanes active.
-    auto retire = [&](uint32_t b) __attribute__((always_inline)) {
-        const uint32_t p = b & 1u;
-        const TextSlot Sl = slotFor(p);
-        // the unused tail of the hit range: empty records (len 0) for the locate scan
-        const uint32_t hn = p ? hn1 : hn0, he = p ? he1 : he0;
-        for (uint32_t i = hn + lane; i < he; i += 64)
-            if (i < a.hitCap) storeThrough(Sl.hits + i, make_uint4(0u, 0u, 0u, 0u));
-        if (p) hn1 = he1 = 0;
-        else hn0 = he0 = 0;
-        const uint32_t fl = p ? filled1 : filled0;
-        if (fl) __hip_atomic_fetch_add(GLOB(uint32_t, Sl.small + 3), fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (p) filled1 = 0;
-        else filled0 = 0;
-        if (__any(bad) && lane == 0)
-            __hip_atomic_fetch_or(GLOB(uint32_t, Sl.small + 2), 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // the wave's hits and ranks (stored write-through) and counts reach
-        // memory before it arrives
-#ifndef SAHARA_V_NORETWAIT
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-        if (lane == 0) {
-            const uint32_t k = __hip_atomic_fetch_add(arrive + (b & 7u), 1u, __ATOMIC_ACQ_REL,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (k + 1u == blockDim.x / 64u) {  // the workgroup's last wave
-                arrive[b & 7u] = 0;
-                const uint32_t g = __hip_atomic_fetch_add((GlobalU32*)(a.bflags + (size_t)b * a.flagStride +
-                                                                       2u * gridDim.x * 16u), 1u,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (g + 1u == gridDim.x) __hip_atomic_store(a.hostDone + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-    };
-    uint32_t pollSkip = 0;  // busy waves poll an unpublished phase every few iterations only
-    uint64_t waitStart = 0;
-    uint32_t idleSpins = 0;
-    bool waiting = false;
-    uint2 cur = make_uint2(0, 0);
-    uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
-    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0, cyIdle = 0, cyGrab = 0, cyStart = 0, cySteal = 0,
-             cyRetire = 0, cyResolve = 0, cySwitch = 0, nGrab = 0, cyShfl = 0, cyTail = 0, cyTop = 0;
-    const uint64_t tBorn = COUNT ? clock64() : 0;
-    __shared__ uint64_t wBorn[4], wDrain[4];
-    uint32_t pIterPre = 0, pIterPost = 0, pActPre = 0, pActPost = 0, pSleeps = 0, pSteals = 0;
-    uint64_t pwPreA = 0, pwPreB = 0, pwPostA = 0, pwPostB = 0;
-    if (a.probe && lane == 0) wBorn[threadIdx.x >> 6] = wall_clock64(), wDrain[threadIdx.x >> 6] = 0;
-
-    for (;;) {
-        const uint64_t pw0 = a.probe ? wall_clock64() : 0;
-        // Starting a task costs a global round trip (window + pattern) that
-        // stalls the whole wave, so idle lanes are refilled in batches: once
-        // refillAt lanes are idle (or nothing else is left).
-        if (COUNT) t0 = clock64();
-        const bool idle = !have && sp == 0;
-        const uint64_t idleMask = __ballot(idle);
-        const bool busy = idleMask != ~0ull;
-        const bool refill = !busy || __popcll(idleMask) >= a.refillAt;
-        uint64_t pending = refill ? idleMask : 0ull;
-        if (COUNT) { const uint64_t r0 = clock64(); cyTop += r0 - t0; if (pending) resolveNext(); cyResolve += clock64() - r0; }
-        else if (pending) resolveNext();
-        bool dry = false, tried = false;  // no task in hand for an idle lane; grab() tried this refill
-        for (;;) {  // wave-uniform
-            // (re)fill the prefetched chunk: at most two chunks serve one
-            // refill (64 tasks each, <= 64 idle lanes). One call site, so
-            // that the prefetched records have one home register; a busy wave
-            // polls an unpublished phase every few iterations only
-            if (!haveNext && !tried && (pending || refill)) {
-                tried = true;
-                if (busy && pollSkip) {
-                    --pollSkip;
-                } else {
-                    const uint64_t g0 = COUNT ? clock64() : 0;
-                    const uint32_t got = grab();
-                    if (got != 1u) pollSkip = 8;
-                    if (a.probe && got == 2u && lane == 0 && wDrain[threadIdx.x >> 6] == 0)
-                        wDrain[threadIdx.x >> 6] = wall_clock64();
-                    if (COUNT) { cyGrab += clock64() - g0; ++nGrab; }
-                }
-            }
-            if (!pending) break;
-            if (qNext >= qEnd) {  // switch to the prefetched chunk
-                if (!haveNext) {
-                    dry = true;
-                    break;
-                }
-                const uint64_t w0 = COUNT ? clock64() : 0;
-                resolveNext();
-                qBase = nBase;
-                qNext = nBase;
-                qEnd = nEnd;
-                curRec = nextRec;
-                cBat = nBat;
-                haveNext = false;
-                tried = false;
-                if (COUNT) cySwitch += clock64() - w0;
-                continue;
-            }
-            const uint64_t h0 = COUNT ? clock64() : 0;
-            const uint32_t take = min(qEnd - qNext, (uint32_t)__popcll(pending));
-            const uint32_t rank = (uint32_t)__popcll(pending & ltMask);
-            const bool mine = ((pending >> lane) & 1ull) && rank < take;
-            // the chunk's task records sit one per lane: fetch ours by shuffle
-            const uint32_t srcLane = (qNext - qBase + rank) & 63u;
-            const uint4 t = make_uint4(__shfl(curRec.x, srcLane), __shfl(curRec.y, srcLane),
-                                       __shfl(curRec.z, srcLane), __shfl(curRec.w, srcLane));
-            const uint64_t s0 = COUNT ? clock64() : 0;
-            if (COUNT) cyShfl += s0 - h0;
-            const __amdgpu_buffer_rsrc_t patBuf = patBufOf(cBat);
-            if (mine && t.y != 0u) {  // |t| = 0: an unused reserved slot (SlotRange::close)
-                // ---- start a task (x = its text position): copy the pattern
-                // and the text window its subtree can reach
-                const uint32_t x = t.x;
-                pid = t.z;
-                lpar = cBat & 1u;
-                sBase = (t.w >> 24) * m;
-                const uint32_t meta = t.w & 0x00FFFFFFu;
-                const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
-                const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
-                const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
-                const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
-                wb = x > left ? x - left : 0u;  // window start
-                if (exactWindow) {              // at wb: m + 2k symbols fit in winBlocks blocks
-                    copyBlocksShifted(W, textBuf, (wb >> 5) * 16u, wb & 31u, winBlocks, P, patBuf,
-                                      pid * patBytes, patBlocks);
-                } else {                        // at the block start below wb (31 more symbols)
-                    wb &= ~31u;
-                    copyBlocks(W, textBuf, (wb >> 5) * 16u, winBlocks, P, patBuf, pid * patBytes, patBlocks);
-                }
-                cur = make_uint2((x - wb) | ((x + (t.y & 0xFFFFu) - wb) << 16), meta);
-                have = true;
-            }
-            pending &= ~__ballot(mine);
-            qNext += take;
-            if (COUNT) cyStart += clock64() - s0;
-        }
-        const uint64_t e0 = COUNT ? clock64() : 0;
-        if (!dry) dry = qNext >= qEnd && !haveNext;
-        // ---- retire the older batch once the wave holds nothing of it
-        bool retired = false;
-        if (lo != qb) {
-            const uint32_t p = lo & 1u;
-            const bool held = __any((have || sp > 0u) && lpar == p) || (cBat == lo && qNext < qEnd) ||
-                              (haveNext && nBat == lo);
-            if (!held) {
-                const uint64_t r0 = COUNT ? clock64() : 0;
-                retire(lo);
-                if (COUNT) cyRetire += clock64() - r0;
-                ++lo;
-                retired = true;
-            }
-        }
-        // ---- work stealing inside the wave while no task is in hand (wave-
-        // uniform: the queue state is the wave's). A batch's tasks end on its
-        // longest subtrees, each on one lane while the others idle (C5: lanes
-        // busy 0.655 of the time); an idle lane takes the bottom (shallowest, so
-        // largest) stack entry of a busy lane, with that lane's window and
-        // pattern copied slot to slot in LDS, and the task state (pattern id,
-        // window start, scheme row, batch parity) by shuffle. The DFS of the
-        // entry is the same whichever lane runs it, so the hits are too.
-        const uint64_t st0 = COUNT ? clock64() : 0;
-#ifdef SAHARA_X_NOSTEAL
-        if (false) {
-#else
-        if (a.stealAt && dry) {
-#endif
-            const bool thief = !have && sp == 0u;
-            const uint64_t I = __ballot(thief);
-            const uint64_t D = __ballot(sp >= 2u || (sp == 1u && have));
-            const uint32_t nI = (uint32_t)__popcll(I), nD = (uint32_t)__popcll(D);
-            if (nI >= a.stealAt && nD) {  // wave-uniform
-                const uint32_t n = min(nI, nD);
-                const uint32_t r = (uint32_t)__popcll(I & ltMask);
-                // donor of thief rank r: the r-th set bit of D
-                uint32_t donor = 0, rr = r;
-                uint64_t dm = D;
-#pragma unroll
-                for (uint32_t w = 32; w; w >>= 1) {
-                    const uint32_t c = (uint32_t)__popcll(dm & ((1ull << w) - 1ull));
-                    if (rr >= c) { rr -= c; dm >>= w; donor += w; }
-                }
-                if (a.probe) ++pSteals;
-                const bool takes = thief && r < n;
-                donor = takes ? donor : lane;
-                const uint32_t dPid = __shfl(pid, donor), dWb = __shfl(wb, donor), dBase = __shfl(sBase, donor);
-                const uint32_t dPar = __shfl(lpar, donor);
-                const uint32_t dTid = (threadIdx.x & ~63u) | donor;
-                if (takes) {
-                    const uint32_t* src = slot + dTid;
-                    uint32_t* dst = slot + threadIdx.x;
-                    for (uint32_t k = 0; k < 3u * (winBlocks + patBlocks); ++k) dst[k * 256u] = src[k * 256u];
-                    const uint2 node = reinterpret_cast<const uint2*>(slot + 3u * (winBlocks + patBlocks) * 256u)[dTid];
-                    cur = node;
-                    pid = dPid;
-                    wb = dWb;
-                    sBase = dBase;
-                    lpar = dPar;
-                    have = true;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                // donors (rank < n) drop their bottom entry
-                const bool gives = ((D >> lane) & 1ull) && (uint32_t)__popcll(D & ltMask) < n;
-                if (gives) {
-                    for (uint32_t d = 1; d < sp; ++d) stackPut(d - 1u, stackGet(d));
-                    --sp;
-                }
-            }
-        }
-        if (COUNT) { const uint64_t e1 = clock64(); cySteal += e1 - st0; cyTail += e1 - e0; }
-        if (!__any(have || sp > 0)) {
-            if (lo >= a.b1) break;  // every batch of the pass retired
-            if (retired) continue;  // the queue may move on now
-            // nothing to do: sleep until tasks are published, unless the host
-            // aborts the pass or the wait times out
-            if (!waiting) {
-                waiting = true;
-                waitStart = wall_clock64();
-            }
-            if (a.probe) ++pSleeps;
-            __builtin_amdgcn_s_sleep(60);  // ~1.6 us
-            if ((++idleSpins & 63u) == 0u) {
-                uint32_t abort = 0;
-                if (threadIdx.x == 0) abortSeen = pollWord(a.ctl);
-                if (lane == 0) abort = abortSeen;
-                if (__builtin_amdgcn_readfirstlane(abort)) break;
-                if (wall_clock64() - waitStart > a.timeoutTicks) {
-                    // what the wave waited for (counters [26..29], read by the
-                    // host when the pass falls back: SAHARA_DEBUG_TEXT)
-                    if (lane == 0) {
-                        atomicAdd(a.counters + 26, 1ull);
-                        atomicMax(a.counters + 27, (unsigned long long)(qb * 2u + qph) << 32 | (qReady ? 1u : 0u));
-                        atomicMin(a.counters + 28, (unsigned long long)(qb * 2u + qph) << 32 | lo);
-                        atomicMax(a.counters + 29, (unsigned long long)pubVal[qb & 7u][qph] << 32 | pubTag[qb & 7u][qph]);
-                    }
-                    break;
-                }
-            }
-            pollSkip = 0;
-            if (COUNT) cyIdle += clock64() - t0;
-            continue;
-        }
-        waiting = false;
-        if (a.probe) {  // iterations and busy lanes before / after the wave saw all tasks taken
-            const uint32_t act = (uint32_t)__popcll(__ballot(have || sp > 0));
-            const uint32_t post = wDrain[threadIdx.x >> 6] != 0 ? 1u : 0u;
-            if (post) { ++pIterPost; pActPost += act; } else { ++pIterPre; pActPre += act; }
-        }
-        if (COUNT) {
-            const uint64_t act = __ballot(have || sp > 0);
-            if (lane == 0) { ++tIter; tActive += (uint64_t)__popcll(act); tRefill += refill ? 1u : 0u; }
-            const uint64_t t1 = clock64();
-            cyRefill += t1 - t0;
-            t0 = t1;
-        }
-
-        const uint64_t pw1 = a.probe ? wall_clock64() : 0;
-        // ---- up to a.steps micro-steps per lane; a lane that reaches a leaf
-        // holds it (stalls) until the emission below
-        bool leaf = false;
-        uint32_t leafStart = 0, leafE = 0;
-        for (uint32_t step = 0; step < a.steps; ++step) {
-            const bool pop = !have && !leaf && sp > 0;
-            const uint2 top = stackGet(pop ? sp - 1u : 0u);
-            if (pop) { cur = top; --sp; have = true; }
-            const bool live = have && !leaf;
-            if (!__any(live)) break;  // wave-uniform
-
-            const uint32_t pos = cur.y & 0xFFFFu;
-            const uint32_t xo = cur.x & 0xFFFFu, yo = cur.x >> 16;
-            const uint32_t e = (cur.y >> 16) & 0xFu;
-            const uint32_t lastL = (cur.y >> 20) & 3u, lastR = (cur.y >> 22) & 3u;
-            const uint2 tab = SC[sBase + min(pos, m - 1u)];
-            const uint32_t t0 = tab.x;
-            const uint32_t q0 = t0 & 0xFFFFu, lb0 = (t0 >> 16) & 0xFu, ub0 = (t0 >> 20) & 0xFu;
-            const bool r0 = (t0 >> 24) & 1u;
-            const uint32_t run0 = t0 >> 25, same0 = (tab.y >> 24) & 0x7Fu;
-
-            // ---- pattern symbols from pi[pos] in this step's direction and
-            // the text symbols beyond the span on that side, both in chain
-            // order (symbol j of the chain in bit j); text past the window
-            // edge or before the text start reads as 0 and never matches.
-            // One read each at a side-dependent offset (a left run ends at the
-            // position and is bit-reversed), so the lanes of both sides share it
-            const Planes P16 = chain32(P, r0 ? q0 : q0 + 1u, r0);
-            const Planes T16 = chain32(W, r0 ? yo : xo, r0);
-            const uint32_t avail = r0 ? (winLen > yo ? winLen - yo : 0u) : xo;
-            const uint32_t VT = onesR(avail);
-            const uint32_t E0 = eqm(P16, T16) & VT;                 // p_j == t_j     (M chain, S runs)
-            const uint32_t ED = eqm(P16, shr1(T16)) & (VT >> 1);    // p_j == t_{j+1} (D runs)
-            const uint32_t EI = eqm(shr1(P16), T16) & VT;           // p_{j+1} == t_j (I runs)
-            const uint32_t TZ = (T16.b0 | T16.b1 | T16.b2) & VT;    // t_j is a symbol (not '$' / edge)
-
-            const bool atLeaf = live && pos == m;
-            const bool node = live && pos < m;
-            const bool forced = e == ub0;          // no error child here or in the rest of the run
-            const bool kidsF = e + 1u == ub0;      // the error children are forced nodes
-            const bool mOK = lb0 <= e && e <= ub0;
-            const bool misOK = lb0 <= e + 1u && e + 1u <= ub0;
-            const uint32_t side = r0 ? lastR : lastL;
-            // chain budget: a forced node matches up to kRun symbols; a node
-            // whose error children are forced walks up to kChain positions of
-            // its match chain (same direction, l and u), checking every error
-            // child's forced run on the way; any other node is expanded alone
-            const uint32_t B = forced ? min(run0, kRun)
-                                      : (kidsF ? max(1u, min(min(same0, run0 - 1u), kChain)) : 1u);
-            const uint32_t miss = ~E0 & kRunMask;
-            const uint32_t L = mOK ? min(B, miss ? (uint32_t)__builtin_ctz(miss) : kRun) : 0u;
-
-            // ---- error children of the chain nodes i < NN (node L = the mismatch)
-            const uint32_t NN = L < B ? L + 1u : B;
-            const uint32_t nodesM = node && !forced ? onesR(NN) : 0u;  // leaves / idle lanes: none
-            const uint32_t first = 1u;  // chain node 0 (= this node)
-            uint32_t Dm = EDIT ? (nodesM & TZ) : 0u;
-            if (pos == 0u || side == OP_I) Dm &= ~first;
-            uint32_t Im = EDIT && misOK ? nodesM : 0u;
-            if (side == OP_D) Im &= ~first;
-            // S at the first mismatch (not where M is merely disallowed: l > e)
-            bool Sx = node && !forced && L < B && misOK && ((TZ & ~E0) >> L) & 1u;
-            // forced runs: a child at e + 1 = u is forced for the rest of the run,
-            // and survives only if min(7, rest of the run) symbols match on its
-            // diagonal (positions past the run count as matches): R7x bit j =
-            // that check for a run starting at chain position j on diagonal x
-            const uint32_t bR = beyondR(run0), bR1 = beyondR(run0 - 1u);
-            const uint32_t R7E0 = run7(E0 | bR), R7ED = run7(ED | bR), R7EI = run7(EI | bR1);
-            if (kidsF) {
-                // D at i: p[i..] vs t[i+1..]; I at i: p[i+1..] vs t[i..]; S at L: p[L+1..] vs t[L+1..]
-                Dm &= R7ED;
-                Im &= R7EI;
-                Sx = Sx && ((R7E0 >> (L + 1u)) & 1u);
-            }
-            if (EDIT && node && e + 2u == ub0) {
-                // A node expanded alone whose error children are chain nodes:
-                // keep only the children whose subtree outlives their own first
-                // step. A child does if its match chain leaves the run or the
-                // 32 symbols read (chain length > kRun - 9), or one of its own
-                // error children (forced) passes the check above on its
-                // diagonal; no I right after D, no D right after I (policy P0).
-                // tests/text_model.py holds this to the plain DFS.
-                const uint32_t ED2 = eqm(P16, shr2(T16)) & (VT >> 2);   // p_j == t_{j+2}
-                const uint32_t EI2 = eqm(shr2(P16), T16) & VT;          // p_{j+2} == t_j
-                const uint32_t bR2 = run0 >= 2u ? beyondR(run0 - 2u) : kRunMask;
-                const uint32_t R7ED2 = run7(ED2 | bR), R7EI2 = run7(EI2 | bR2);
-                const uint32_t I2after = (R7E0 >> 1) & ~1u;  // bit j: I2 (back to diagonal 0) at chain node j > 0
-                constexpr uint32_t kLim = kRun - 9u;
-                if (Dm & first) {  // D child: p_j vs t_{j+1}
-                    const uint32_t LD = (uint32_t)__builtin_ctz(~ED);
-                    const bool keep = LD >= run0 || LD > kLim || ((R7ED >> (LD + 1u)) & 1u) ||
-                                      ((R7ED2 | I2after) & onesR(LD + 1u)) != 0u;
-                    if (!keep) Dm &= ~first;
-                }
-                if (Im & first) {  // I child: p_{x+1} vs t_x
-                    const uint32_t LI = ~EI ? (uint32_t)__builtin_ctz(~EI) : kRun;
-                    const bool keep = LI + 1u >= run0 || LI > kLim || ((R7EI >> (LI + 1u)) & 1u) ||
-                                      ((I2after | R7EI2) & onesR(LI + 1u)) != 0u;
-                    if (!keep) Im &= ~first;
-                }
-                if (Sx) {  // S child at the mismatch L = 0: p_x vs t_x, x >= 1
-                    const uint32_t rest = ~E0 & ~1u;
-                    const uint32_t LS = rest ? (uint32_t)__builtin_ctz(rest) : kRun;
-                    Sx = LS >= run0 || LS > kLim || ((R7E0 >> (LS + 1u)) & 1u) ||
-                         ((R7ED | R7EI) & ~1u & onesR(LS + 1u)) != 0u;
-                }
-            }
-            const bool contM = node && L >= B;  // the match chain continues at pos + B
-            uint32_t nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
-            // the lane continues with one child and stacks the others: a
-            // surviving error child first, the match chain below it
-            uint32_t Bc = B;
-            // Stack invariant (stackCap = 2k + 2): a node that stacks entries
-            // with e errors finds sp <= 2e + 2. One node expanded alone stacks
-            // <= 2; a chain may stack more only while the child it continues
-            // with (e + 1) still finds sp <= 2(e + 1) + 2.
-            if (nSurv && sp + nSurv + (contM ? 1u : 0u) - 1u > 2u * e + 4u) {
-                // not enough stack for this chain: expand its first node only
-                Bc = 1u;
-                Dm &= first;
-                Im &= first;
-                Sx = Sx && L == 0u;
-                nSurv = (uint32_t)__popc(Dm) + (uint32_t)__popc(Im) + (Sx ? 1u : 0u);
-            }
-            const bool contM1 = node && L >= Bc;
-            // cannot happen (the reserve rule above; tests/text_model.py): flagged, not handled
-            bad = bad || (node && nSurv && sp + nSurv + (contM1 ? 1u : 0u) - 1u > a.stackCap);
-
-            // ---- children as stack entries (x = span, y = meta). Per step:
-            // extending by n symbols adds n << 16 (right) or -n (left) to the
-            // span, one mad; a child's side memory is its operation on the
-            // extension side (MS once k forced matches follow it), the other
-            // side keeps its memory — except at pos 0, where the first
-            // operation sets both (for chain node i > 0 that was a match)
-            const int extMul = r0 ? 65536 : -1;
-            auto extend = [&](uint32_t span, uint32_t n) -> uint32_t { return span + (uint32_t)((int)n * extMul); };
-            const uint32_t shMine = r0 ? 22u : 20u, shOther = r0 ? 20u : 22u;
-            const uint32_t otherKept = pos ? (r0 ? lastL : lastR) : (uint32_t)OP_MS;
-            auto metaAt = [&](uint32_t i, uint32_t op, uint32_t k) -> uint32_t {
-                const uint32_t mine = k ? (uint32_t)OP_MS : op;
-                const uint32_t other = (pos == 0u && i == 0u) ? op : otherKept;
-                return (mine << shMine) | (other << shOther);
-            };
-            const uint32_t e1 = (e + 1u) << 16;
-            // forced matches after an error child whose run starts at chain node ii
-            const uint32_t kEnd = kidsF ? run0 : 0u;
-            const uint2 cM = make_uint2(extend(cur.x, Bc), (pos + Bc) | (e << 16) | metaAt(Bc, OP_MS, 0u));
-            if (nSurv) {  // the surviving error children; the last one stays in registers
-                uint32_t spw = sp;
-                uint2 pend = cM;
-                bool hasPend = contM1;
-                // one loop over all of them — D at chain node i (bit i), I at i
-                // (bit 32 + i), S at L (bit 63), in that order — so the wave
-                // runs max(nSurv) iterations rather than one loop per kind
-                uint64_t sv = (uint64_t)Dm | ((uint64_t)Im << 32) | (Sx ? 1ull << 63 : 0ull);
-                while (sv) {
-                    const uint32_t j = (uint32_t)__builtin_ctzll(sv);
-                    sv &= sv - 1ull;
-                    const bool isS = j == 63u, isD = j < 32u, isI = !isD && !isS;
-                    const uint32_t i = isS ? L : (j & 31u);
-                    const uint32_t ii = i + (isD ? 0u : 1u);  // chain node where its forced run starts
-                    const uint32_t k = ii < kEnd ? min(kEnd - ii, 7u) : 0u;
-                    const uint32_t op = isD ? (uint32_t)OP_D : (isI ? (uint32_t)OP_I : (uint32_t)OP_MS);
-                    const uint2 v = make_uint2(extend(cur.x, i + k + (isI ? 0u : 1u)), (pos + ii + k) | e1 | metaAt(i, op, k));
-                    if (hasPend) stackPut(min(spw++, a.stackCap - 1u), pend);
-                    pend = v;
-                    hasPend = true;
-                }
-                sp = min(spw, a.stackCap);
-                cur = pend;
-            } else if (node && contM1) {
-                cur = cM;
-            }
-
-            if (atLeaf) { leaf = true; leafStart = xo; leafE = e; }
-            have = live ? node && (nSurv || contM1) : have;
-            if (COUNT) {
-                cNodes += forced ? 0u : (node ? NN : 0u);
-                cCmp += (node && forced) ? 1u : 0u;
-                cSteps += node ? 1u : 0u;
-            }
-        }
-        if (COUNT) {
-            const uint64_t t1 = clock64();
-            cyStep += t1 - t0;
-            t0 = t1;
-        }
-        {
-            // leaves -> the hit buffer of their batch: a slot per leaf lane
-            // from the wave's range of its batch parity, one store site, and
-            // a count on the query (tcnt) by an atomic whose result is not
-            // used. No value returns into the wave: a returning atomic (the
-            // hit's rank, as the FM phase does it) left a register pending
-            // across the micro-steps, which the compiler then waited for in
-            // every one of them (4.5x the text time, r5); kLocate ranks text
-            // hits instead, at the tail of their query's segment
-            uint32_t s = ~0u;
-            auto take = [&](uint32_t p, uint32_t& hn, uint32_t& he, uint32_t* counter) __attribute__((always_inline)) {
-                const bool want = leaf && lpar == p;
-                const uint64_t wm = __ballot(want);
-                if (!wm) return;
-                const uint32_t cnt = (uint32_t)__popcll(wm), rank = (uint32_t)__popcll(wm & ltMask);
-                const uint32_t avail = he - hn;
-                uint32_t base = 0;
-                if (cnt > avail) {
-                    if (lane == 0)
-                        base = __hip_atomic_fetch_add(GLOB(uint32_t, counter), kHitChunk, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-                    base = __builtin_amdgcn_readfirstlane(base);
-                }
-                if (want) s = rank < avail ? hn + rank : base + (rank - avail);
-                if (cnt > avail) { hn = base + (cnt - avail); he = base + kHitChunk; }
-                else hn += cnt;
-            };
-            if (__any(leaf)) {
-                take(0u, hn0, he0, slotP0.small + 1);
-                take(1u, hn1, he1, slotP1.small + 1);
-                if (leaf) {
-                    const bool p1 = lpar != 0u;
-                    if (s < a.hitCap) {
-                        storeThrough((p1 ? slotP1.hits : slotP0.hits) + s,
-                                     make_uint4(pid, wb + leafStart, 1u, leafE | kPosKnown));
-#ifndef SAHARA_V_NOTCNT
-                        (void)__hip_atomic_fetch_add(GLOB(uint32_t, (p1 ? slotP1.tcnt : slotP0.tcnt) + pid), 1u,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-                    } else {
-                        __hip_atomic_fetch_or(GLOB(uint32_t, (p1 ? slotP1.small : slotP0.small) + 2), 2u,
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    if (p1) ++filled1;
-                    else ++filled0;
-                }
-            }
-        }
-        if (COUNT) cyEmit += clock64() - t0;
-        if (a.probe) {
-            const uint64_t pw2 = wall_clock64();
-            if (wDrain[threadIdx.x >> 6] != 0) { pwPostA += pw1 - pw0; pwPostB += pw2 - pw1; }
-            else { pwPreA += pw1 - pw0; pwPreB += pw2 - pw1; }
-        }
-    }
-    if (a.probe && a.b0 == 0 && lane == 0) {  // the first launch's wave lives on the wall clock
-        const uint64_t wEnd = wall_clock64(), w0 = wBorn[threadIdx.x >> 6];
-        atomicMin(a.counters + 33, (unsigned long long)w0);
-        atomicMax(a.counters + 34, (unsigned long long)w0);
-        atomicMax(a.counters + 35, (unsigned long long)wEnd);
-        atomicAdd(a.counters + 36, (unsigned long long)(wEnd - w0));
-        atomicMin(a.counters + 37, (unsigned long long)wEnd);
-        const uint64_t wd = wDrain[threadIdx.x >> 6];
-        if (wd) {  // the wave saw the pass's tasks all taken: when, and how long it ran on
-            atomicMin(a.counters + 38, (unsigned long long)wd);
-            atomicMax(a.counters + 39, (unsigned long long)wd);
-            atomicAdd(a.counters + 30, (unsigned long long)(wEnd - wd));
-            atomicAdd(a.counters + 31, 1ull);
-        }
-        atomicAdd(a.counters + 40, (unsigned long long)pIterPre);
-        atomicAdd(a.counters + 41, (unsigned long long)pActPre);
-        atomicAdd(a.counters + 42, (unsigned long long)pIterPost);
-        atomicAdd(a.counters + 43, (unsigned long long)pActPost);
-        atomicAdd(a.counters + 44, (unsigned long long)pSleeps);
-        atomicAdd(a.counters + 45, (unsigned long long)pSteals);
-        atomicAdd(a.counters + 46, (unsigned long long)pwPreA);
-        atomicAdd(a.counters + 47, (unsigned long long)pwPreB);
-        atomicAdd(a.counters + 48, (unsigned long long)pwPostA);
-        atomicAdd(a.counters + 49, (unsigned long long)pwPostB);
-    }
-    if (COUNT) {
-        atomicAdd(a.counters + 5, (unsigned long long)cNodes);
-        if (lane == 0) {
-            atomicAdd(a.counters + 8, (unsigned long long)tIter);
-            atomicAdd(a.counters + 9, (unsigned long long)tActive);
-            atomicAdd(a.counters + 10, (unsigned long long)tRefill);
-            atomicAdd(a.counters + 11, (unsigned long long)cyRefill);
-            atomicAdd(a.counters + 12, (unsigned long long)cyStep);
-            atomicAdd(a.counters + 13, (unsigned long long)cyEmit);
-            atomicAdd(a.counters + 17, (unsigned long long)cyIdle);
-            atomicAdd(a.counters + 18, (unsigned long long)cyGrab);
-            atomicAdd(a.counters + 19, (unsigned long long)(clock64() - tBorn));
-            atomicAdd(a.counters + 20, (unsigned long long)cyStart);
-            atomicAdd(a.counters + 21, (unsigned long long)cySteal);
-            atomicAdd(a.counters + 22, (unsigned long long)cyRetire);
-            atomicAdd(a.counters + 23, (unsigned long long)cyResolve);
-            atomicAdd(a.counters + 24, (unsigned long long)cySwitch);
-            atomicAdd(a.counters + 25, (unsigned long long)nGrab);
-            atomicAdd(a.counters + 30, (unsigned long long)cyShfl);
-            atomicAdd(a.counters + 31, (unsigned long long)cyTail);
-            atomicAdd(a.counters + 32, (unsigned long long)cyTop);
-
-        }
-        atomicAdd(a.counters + 14, (unsigned long long)cCmp);
-        atomicAdd(a.counters + 15, (unsigned long long)cSteps);
-    }
-}
-
-// A producer stream's step of the text phase's hand-off: flag[16 w] = the
-// task count (capped) | kTaskReady for each of the text launch's nwg
-// workgroups w, stored sc1 (relaxed, agent scope). The tasks were written by
-// the kernels before this one on its stream, whose end released them; a text
-// workgroup polls its own copy, then acquires.
-__global__ void kPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, uint32_t nwg) {
-    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nwg) return;
-    const uint32_t v = min(*count, cap) | kTaskReady;
-    __hip_atomic_store((GlobalU32*)(flag + 16u * w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ================================================================ locate ====
@@ -2193,13 +1322,12 @@ __device__ __forceinline__ uint64_t blockExclusiveScan(uint64_t v, uint64_t& tot
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(256) void kTileSums(const uint32_t* __restrict__ cnt,
-                                                const uint32_t* __restrict__ tcnt, uint32_t n,
+__global__ __launch_bounds__(256) void kTileSums(const uint32_t* __restrict__ cnt, uint32_t n,
                                                 uint64_t* __restrict__ partial) {
     __shared__ uint64_t wsum[4];
     const uint32_t base = blockIdx.x * kScanTile;
     uint64_t acc = 0;
-    for (uint32_t i = threadIdx.x; i < kScanTile && base + i < n; i += 256) acc += cnt[base + i] + tcnt[base + i];
+    for (uint32_t i = threadIdx.x; i < kScanTile && base + i < n; i += 256) acc += cnt[base + i];
     for (uint32_t off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
     if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = acc;
     __syncthreads();
@@ -2219,8 +1347,7 @@ __global__ __launch_bounds__(256) void kScanPartials(uint64_t* __restrict__ part
     }
 }
 
-__global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tcnt,
-                                                 uint32_t n,
+__global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, uint32_t n,
                                                  const uint64_t* __restrict__ partial, uint64_t* __restrict__ off,
                                                  uint32_t* __restrict__ list, uint32_t* __restrict__ nlist,
                                                  uint32_t* __restrict__ huge, uint32_t* __restrict__ nhuge) {
@@ -2233,9 +1360,8 @@ __global__ __launch_bounds__(256) void kScanTiles(uint32_t* __restrict__ cnt, co
     uint64_t carry = partial[blockIdx.x];
     for (uint32_t c = 0; c < kScanTile; c += 256) {  // uniform trip count: block scans inside
         const uint32_t i = base + c + threadIdx.x;
-        const uint32_t f = i < n ? cnt[i] : 0u;
-        if (f) cnt[i] = 0u;  // zero again for the next batch (tcnt: kLocate counts it down)
-        const uint32_t v = f + (i < n ? tcnt[i] : 0u);
+        const uint32_t v = i < n ? cnt[i] : 0u;
+        if (v) cnt[i] = 0u;  // zero again for the next batch
         uint64_t tot;
         const uint64_t ex = blockExclusiveScan(v, tot, wsum);
         if (i < n) off[i] = carry + ex;
@@ -2267,11 +1393,6 @@ __global__ __launch_bounds__(256) void kLocate(LocateArgs a) {
         const uint4 hit = a.hits[h];
         if (hit.z == 0) continue;  // reserved hole
         const uint64_t e = hit.w & 0xFu;
-        if ((hit.w & kPosKnown) && a.tcnt) {  // (one text launch) the segment's tail, counted down
-            const uint32_t left = atomicSub(a.tcnt + hit.x, 1u);
-            a.keys[a.qoff[hit.x + 1] - left] = ((uint64_t)hit.y << 4) | e;
-            continue;
-        }
         const uint64_t out = a.qoff[hit.x] + a.rank[h];
         if (hit.w & kPosKnown) {  // resolved by the text phase, ranked where it was written
             a.keys[out] = ((uint64_t)hit.y << 4) | e;
@@ -2629,37 +1750,6 @@ void launchFMT(const SearchArgs& a, bool edit, bool count, dim3 grid, size_t lds
 
 
 
-template <int SIGMA, int SHAPE>
-void launchTextShaped(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
-    if (edit) {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, true, true, SHAPE>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, true, false, SHAPE>), grid, dim3(256), lds, st, a);
-    } else {
-        if (count) hipLaunchKernelGGL((kSearchText<SIGMA, false, true, SHAPE>), grid, dim3(256), lds, st, a);
-        else       hipLaunchKernelGGL((kSearchText<SIGMA, false, false, SHAPE>), grid, dim3(256), lds, st, a);
-    }
-}
-
-template <int SIGMA, int SHAPE>
-const void* textKernelOf(bool edit, bool count) {
-    if (edit) return count ? (const void*)kSearchText<SIGMA, true, true, SHAPE> : (const void*)kSearchText<SIGMA, true, false, SHAPE>;
-    return count ? (const void*)kSearchText<SIGMA, false, true, SHAPE> : (const void*)kSearchText<SIGMA, false, false, SHAPE>;
-}
-
-template <int SIGMA>
-const void* textKernelOfShape(bool edit, bool count, int shape) {
-    return shape == 1 ? textKernelOf<SIGMA, 1>(edit, count)
-                      : shape == 2 ? textKernelOf<SIGMA, 2>(edit, count) : textKernelOf<SIGMA, 0>(edit, count);
-}
-
-template <int SIGMA>
-void launchTextT(const TextArgs& a, bool edit, bool count, dim3 grid, size_t lds, hipStream_t st) {
-    const int shape = textShapeOf(a.winBlocks, a.patBlocks, a.exactWindow != 0u);
-    if (shape == 1) launchTextShaped<SIGMA, 1>(a, edit, count, grid, lds, st);
-    else if (shape == 2) launchTextShaped<SIGMA, 2>(a, edit, count, grid, lds, st);
-    else launchTextShaped<SIGMA, 0>(a, edit, count, grid, lds, st);
-}
-
 }  // namespace
 
 // the compile-time shape matching a launch (0: the generic kernel)
@@ -2695,41 +1785,12 @@ const void* textBatchKernelOf(bool edit, bool count, int shape) {
     return nullptr;
 }
 
-int textBlocksPerCU(uint32_t sigma, bool edit, bool count, int shape, size_t lds, bool persistent) {
+int textBlocksPerCU(uint32_t sigma, bool edit, bool count, int shape, size_t lds) {
     // (the variant that is launched: its registers differ by shape and count mode)
     int b = 0;
-    const void* f = persistent
-                        ? (sigma == 5 ? textKernelOfShape<5>(edit, count, shape) : textKernelOfShape<6>(edit, count, shape))
-                        : (sigma == 5 ? textBatchKernelOf<5>(edit, count, shape) : textBatchKernelOf<6>(edit, count, shape));
+    const void* f = sigma == 5 ? textBatchKernelOf<5>(edit, count, shape) : textBatchKernelOf<6>(edit, count, shape);
     SH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 256, lds));
     return b;
-}
-
-// The text kernel waits inside its launch for tasks that the seed and FM
-// kernels publish, so those must be able to run beside its resident
-// workgroups: the most text workgroups per CU (at most `want`) that leave a
-// SIMD's VGPRs (512 per lane) and the CU's LDS (160 KB) for one FM workgroup
-// and a 16 KB locate-chain workgroup (kSortBigLds, kScanTiles).
-int textBlocksBeside(uint32_t sigma, bool edit, bool count, int shape, size_t textLds, size_t fmLds, int want) {
-    auto textFn = [&]() -> const void* {
-        return sigma == 5 ? textKernelOfShape<5>(edit, count, shape) : textKernelOfShape<6>(edit, count, shape);
-    };
-    const void* fm;
-    if (sigma == 5)
-        fm = edit ? (count ? (const void*)kSearchFM<5, true, true> : (const void*)kSearchFM<5, true, false>)
-                  : (count ? (const void*)kSearchFM<5, false, true> : (const void*)kSearchFM<5, false, false>);
-    else
-        fm = edit ? (count ? (const void*)kSearchFM<6, true, true> : (const void*)kSearchFM<6, true, false>)
-                  : (count ? (const void*)kSearchFM<6, false, true> : (const void*)kSearchFM<6, false, false>);
-    hipFuncAttributes ta{}, fa{};
-    SH_HIP(hipFuncGetAttributes(&ta, textFn()));
-    SH_HIP(hipFuncGetAttributes(&fa, fm));
-    auto granule = [](int r) { return (std::max(r, 1) + 7) / 8 * 8; };
-    const int vt = granule(ta.numRegs), vf = granule(fa.numRegs);
-    const size_t lt = textLds + ta.sharedSizeBytes, lf = fmLds + fa.sharedSizeBytes;
-    for (int t = std::max(want, 1); t > 1; --t)
-        if (t * vt + vf <= 512 && t * lt + lf + (16u << 10) <= (160u << 10) && t + 1 <= 8) return t;
-    return 1;
 }
 
 void launchSearch(const SearchArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
@@ -2762,18 +1823,6 @@ void launchTextBatch(const TextBatchArgs& a, uint32_t sigma, bool edit, bool cou
                      hipStream_t st) {
     if (sigma == 5) launchTextBatchT<5>(a, edit, count, dim3(blocks), lds, st);
     else            launchTextBatchT<6>(a, edit, count, dim3(blocks), lds, st);
-    SH_HIP(hipGetLastError());
-}
-
-void launchText(const TextArgs& a, uint32_t sigma, bool edit, bool count, uint32_t blocks, size_t lds,
-                hipStream_t st) {
-    if (sigma == 5) launchTextT<5>(a, edit, count, dim3(blocks), lds, st);
-    else            launchTextT<6>(a, edit, count, dim3(blocks), lds, st);
-    SH_HIP(hipGetLastError());
-}
-
-void launchPublish(const uint32_t* count, uint32_t cap, uint32_t* flag, uint32_t nwg, hipStream_t st) {
-    hipLaunchKernelGGL(kPublish, dim3((nwg + 255) / 256), dim3(256), 0, st, count, cap, flag, nwg);
     SH_HIP(hipGetLastError());
 }
 
@@ -3100,14 +2149,13 @@ void launchPackPatterns(const uint8_t* src, uint64_t npat, uint32_t m, uint32_t 
     SH_HIP(hipGetLastError());
 }
 
-void querySegments(uint32_t* qcnt, const uint32_t* tcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial,
-                   uint32_t* big, uint32_t* nbig, uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
-    // qcnt[nq] and tcnt[nq] stay 0, so qoff[nq] = total rows
+void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
+                   uint32_t* huge, uint32_t* nhuge, hipStream_t st) {
+    // qcnt[nq] stays 0, so qoff[nq] = total rows
     const uint32_t n = nq + 1, tiles = (n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, tcnt, n, partial);
+    hipLaunchKernelGGL(kTileSums, dim3(tiles), dim3(256), 0, st, qcnt, n, partial);
     hipLaunchKernelGGL(kScanPartials, dim3(1), dim3(256), 0, st, partial, tiles);
-    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, tcnt, n, partial, qoff, big, nbig, huge,
-                       nhuge);
+    hipLaunchKernelGGL(kScanTiles, dim3(tiles), dim3(256), 0, st, qcnt, n, partial, qoff, big, nbig, huge, nhuge);
     SH_HIP(hipGetLastError());
 }
 

@@ -676,11 +676,23 @@ static void stagePackedN(Ctx* c, const PackedReads& P, uint64_t rows, uint32_t m
     const uint64_t* all = P.nCount ? P.nPos : nullptr;
     // the whole list, not only this call's range: the binary searches below
     // place the range correctly only in an ascending list (a shard of a larger
-    // stream sees every entry)
-    for (uint64_t i = 1; i < P.nCount; ++i)
-        if (all[i] <= all[i - 1]) throw Error("N positions of packed reads must be strictly ascending");
+    // stream sees every entry). Checked once per list (a stream's shards share
+    // it); the range found is checked on every call.
+    const char* kUnordered = "N positions of packed reads must be strictly ascending";
+    if (all && (c->nPosChecked != all || c->nCountChecked != P.nCount)) {
+        for (uint64_t i = 1; i < P.nCount; ++i)
+            if (all[i] <= all[i - 1]) throw Error(kUnordered);
+        c->nPosChecked = all;
+        c->nCountChecked = P.nCount;
+    }
     const uint64_t* b = all ? std::lower_bound(all, all + P.nCount, lo) : nullptr;
     const uint64_t* e = all ? std::lower_bound(b, all + P.nCount, hi) : nullptr;
+    if (all) {  // [b, e) ascending inside [lo, hi), its neighbours outside
+        const uint64_t* end = all + P.nCount;
+        if ((b > all && b[-1] >= lo) || (e < end && *e < hi)) throw Error(kUnordered);
+        for (const uint64_t* q = b; q < e; ++q)
+            if (*q < lo || *q >= hi || (q > b && *q <= q[-1])) throw Error(kUnordered);
+    }
     const uint64_t nN = all ? (uint64_t)(e - b) : 0;
     if (nN && c->I.sigma == 5) throw Error("pattern rank out of range for this index");  // N is no dna4 rank
     const uint64_t nch = chunkCount(U);

@@ -7,6 +7,9 @@ no part of the GPU's index reaches the checker), in all four execution modes:
 - C1 exactly: 1,000 x 32 bp, k = 0, against 1 Mbp (search.cpp:221-231, k = 0);
 - C2: k = 1 Hamming (`-d ham`, limitToHamming, search.cpp:226-227), 100 bp,
   substitution-only reads, against a 10 Mbp single-record reference;
+- C3 (the bench's workload, reduced): k = 2 Levenshtein, 100 bp, h2-k2 (3
+  searches), against a 12 Mbp reference in 24 records, also through the
+  streamed packed call the bench times (search.cpp:221-250);
 - C5: k = 3 Levenshtein, 250 bp, h2-k2 expanded to 5 searches, against a
   10 Mbp reference in 24 records (GRCh38 proportions, like bench.py).
 
@@ -54,7 +57,7 @@ def _origin_recall(rows, origin, k):
     return found.mean()
 
 
-def _check_config(gpu_device, ref_len, n_rec, n_reads, m, k, edit, n_searches, check_index=False):
+def _check_config(gpu_device, ref_len, n_rec, n_reads, m, k, edit, n_searches, check_index=False, streamed=False):
     flat, lens = sa.synth_reference(_lens(ref_len, n_rec), sigma=6, seed=42)
     reads, origin = sa.synth_reads(flat, lens, n_reads, m, k if edit else 0, sigma=6, seed=7, with_origin=True,
                                    substitutions=0 if edit else k)
@@ -78,6 +81,12 @@ def _check_config(gpu_device, ref_len, n_rec, n_reads, m, k, edit, n_searches, c
         got = hits_as_rows(sa.search(gpu, pats, sch, edit=edit))
         assert len(got) == len(want), (verify, locate_sa, len(got), len(want))
         assert np.array_equal(got, want), (verify, locate_sa)
+    if streamed:  # the bench's call: 2-bit reads in page-locked memory in, compact records out
+        gpu.set_mode(verify=True, locate_sa=True)
+        rec = sa.search_packed_compact(gpu, sa.pack_reads(reads, 6, pinned=True), sch, edit=edit)
+        got = hits_as_rows(rec.to_hits())
+        rec.close()
+        assert np.array_equal(got, want)
     assert _origin_recall(want, origin, k) == 1.0
     return want
 
@@ -92,6 +101,12 @@ def test_c2_shape_hamming(gpu_device):
     """C2: k=1 Hamming, 100 bp substitution-only reads, single record."""
     want = _check_config(gpu_device, 10_000_000, 1, 20_000, 100, 1, False, 2, check_index=True)
     assert want[:, 3].max() <= 1
+
+
+def test_c3_shape_k2_edit_100bp(gpu_device):
+    """C3: k=2 Levenshtein, 100 bp, h2-k2 (3 searches), 24 GRCh38-proportioned records."""
+    want = _check_config(gpu_device, 12_000_000, 24, 50_000, 100, 2, True, 3, streamed=True)
+    assert want[:, 3].max() <= 2 and len(np.unique(want[:, 1])) > 12
 
 
 def test_c5_shape_k3_250bp(gpu_device):

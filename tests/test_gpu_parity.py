@@ -677,19 +677,14 @@ def test_single_row_seeds_near_text_ends(gpu_device, m, k, gen):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch,one", [("61", "1"), ("61", "0"), ("1000", "1")])
-def test_one_text_launch_many_batches(gpu_device, monkeypatch, batch, one):
-    """The text phase per batch (search.hip kSearchTextBatch, the default:
-    SAHARA_TEXT_ONE_LAUNCH=0) or as one launch per pass (kSearchText,
-    SAHARA_TEXT_ONE_LAUNCH=1) that takes each batch's tasks as the seed and
-    FM streams publish them and tells the host when a batch is done. More
+@pytest.mark.parametrize("batch", ["61", "1000"])
+def test_text_phase_many_batches(gpu_device, monkeypatch, batch):
+    """The text phase per batch (search.hip kSearchTextBatch) with more
     batches than slots (61 patterns per batch: 14 batches over 5 slots),
-    repeat-rich text with k = 3 (tasks that outlive their batch, work stealing
-    across batch parities): the oracle's hits through the device-resident
-    pass, the rank-form reads call and the packed call; one text launch per
-    pass (or at least one per batch) and no wave gave up waiting."""
+    repeat-rich text with k = 3 (long tasks, work stealing): the oracle's hits
+    through the device-resident pass (plain and count mode), the rank-form
+    reads call and the packed call; at least one text launch per batch."""
     monkeypatch.setenv("SAHARA_BATCH", batch)
-    monkeypatch.setenv("SAHARA_TEXT_ONE_LAUNCH", one)
     rng = np.random.default_rng(505)
     recs = random_records(rng, [30000, 12000], 6, repeats=True)
     reads = mutate_reads(rng, recs, 400, 80, 3, 6)
@@ -704,49 +699,51 @@ def test_one_text_launch_many_batches(gpu_device, monkeypatch, batch, one):
         st = gpu.stats()
         assert np.array_equal(hits_as_rows(gpu.fetch()), want), count
         assert st["batches"] == nbatch and st["text_fallbacks"] == 0, st
-        # (per batch: the first batch of an early pass launches twice, on
-        # its seed tasks and then on the FM phase's)
-        assert (st["text_launches"] == 1) if one == "1" else (nbatch <= st["text_launches"] <= nbatch + 1), st
+        assert st["text_launches"] >= nbatch, st
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme)), want)
-    assert gpu.stats()["text_fallbacks"] == 0
     c = sa.search_packed_compact(gpu, sa.pack_reads(reads, 6, pinned=True), scheme)
     got = c.to_hits()
     c.close()
     assert np.array_equal(hits_as_rows(got), want)
-    assert gpu.stats()["text_fallbacks"] == 0
 
 
 @pytest.mark.gpu
-def test_one_text_launch_with_few_hardware_queues(gpu_device, tmp_path):
-    """The text launch waits inside for kernels on the seed and FM streams.
-    Its stream is created with a CU mask, which gives it a hardware queue of
-    its own: with GPU_MAX_HW_QUEUES=1 (every other stream of the process on
-    one queue) no kernel it waits for queues behind it, so no wave gives up
-    (text_fallbacks 0) and the hits are the oracle's."""
+def test_buffers_at_high_addresses(gpu_device, tmp_path):
+    """Every device buffer placed at an address whose low 32-bit word has bit
+    31 set (test hook SAHARA_TEST_HIGH_ADDR=1, device_index.h DevBuf): a
+    kernel that rebuilds a 64-bit address from a sign-extended 32-bit half —
+    the round-5 fault — would fault or read the wrong memory
+    here whatever the allocator does. The oracle's hits in all four execution
+    modes, through the streamed packed call, and the rank-form reads call."""
     import os
     import subprocess
     import sys
-    script = tmp_path / "q.py"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "high.py"
     script.write_text(f"""
 import sys
-sys.path[:0] = {[os.path.dirname(os.path.dirname(os.path.abspath(__file__))), os.path.dirname(os.path.abspath(__file__)), os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")]!r}
+sys.path[:0] = {[root, os.path.join(root, "tests"), os.path.join(root, "oracle")]!r}
 import numpy as np
 import oracle as O
 import sahara_amd as sa
 from helpers import hits_as_rows, mutate_reads, random_records
-rng = np.random.default_rng(506)
-recs = random_records(rng, [20000, 9000], 6, repeats=True)
-reads = mutate_reads(rng, recs, 300, 60, 2, 6)
+rng = np.random.default_rng(3131)
+recs = random_records(rng, [40000, 9000, 300], 6, with_n=True, repeats=True)
+reads = mutate_reads(rng, recs, 500, 100, 2, 6)
 pats = sa.interleave_rc(reads, 6)
-scheme = sa.search_scheme("h2-k2", 0, 2, 60)
-want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, scheme, edit=True, nthreads=8)[0])
+sch = sa.search_scheme("h2-k2", 0, 2, 100)
+want = hits_as_rows(O.Index.build(recs, 6, 16).search(pats, sch, edit=True, nthreads=8)[0])
 gpu = sa.BiFMIndex.build(recs, sigma=6, device={gpu_device})
-got = hits_as_rows(sa.search(gpu, pats, scheme))
-st = gpu.stats()
-print("fallbacks", st["text_fallbacks"], "launches", st["text_launches"], "batches", st["batches"])
-assert np.array_equal(got, want)
-assert st["text_fallbacks"] == 0 and st["text_launches"] == 1 and st["batches"] > 5
+for verify, locate_sa in [(True, True), (False, False), (True, False), (False, True)]:
+    gpu.set_mode(verify=verify, locate_sa=locate_sa)
+    assert np.array_equal(hits_as_rows(sa.search(gpu, pats, sch)), want), (verify, locate_sa)
+gpu.set_mode(verify=True, locate_sa=True)
+rec = sa.search_packed_compact(gpu, sa.pack_reads(reads, 6, pinned=True), sch)
+assert np.array_equal(hits_as_rows(rec.to_hits()), want)
+rec.close()
+assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, sch)), want)
+print("ok", len(want))
 """)
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="1", SAHARA_BATCH="53", SAHARA_TEXT_ONE_LAUNCH="1")
-    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout + r.stderr
+    env = dict(os.environ, SAHARA_TEST_HIGH_ADDR="1", SAHARA_BATCH="301")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

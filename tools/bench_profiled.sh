@@ -48,5 +48,9 @@ n, tot = ks[dom]
 avg = tot / n / 1e6
 print(f"bench {d['value']/1e6:.1f}M reads/s; {dom}: all {n} launches (timed, warmup, device-resident, "
       f"PCIe-inclusive calls) average {avg:.3f} ms")
+json.dump({"kernel": dom, "build_id": d["config"].get("build_id"), "bench_value": d["value"],
+           "bench_launch_ms": rl["launch_ms"], "rocprof_timed_avg_ms": round(avg_timed, 4),
+           "timed_launches": len(timed), "ratio": round(rl["launch_ms"] / avg_timed, 4),
+           "rocprof_all_avg_ms": round(avg, 4), "all_launches": n}, open(f"{out}/summary.json", "w"), indent=1)
 PY
 rm -f "$OUT"/trace/run_kernel_trace.csv

@@ -16,6 +16,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
 
@@ -23,6 +24,14 @@ import sys
 def short(n):
     m = re.search(r"::(k[A-Z]\w*)", n) or re.search(r"(k[A-Z]\w*)", n)
     return m.group(1) if m else n[:40]
+
+
+def lib_build_id():
+    """The build id of the library the profiled command loaded (sahara_build_id)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import sahara_amd
+    return sahara_amd.build_id()
 
 
 def main(d, out, txt=None):
@@ -45,6 +54,7 @@ def main(d, out, txt=None):
             e["lds_conflict"] = round(avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_ACTIVE_INST_LDS"], 3)
         res[k] = e
         lines.append(f"{k:16s} " + " ".join(f"{c}={v:.4g}" for c, v in e.items()))
+    res["build_id"] = lib_build_id()
     json.dump(res, open(out, "w"), indent=1)
     print("\n".join(lines))
     if txt:

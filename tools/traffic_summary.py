@@ -23,6 +23,14 @@ def short(n):
     return m.group(1) if m else n[:40]
 
 
+def lib_build_id():
+    """The build id of the library the profiled command loaded (sahara_build_id)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import sahara_amd
+    return sahara_amd.build_id()
+
+
 def main(d, out, txt=None):
     lines = []
     stats = {}
@@ -65,6 +73,7 @@ def main(d, out, txt=None):
         lines.append(f"{k:28s} launches={len(v):3d} avg={avg_us:9.1f} us  FETCH_SIZE={kb/1024/1024:8.3f} GiB/launch "
                      f"-> {b/1e9:7.3f} GB/launch = {b/(avg_us/1e6)/1e9:7.1f} GB/s")
     res["calibration_factor"] = round(factor, 4)
+    res["build_id"] = lib_build_id()
     if os.environ.get("STEPS"):  # timed steps of the profiled command (no warmup): launches per step
         res["steps"] = int(os.environ["STEPS"])
     json.dump(res, open(out, "w"), indent=1)
