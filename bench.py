@@ -211,7 +211,7 @@ def main():
     else:
         packed_call = lambda: sa.search_packed_compact(idx, packed, scheme, edit=edit)  # noqa: E731
     step_stats = {"search_ms": 0.0, "text_ms": 0.0, "locate_ms": 0.0, "sort_ms": 0.0, "seed_ms": 0.0,
-                  "stage_ms": 0.0, "output_ms": 0.0, "search_launches": 0, "text_launches": 0, "text_fallbacks": 0}
+                  "stage_ms": 0.0, "output_ms": 0.0, "search_launches": 0, "text_launches": 0}
     h = None
     last_result = None
     if args.execution != "reference":

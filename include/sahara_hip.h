@@ -94,11 +94,10 @@ typedef struct sahara_stats {
     double   output_ms;          /* sahara_gpu_search: wall time of handing the hits to the host */
     uint64_t text_launches;      /* text-phase kernel launches in the pass */
     uint64_t upload_chunks[3];   /* streamed upload chunks sent at 2 / 4 / 8 bits per symbol */
-    uint64_t text_fallbacks;     /* passes whose one text launch gave up (a wait timed out) and were redone batch by batch */
     uint64_t text_pos_tasks;     /* text tasks that came with their text position from the k-mer table (count=1) */
-    uint64_t text_cycles_idle;   /* shader cycles summed over text-kernel waves: asleep, nothing to do (count=1) */
-    uint64_t text_cycles_grab;   /* ... taking a task chunk from the queues (inside refill; count=1) */
-    uint64_t text_cycles_life;   /* ... each wave's whole life, first instruction to exit (count=1) */
+    uint64_t text_residues;      /* DFS nodes handed to residue launches by waves that ended early (count=1) */
+    uint64_t text_stolen;        /* nodes taken by idle lanes from busy lanes of their wave (count=1) */
+    uint64_t text_residue_launches; /* text-phase launches that ran residues (included in text_launches) */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

@@ -698,7 +698,7 @@ def test_text_phase_many_batches(gpu_device, monkeypatch, batch):
         gpu.run(count=count)
         st = gpu.stats()
         assert np.array_equal(hits_as_rows(gpu.fetch()), want), count
-        assert st["batches"] == nbatch and st["text_fallbacks"] == 0, st
+        assert st["batches"] == nbatch, st
         assert st["text_launches"] >= nbatch, st
     assert np.array_equal(hits_as_rows(sa.search_reads(gpu, reads, scheme)), want)
     c = sa.search_packed_compact(gpu, sa.pack_reads(reads, 6, pinned=True), scheme)

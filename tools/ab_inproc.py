@@ -63,12 +63,10 @@ def main():
             one()
             t = time.perf_counter()
             tm = 0.0
-            fb = 0
             for _ in range(a.steps):
                 nh = one()
                 st = idx.stats()
                 tm += st["text_ms"]
-                fb += st.get("text_fallbacks", 0)
             el = time.perf_counter() - t
             res[name].append(nreads * a.steps / el)
             hits.setdefault(name, nh)
@@ -82,14 +80,9 @@ def main():
                          f" refills {c['text_refills']} cy/iter refill {c['text_cycles_refill'] / it:.0f}"
                          f" step {c['text_cycles_step'] / it:.0f} emit {c['text_cycles_emit'] / it:.0f}"
                          f" count-mode text {c['text_ms']:.2f} ms launches {c['text_launches']} grid {c['text_grid']}"
-                         f" life/wave-ms {c['text_cycles_life'] / max(1, c['text_ms']):.3g}"
-                         f" of life: idle {c['text_cycles_idle'] / max(1, c['text_cycles_life']):.3f}"
-                         f" refill {c['text_cycles_refill'] / max(1, c['text_cycles_life']):.3f}"
-                         f" (grab {c['text_cycles_grab'] / max(1, c['text_cycles_life']):.3f})"
-                         f" step {c['text_cycles_step'] / max(1, c['text_cycles_life']):.3f}"
-                         f" emit {c['text_cycles_emit'] / max(1, c['text_cycles_life']):.3f}")
+                         f" residues/read {c['text_residues'] / nreads:.3f} stolen/read {c['text_stolen'] / nreads:.3f}")
             print(f"round {r} {name:10s} {nreads * a.steps / el / 1e6:8.1f}M reads/s {el * 1e3 / a.steps:7.2f} ms/step "
-                  f"text {tm / a.steps:6.2f} ms hits {nh} fallbacks {fb}{extra}", flush=True)
+                  f"text {tm / a.steps:6.2f} ms hits {nh}{extra}", flush=True)
     base = None
     for name, v in res.items():
         mean = float(np.mean(v))
