@@ -604,15 +604,27 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         const uint64_t q0 = bstart[b], nb = bstart[b + 1] - q0;
         c->mark("finish", b);
-        // the batch's counters, copied on sC (a copy on sB would wait for CU
-        // slots between two text phases)
+        // After the text phase, on sC (work on sB would wait for CU slots
+        // between two text phases): the per-query row counts are scanned into
+        // segment offsets right away, and one small kernel then writes the
+        // batch's counters, its row total and its long-segment counts into
+        // pinned host memory: one host round trip per batch, not two (until
+        // r5 the counters went up first, and the scan waited for the host to
+        // check them). A batch whose buffers overflowed is redone anyway, so
+        // its scan is wasted work, not wrong work.
         SH_HIP(hipStreamWaitEvent(sC, sl.textDone, 0));
-        SH_HIP(hipMemcpyAsync(c->pinned + b * 16, sl.small.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, sC));
+        SH_HIP(hipEventRecord(c->ev[2], sC));
+        SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
+        c->partial.reserve(scanTiles((uint32_t)nb));
+        querySegments(sl.qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4, c->huge.ptr,
+                      c->small.ptr + 5, sC);
+        uint32_t* pr = c->pinned + b * 16;
+        launchBatchTotals(sl.small.ptr, c->qoff.ptr + nb, c->small.ptr + 4, pr, sC);
         SH_HIP(hipEventRecord(sleepy ? c->evSleep[0] : c->ev[6], sC));
         if (sleepy) waitSleepy(c->evSleep[0], pollUs);
         else SH_HIP(hipEventSynchronize(c->ev[6]));
-        c->mark("text done", b);
-        const uint32_t* hs = c->pinned + b * 16;
+        c->mark("text done, rows", b);
+        const uint32_t* hs = pr;
         float ms = 0;
         if (sl.seedsInParts) {  // the seed launches, not the upload waits between them
             SH_HIP(hipEventElapsedTime(&ms, sl.fmStart, sl.seedDone0));
@@ -641,8 +653,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             // thread; they grow after the pass, before the serial re-run)
             if (hs[2] & 8u) growCap(serial ? c->taskCap : seenTask, hs[4]);
             if (hs[2] & 2u) growCap(serial ? c->hitCap : seenHit, hs[1]);
-            overflow = true;
-            SH_HIP(hipMemsetAsync(sl.qcnt.ptr, 0, (nb + 1) * sizeof(uint32_t), sC));  // the re-run counts again
+            overflow = true;  // (the scan zeroed the slot's per-query counts)
             resetSlot(sl, sC);
             return false;
         }
@@ -650,24 +661,9 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         // the capacity without having written there (no overflow flag)
         const uint64_t nh = std::min<uint64_t>(hs[1], c->hitCap);
         S.cursors += hs[3];
-        SH_HIP(hipEventRecord(c->ev[2], sC));
-        SH_HIP(hipMemsetAsync(c->small.ptr, 0, 8 * sizeof(uint32_t), sC));
-        c->partial.reserve(scanTiles((uint32_t)nb));
-        querySegments(sl.qcnt.ptr, (uint32_t)nb, c->qoff.ptr, c->partial.ptr, c->big.ptr, c->small.ptr + 4, c->huge.ptr,
-                      c->small.ptr + 5, sC);
-        uint32_t* pr = c->pinned + b * 16;
-        SH_HIP(hipMemcpyAsync(pr + 8, c->qoff.ptr + nb, 8, hipMemcpyDeviceToHost, sC));
-        SH_HIP(hipMemcpyAsync(pr + 10, c->small.ptr + 4, 8, hipMemcpyDeviceToHost, sC));  // long, huge segments
-        if (sleepy) {
-            SH_HIP(hipEventRecord(c->evSleep[1], sC));
-            waitSleepy(c->evSleep[1], pollUs);
-        } else {
-            SH_HIP(hipStreamSynchronize(sC));
-        }
         uint64_t rows = 0;
         std::memcpy(&rows, pr + 8, 8);
         const uint32_t nbig2[2] = {pr[10], pr[11]};
-        c->mark("rows", b);
         if (rows >= (1ull << 32)) throw Error("more than 2^32 located hits in one batch of patterns");
         const uint32_t nbig = nbig2[0], nhuge = nbig2[1];
         const uint32_t* hugeList = c->huge.ptr;

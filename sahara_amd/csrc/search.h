@@ -201,6 +201,11 @@ uint32_t scanTiles(uint32_t nq);  // u64 partials querySegments needs
 void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partial, uint32_t* big, uint32_t* nbig,
                    uint32_t* huge, uint32_t* nhuge, hipStream_t st);
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st);
+// a batch's totals into pinned host memory in one launch: out[0..8) = the
+// slot's counters (small), out[8..10) = the row total (u64), out[10..12) =
+// the long / huge segment counts
+void launchBatchTotals(const uint32_t* small, const uint64_t* rowTotal, const uint32_t* segCounts, uint32_t* out,
+                       hipStream_t st);
 size_t bigSortTempBytes(uint64_t rows, uint32_t nbig);
 // long segments (> 64 rows, listed in big) are sorted in LDS, huge ones
 // (> 2048, listed in huge) by the segmented radix sort

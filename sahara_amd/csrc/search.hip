@@ -2197,6 +2197,20 @@ void querySegments(uint32_t* qcnt, uint32_t nq, uint64_t* qoff, uint64_t* partia
 
 uint32_t scanTiles(uint32_t nq) { return (nq + 1 + kScanTile - 1) / kScanTile; }
 
+__global__ void kBatchTotals(const uint32_t* __restrict__ small, const uint64_t* __restrict__ rowTotal,
+                             const uint32_t* __restrict__ segCounts, uint32_t* __restrict__ out) {
+    const uint32_t i = threadIdx.x;
+    if (i < 8) out[i] = small[i];
+    else if (i < 10) out[i] = (uint32_t)(*rowTotal >> (32 * (i - 8)));
+    else if (i < 12) out[i] = segCounts[i - 10];
+}
+
+void launchBatchTotals(const uint32_t* small, const uint64_t* rowTotal, const uint32_t* segCounts, uint32_t* out,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(kBatchTotals, dim3(1), dim3(64), 0, st, small, rowTotal, segCounts, out);
+    SH_HIP(hipGetLastError());
+}
+
 void launchLocate(const LocateArgs& a, bool count, hipStream_t st) {
     if (a.nhits == 0) return;
     const uint64_t blocks = std::min<uint64_t>((a.nhits + 255) / 256, 65536);
