@@ -95,9 +95,7 @@ typedef struct sahara_stats {
     uint64_t text_launches;      /* text-phase kernel launches in the pass */
     uint64_t upload_chunks[3];   /* streamed upload chunks sent at 2 / 4 / 8 bits per symbol */
     uint64_t text_pos_tasks;     /* text tasks that came with their text position from the k-mer table (count=1) */
-    uint64_t text_residues;      /* DFS nodes handed to residue launches by waves that ended early (count=1) */
     uint64_t text_stolen;        /* nodes taken by idle lanes from busy lanes of their wave (count=1) */
-    uint64_t text_residue_launches; /* text-phase launches that ran residues (included in text_launches) */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

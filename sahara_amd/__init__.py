@@ -78,8 +78,7 @@ class Stats(C.Structure):
                 ("seed_ms", C.c_double), ("text_steps", C.c_uint64), ("stage_ms", C.c_double),
                 ("output_ms", C.c_double), ("text_launches", C.c_uint64),
                 ("upload_chunks", C.c_uint64 * 3), ("text_pos_tasks", C.c_uint64),
-                ("text_residues", C.c_uint64), ("text_stolen", C.c_uint64),
-                ("text_residue_launches", C.c_uint64)]
+                ("text_stolen", C.c_uint64)]
 
     def as_dict(self):
         return {n: (list(v) if isinstance(v, C.Array) else v) for n, v in

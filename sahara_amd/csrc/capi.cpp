@@ -208,7 +208,7 @@ Ctx* newCtx(int device) {
                               &sl.textStart, &sl.textDone, &sl.free, &sl.textMid0, &sl.textMid1})
             SH_HIP(hipEventCreate(e));
         sl.small.reserve(8);
-        sl.queues.reserve(1024);
+        sl.queues.reserve(768);
     }
     for (void*& p : c->outStage) SH_HIP(hipHostMalloc(&p, Ctx::kOutChunk));
     c->small.reserve(8);

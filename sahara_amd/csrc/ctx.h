@@ -311,11 +311,6 @@ private:
 // C5, C2 within noise (profiles/r05_text_steps_ab.txt).
 constexpr uint32_t kTextStepsDefault = 2;
 constexpr uint32_t kRefillAtDefault = 8;
-// A text wave whose task queue is dry hands its remaining DFS nodes to the
-// batch's residue launch once fewer than this many of its lanes are busy
-// (SAHARA_DUMP_BELOW; 0: never, the wave runs them to the end).
-constexpr uint32_t kDumpBelowDefault = 32;
-
 struct Ctx {
     int device = 0;
     Placement place;                      // NUMA node of the device; the context's threads run there
@@ -437,12 +432,6 @@ struct Ctx {
         std::vector<uint64_t> nFirst;
     } up;
     DevBuf<uint32_t> nList;
-    // the text phase's residue lists (search.h ResidueList): one record
-    // buffer (the text launches run one at a time on stB), a list per slot
-    // (its count is the slot's small[7])
-    DevBuf<uint4> resid;
-    DevBuf<ResidueList> residLists;
-    ResidueList residHost[kSlots] = {};
     // the packed reads' N list last checked whole (strictly ascending): a
     // stream processed shard by shard is checked once, not once per shard
     const uint64_t* nPosChecked = nullptr;

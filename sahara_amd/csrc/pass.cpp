@@ -83,8 +83,7 @@ void run(Ctx* c, bool count) {
                   &sahara_stats::text_active, &sahara_stats::text_refills, &sahara_stats::text_cycles_refill,
                   &sahara_stats::text_cycles_step, &sahara_stats::text_cycles_emit, &sahara_stats::text_compare_steps,
                   &sahara_stats::text_steps, &sahara_stats::text_launches,
-                  &sahara_stats::text_pos_tasks, &sahara_stats::text_residues, &sahara_stats::text_stolen,
-                  &sahara_stats::text_residue_launches})
+                  &sahara_stats::text_pos_tasks, &sahara_stats::text_stolen})
                 T.*f += S.*f;
             for (double sahara_stats::*f : {&sahara_stats::search_ms, &sahara_stats::locate_ms, &sahara_stats::sort_ms,
                                             &sahara_stats::text_ms, &sahara_stats::seed_ms})
@@ -349,7 +348,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // here for the first use, after its locate (finish) for the next
     auto resetSlot = [&](Ctx::Slot& sl, hipStream_t s) {
         SH_HIP(hipMemsetAsync(sl.small.ptr, 0, 8 * sizeof(uint32_t), s));
-        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 1024 * sizeof(uint32_t), s));
+        SH_HIP(hipMemsetAsync(sl.queues.ptr, 0, 768 * sizeof(uint32_t), s));
         SH_HIP(hipEventRecord(sl.free, s));
     };
     for (auto& sl : c->slot) resetSlot(sl, sA);
@@ -493,29 +492,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     // 0.890; C3 948M -> 1045M / 1056M, 0.787 -> 0.900
     uint32_t stealAt = 8;
     if (const char* e = std::getenv("SAHARA_STEAL_AT")) stealAt = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-    // Residues: a wave whose task queue is dry and which has
-    // fewer than dumpBelow busy lanes writes its remaining DFS nodes to the
-    // slot's residue list and ends, instead of running them at that width to
-    // the launch's end; one more launch of the text kernel per batch (the
-    // residue launch, which dumps nothing) runs them at full width. The list
-    // holds every node the batch's (at most two) launches can hand over:
-    // 1 + stackCap per lane each.
-    uint32_t dumpBelow = kDumpBelowDefault;
-    if (const char* e = std::getenv("SAHARA_DUMP_BELOW")) dumpBelow = (uint32_t)std::max(0, std::min(64, std::atoi(e)));
-    if (!split) dumpBelow = 0;
-    const uint32_t residCap = dumpBelow ? 2u * textBlocks * 256u * (textStack + 1u) : 0u;
-    if (dumpBelow) {
-        c->resid.reserve(residCap);
-        c->residLists.reserve(Ctx::kSlots);
-        bool changed = false;
-        for (int i = 0; i < Ctx::kSlots; ++i) {
-            const ResidueList r{c->resid.ptr, c->slot[i].small.ptr + 7, residCap, 0u};
-            changed = changed || std::memcmp(&r, &c->residHost[i], sizeof(r)) != 0;
-            c->residHost[i] = r;
-        }
-        if (changed)
-            SH_HIP(hipMemcpy(c->residLists.ptr, c->residHost, Ctx::kSlots * sizeof(ResidueList), hipMemcpyHostToDevice));
-    }
     auto issueText = [&](uint64_t b) {
         Ctx::Slot& sl = c->slot[b % Ctx::kSlots];
         // one launch per batch (kSearchTextBatch) after its FM phase; the
@@ -558,8 +534,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.rank = sl.rank.ptr;
             t.probe = probe ? 1u : 0u;
             t.isFirst = b == 0 ? 1u : 0u;
-            t.dumpBelow = dumpBelow;
-            t.residues = c->residLists.ptr + b % Ctx::kSlots;
             if (split0) {
                 t.taskCount = sl.small.ptr + 5;
                 launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);
@@ -573,18 +547,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             }
             launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);
             ++S.text_launches;
-            if (dumpBelow) {  // the residue launch: the nodes the launches above handed over
-                t.tasks = c->resid.ptr;
-                t.taskBegin = nullptr;
-                t.taskCount = sl.small.ptr + 7;
-                t.taskCap = residCap;
-                t.work = sl.queues.ptr + 768;
-                t.dumpBelow = 0;
-                t.isFirst = 0;
-                launchTextBatch(t, sigma, c->edit, count, textBlocks, textLds, sB);
-                ++S.text_launches;
-                ++S.text_residue_launches;
-            }
         }
         SH_HIP(hipEventRecord(sl.textDone, sB));
     };
@@ -885,8 +847,8 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
                      h[36] / 100.0 / std::max<double>(1, S.text_grid * 4.0), (h[38] - h[33]) / 100.0,
                      (h[39] - h[33]) / 100.0, h[31], h[30] / 100.0 / std::max<double>(1, (double)h[31]));
         std::fprintf(stderr, "text iterations before / after: %llu (busy lanes %.1f) / %llu (busy lanes %.1f); "
-                     "nodes stolen %llu, handed to residue launches %llu\n",
-                     h[40], h[41] / std::max(1.0, (double)h[40]), h[42], h[43] / std::max(1.0, (double)h[42]), h[45], h[44]);
+                     "nodes stolen %llu\n",
+                     h[40], h[41] / std::max(1.0, (double)h[40]), h[42], h[43] / std::max(1.0, (double)h[42]), h[45]);
         std::fprintf(stderr, "text wall per iteration (us) before: refill %.2f steps+emit %.2f; after: refill %.2f steps+emit %.2f\n",
                      h[46] / 100.0 / std::max(1.0, (double)h[40]), h[47] / 100.0 / std::max(1.0, (double)h[40]),
                      h[48] / 100.0 / std::max(1.0, (double)h[42]), h[49] / 100.0 / std::max(1.0, (double)h[42]));
@@ -911,7 +873,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
         S.text_compare_steps = h[14];
         S.text_steps = h[15];
         S.text_pos_tasks = h[16];
-        S.text_residues = h[44];
         S.text_stolen = h[45];
         if (std::getenv("SAHARA_DUMP_COUNTERS")) {  // (profiling hook: the raw count-mode counters)
             for (uint32_t i = 0; i < kCounters; ++i) std::fprintf(stderr, "%s%llu", i ? " " : "counters ", h[i]);

@@ -120,23 +120,6 @@ struct TextBatchArgs {
     uint32_t* rank;
     uint32_t probe;          // (count mode) wave lives on the wall clock into counters [30..49] ...
     uint32_t isFirst;        // ... for the pass's first launch only
-    // Residues (dumpBelow 0: off): once the task queue is dry and fewer than
-    // dumpBelow lanes of a wave are busy, the wave writes its lanes' remaining
-    // DFS nodes (the node in hand and the stack entries) as positioned task
-    // records to the residue list and ends; a residue launch of the same
-    // kernel runs them at full lane width (pass.cpp). The list's address is
-    // read from device memory when a wave dumps (kernel arguments would stay
-    // in SGPRs across the whole loop).
-    uint32_t dumpBelow;
-    const struct ResidueList* residues;
-};
-// A residue list: its records, their capacity (at least 1 + stackCap per lane
-// of the launches that dump into it) and the count, bumped by the dumping waves.
-struct ResidueList {
-    uint4* recs;
-    uint32_t* count;
-    uint32_t cap;
-    uint32_t pad;
 };
 
 struct LocateArgs {

@@ -880,9 +880,8 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
     SlotRange hitSlots;
     uint32_t rankSlot = ~0u, rankVal = 0;  // the lane's last hit whose rank is not stored yet
     uint2 cur = make_uint2(0, 0);
-    bool dump = false;  // the wave hands its remaining nodes to the residue launch
     uint64_t cNodes = 0, tIter = 0, tActive = 0, tRefill = 0, cCmp = 0, cSteps = 0;
-    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0, cSteal = 0, cDump = 0;
+    uint64_t cyRefill = 0, cyStep = 0, cyEmit = 0, t0 = 0, cSteal = 0;
     // (count mode, a.probe) the first launch's wave lives on the wall clock:
     // the queue seen drained, iterations and busy lanes before / after it.
     // Only in count mode: it costs the product kernel 14 VGPRs and 12 SGPR spills.
@@ -944,7 +943,7 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
                 sBase = (t.w >> 24) * m;
                 const uint32_t meta = t.w & 0x00FFFFFFu;
                 const uint32_t pos = meta & 0xFFFFu, e = (meta >> 16) & 0xFu;
-                const uint32_t ca = SC[sBase + min(pos, m - 1u)].y & 0xFFFu;  // (a residue may be a leaf: pos = m)
+                const uint32_t ca = SC[sBase + pos].y & 0xFFFu;
                 const uint32_t K = (SC[sBase + m - 1u].x >> 20) & 0xFu;
                 const uint32_t left = ca + (K > e ? K - e : 0u);  // text the left side can still consume
                 wb = x > left ? x - left : 0u;  // window start
@@ -1012,13 +1011,7 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
                 }
             }
         }
-        // ---- residues: once the queue is dry and fewer than a.dumpBelow lanes
-        // of the wave are busy, the wave's last nodes would run at that width
-        // to the launch's end (the launch's tail: DESIGN.md §3.4). Instead the
-        // wave hands them to the residue launch (after the loop) and ends.
-        const uint64_t busyMask = __ballot(have || sp > 0);
-        dump = a.dumpBelow && qDone && !haveNext && qNext >= qEnd && busyMask && __popcll(busyMask) < a.dumpBelow;
-        if (dump || !__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
+        if (!__any(have || sp > 0 || (!exhausted && (!qDone || haveNext || qNext < qEnd)))) break;  // nothing left
         if (kProbe && a.probe) {
             if (qDone && lane == 0 && wDrain[threadIdx.x >> 6] == 0) wDrain[threadIdx.x >> 6] = wall_clock64();
             const uint32_t act = (uint32_t)__popcll(__ballot(have || sp > 0));
@@ -1268,34 +1261,6 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
         atomicAdd(a.counters + 48, (unsigned long long)pwPostA);
         atomicAdd(a.counters + 49, (unsigned long long)pwPostB);
     }
-    if (dump) {
-        // Each lane's node in hand and its stack entries become positioned
-        // task records (text position of the span, |t|, pattern, meta |
-        // search << 24: the FM phase's task format, so the residue launch's
-        // task start rebuilds the same node). A node's subtree is the same
-        // DFS wherever it runs, so the hits are too.
-        const uint32_t n = (have ? 1u : 0u) + sp;
-        uint32_t incl = n;  // inclusive prefix sum of n over the wave's lanes
-#pragma unroll
-        for (uint32_t off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (lane >= off) incl += y;
-        }
-        const ResidueList R = *a.residues;
-        uint32_t base = 0;
-        if (lane == 63) base = atomicAdd(R.count, incl);
-        base = __shfl(base, 63) + incl - n;
-        uint32_t srch = 0;  // sBase = srch * m
-        for (uint32_t t = m; t <= sBase; t += m) ++srch;
-        auto put = [&](uint32_t o, const uint2& v) {
-            const uint32_t xo = v.x & 0xFFFFu, yo = v.x >> 16;
-            if (o < R.cap) R.recs[o] = make_uint4(wb + xo, (yo - xo) | kTaskPos, pid, v.y | (srch << 24));
-            else atomicOr(a.flags, 8u);  // (cannot happen: residCap covers every lane's bound)
-        };
-        if (have) put(base++, cur);
-        for (uint32_t d = 0; d < sp; ++d) put(base + d, stackGet(d));
-        if (COUNT) cDump += n;
-    }
     hitSlots.close(lane, a.hits, a.hitCap);
     if (rankSlot != ~0u) a.rank[rankSlot] = rankVal;
     if (filled) atomicAdd(a.filled, filled);  // per-lane counts
@@ -1313,7 +1278,6 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
         atomicAdd(a.counters + 14, (unsigned long long)cCmp);
         atomicAdd(a.counters + 15, (unsigned long long)cSteps);
         if (cSteal) atomicAdd(a.counters + 45, (unsigned long long)cSteal);
-        if (cDump) atomicAdd(a.counters + 44, (unsigned long long)cDump);
     }
 }
 
