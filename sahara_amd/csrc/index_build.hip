@@ -18,6 +18,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+
 #include <cstdlib>
 #include <cstring>
 
@@ -525,6 +528,39 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
     if (n >= 0xFFFFFFFEull) throw Error("text too long for 32-bit rows");
     setCommon(I, sigma, n, recLens, nrec, rate, st);
+    // SAHARA_TIMING: where the load's time goes (stderr), from events between
+    // its steps and the host clock
+    struct Phases {
+        bool on = std::getenv("SAHARA_TIMING") != nullptr;
+        hipStream_t st;
+        std::vector<std::pair<const char*, hipEvent_t>> ev;
+        std::vector<double> host;
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+        void operator()(const char* what) {
+            if (!on) return;
+            hipEvent_t e;
+            SH_HIP(hipEventCreate(&e));
+            SH_HIP(hipEventRecord(e, st));
+            ev.emplace_back(what, e);
+            host.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+        void report() {
+            if (!on || ev.empty()) return;
+            SH_HIP(hipEventSynchronize(ev.back().second));
+            std::fprintf(stderr, "[sahara] index load (ms, device | host issue):");
+            for (size_t i = 1; i < ev.size(); ++i) {
+                float ms = 0;
+                SH_HIP(hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second));
+                std::fprintf(stderr, " %s %.1f | %.1f", ev[i].first, ms, host[i] - host[i - 1]);
+            }
+            std::fprintf(stderr, "\n");
+        }
+        ~Phases() {
+            for (auto& x : ev) (void)hipEventDestroy(x.second);
+        }
+    } phase{};
+    phase.st = st;
+    phase("start");
     const uint64_t nb = n / 64 + 1;
     DevBuf<uint8_t> bwt;
     DevBuf<uint64_t> sampled;
@@ -533,14 +569,19 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     uint64_t totals[6], totalsR[6];
     SH_HIP(hipMemcpyAsync(sampled.ptr, sampledBits, nb * 8, hipMemcpyHostToDevice, st));
     SH_HIP(hipMemcpyAsync(bwt.ptr, bwtF, n, hipMemcpyHostToDevice, st));
+    phase("bwtF up");
     buildLines(bwt.ptr, n, sampled.ptr, I.occF, totals, st);
+    phase("occF");
     if (totals[5] != nsamples) throw Error("sampled bitvector and sample count disagree");
     setC(I, totals, nrec);
     I.nsamples = nsamples;
     I.samples.reserve(std::max<uint64_t>(nsamples, 1));
     SH_HIP(hipMemcpyAsync(I.samples.ptr, samples, nsamples * 4, hipMemcpyHostToDevice, st));
+    phase("samples up");
     SH_HIP(hipMemcpyAsync(bwt.ptr, bwtR, n, hipMemcpyHostToDevice, st));
+    phase("bwtR up");
     buildLines(bwt.ptr, n, nullptr, I.occR, totalsR, st);
+    phase("occR");
     for (int c = 0; c < 5; ++c)
         if (totalsR[c] != totals[c]) throw Error("forward/reverse BWT symbol counts differ");
     // full SA + text from the sampled SA by bounded LF walks
@@ -555,6 +596,7 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     hipLaunchKernelGGL(kDensify, dim3(gridFor(n)), dim3(kTB), 0, st, I.occF.ptr, n, I.samples.ptr, dC.ptr, rate,
                        I.saFull.ptr, bwt.ptr, err.ptr);
     SH_HIP(hipGetLastError());
+    phase("densify");
     I.text3.reserve(text3Blocks(n));
     SH_HIP(hipMemsetAsync(I.text3.ptr, 0, text3Blocks(n) * sizeof(uint4), st));
     hipLaunchKernelGGL(kPackText, dim3(gridFor((n + 31) / 32)), dim3(kTB), 0, st, bwt.ptr, n, I.text3.ptr);
@@ -562,8 +604,11 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     unsigned int herr = 0;
     SH_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, st));
     SH_HIP(hipStreamSynchronize(st));
+    phase("text");
     if (herr) throw Error("SA densification walk exceeded its bound (inconsistent .idx samples)");
     if (withKmer) buildKmerTable(I, kmerDepth(n), st);
+    phase("kmer");
+    phase.report();
 }
 
 uint32_t kmerDepth(uint64_t n, uint32_t tables) {
