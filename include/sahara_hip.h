@@ -96,6 +96,7 @@ typedef struct sahara_stats {
     uint64_t upload_chunks[3];   /* streamed upload chunks sent at 2 / 4 / 8 bits per symbol */
     uint64_t text_pos_tasks;     /* text tasks that came with their text position from the k-mer table (count=1) */
     uint64_t text_stolen;        /* nodes taken by idle lanes from busy lanes of their wave (count=1) */
+    uint64_t reserved[8];        /* zero: room for counters added later without changing the struct's size */
 } sahara_stats;
 
 const char* sahara_gpu_last_error(void);

@@ -78,7 +78,7 @@ class Stats(C.Structure):
                 ("seed_ms", C.c_double), ("text_steps", C.c_uint64), ("stage_ms", C.c_double),
                 ("output_ms", C.c_double), ("text_launches", C.c_uint64),
                 ("upload_chunks", C.c_uint64 * 3), ("text_pos_tasks", C.c_uint64),
-                ("text_stolen", C.c_uint64)]
+                ("text_stolen", C.c_uint64), ("reserved", C.c_uint64 * 8)]
 
     def as_dict(self):
         return {n: (list(v) if isinstance(v, C.Array) else v) for n, v in
@@ -181,8 +181,10 @@ def lib():
 
 
 def build_id():
-    """The library's build id (sahara_build_id: SHA-256 prefix of its sources, tools/build_id.py)."""
-    return lib().sahara_build_id().decode()
+    """The library's build id (sahara_build_id: SHA-256 prefix of its sources, tools/build_id.py);
+    "unknown" for an older build loaded through SAHARA_HIP_LIB (A/B runs)."""
+    f = getattr(lib(), "sahara_build_id", None)
+    return f().decode() if f else "unknown"
 
 
 def _check(rc):
