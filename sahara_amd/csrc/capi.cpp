@@ -226,8 +226,14 @@ Ctx* ctxOf(void* p) {
 
 // an .idx image (one part or several) -> a context holding every part
 Ctx* openImage(int device, const uint8_t* buf, size_t bytes) {
+    const auto t0 = std::chrono::steady_clock::now();
+    auto since = [&t0] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     const std::vector<IdxParts> parts = parseIdxAll(buf, bytes);
+    const double tParse = since();
     std::unique_ptr<Ctx> c(newCtx(device));
+    const double tCtx = since();
+    if (std::getenv("SAHARA_TIMING"))  // (the parts' own steps follow from buildFromParts)
+        std::fprintf(stderr, "[sahara] open: parse %.1f ms, context %.1f ms\n", tParse, tCtx - tParse);
     uint64_t rec0 = 0, nmax = 0;
     c->partRec0.clear();
     for (size_t p = 0; p < parts.size(); ++p) {

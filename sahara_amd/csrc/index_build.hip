@@ -264,30 +264,61 @@ __device__ __forceinline__ uint32_t rankAll(const OccLine& L, uint32_t row, uint
 // every sampled row seeds a backward LF walk that stops at the next sampled
 // row or at a record start, writing SA[row] = pos and T[pos-1] = BWT[row] on
 // the way ('$' entries of T stay 0). Each row is visited by exactly one walk.
-__global__ void kDensify(const OccLine* __restrict__ occ, uint64_t N, const uint32_t* __restrict__ samples,
-                         const uint64_t* __restrict__ C, uint32_t rate, uint32_t* __restrict__ sa,
-                         uint8_t* __restrict__ T, unsigned int* __restrict__ err) {
-    for (uint64_t r0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r0 < N;
-         r0 += (uint64_t)gridDim.x * blockDim.x) {
-        const OccLine& L0 = occ[r0 >> 6];
-        const uint32_t o0 = (uint32_t)(r0 & 63);
-        const bool sampled = (L0.sampled >> o0) & 1ull;
-        if (!sampled) continue;
-        uint64_t pos = samples[L0.srank + __popcll(L0.sampled & lowMask(o0))];
-        uint32_t row = (uint32_t)r0;
-        sa[row] = (uint32_t)pos;
-        for (uint32_t step = 0;; ++step) {
-            if (step > rate) { atomicOr(err, 1u); break; }
-            const OccLine& L = occ[row >> 6];
-            const uint32_t c = symAt(L.plane, row & 63u);
-            if (pos == 0 || c == 0) break;  // record start: the '$' before it is sampled
-            T[pos - 1] = (uint8_t)c;
-            row = (uint32_t)C[c] + rankAll(L, row, c);
-            --pos;
-            const OccLine& L2 = occ[row >> 6];
-            if ((L2.sampled >> (row & 63u)) & 1ull) break;
-            sa[row] = (uint32_t)pos;
+// A wave takes 1024 consecutive rows (16 Occ lines), compacts their sampled
+// rows (about 1 in rate) with their text positions into an LDS list, and its
+// lanes then walk one chain each: every lane of the wave has a walk in flight.
+// (A lane per row, r5, left ~4 of 64 lanes walking: 238 ms at 3 Gbp, 12.6 G
+// LF steps/s against the ~50 G random lines/s the gather ceiling allows.)
+constexpr uint32_t kDensifyRows = 1024;  // rows per wave
+__global__ __launch_bounds__(256) void kDensify(const OccLine* __restrict__ occ, uint64_t N,
+                                                const uint32_t* __restrict__ samples, const uint64_t* __restrict__ C,
+                                                uint32_t rate, uint32_t* __restrict__ sa, uint8_t* __restrict__ T,
+                                                unsigned int* __restrict__ err) {
+    __shared__ uint2 list[4][kDensifyRows];  // (row, text position) of the wave's sampled rows
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t nblk = (N + kDensifyRows - 1) / kDensifyRows;
+    for (uint64_t blk = (uint64_t)blockIdx.x * 4 + w; blk < nblk; blk += (uint64_t)gridDim.x * 4) {
+        // lane l looks at rows [16 l, 16 l + 16) of the block: a quarter of one line
+        const uint64_t r16 = blk * kDensifyRows + 16u * lane;
+        uint32_t bits = 0, k0 = 0;
+        if (r16 < N) {
+            const OccLine& L = occ[r16 >> 6];
+            const uint32_t o = (uint32_t)(r16 & 63u);
+            bits = (uint32_t)(L.sampled >> o) & 0xFFFFu;
+            if (r16 + 16 > N) bits &= (1u << (uint32_t)(N - r16)) - 1u;
+            k0 = L.srank + (uint32_t)__popcll(L.sampled & lowMask(o));  // the first one's sample index
         }
+        const uint32_t cnt = (uint32_t)__popc(bits);
+        uint32_t incl = cnt;  // inclusive prefix over the wave's lanes
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        for (uint32_t at = incl - cnt, k = k0; bits; bits &= bits - 1u, ++at, ++k)
+            list[w][at] = make_uint2((uint32_t)(r16 + (uint32_t)__builtin_ctz(bits)), samples[k]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t j = lane; j < total; j += 64) {
+            uint32_t row = list[w][j].x;
+            uint64_t pos = list[w][j].y;
+            sa[row] = (uint32_t)pos;
+            for (uint32_t step = 0;; ++step) {
+                if (step > rate) { atomicOr(err, 1u); break; }
+                const OccLine& L = occ[row >> 6];
+                const uint32_t c = symAt(L.plane, row & 63u);
+                if (pos == 0 || c == 0) break;  // record start: the '$' before it is sampled
+                T[pos - 1] = (uint8_t)c;
+                row = (uint32_t)C[c] + rankAll(L, row, c);
+                --pos;
+                const OccLine& L2 = occ[row >> 6];
+                if ((L2.sampled >> (row & 63u)) & 1ull) break;
+                sa[row] = (uint32_t)pos;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the list is reused for the next block
     }
 }
 
@@ -562,7 +593,7 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     phase.st = st;
     phase("start");
     const uint64_t nb = n / 64 + 1;
-    DevBuf<uint8_t> bwt;
+    DevBuf<uint8_t> bwt, bwtRev;
     DevBuf<uint64_t> sampled;
     bwt.reserve(n + 64);
     sampled.reserve(nb);
@@ -578,13 +609,10 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     I.samples.reserve(std::max<uint64_t>(nsamples, 1));
     SH_HIP(hipMemcpyAsync(I.samples.ptr, samples, nsamples * 4, hipMemcpyHostToDevice, st));
     phase("samples up");
-    SH_HIP(hipMemcpyAsync(bwt.ptr, bwtR, n, hipMemcpyHostToDevice, st));
-    phase("bwtR up");
-    buildLines(bwt.ptr, n, nullptr, I.occR, totalsR, st);
-    phase("occR");
-    for (int c = 0; c < 5; ++c)
-        if (totalsR[c] != totals[c]) throw Error("forward/reverse BWT symbol counts differ");
-    // full SA + text from the sampled SA by bounded LF walks
+    // full SA + text from the sampled SA by bounded LF walks (the forward
+    // BWT's buffer becomes the unpacked text); the reverse BWT goes up on a
+    // second stream meanwhile (a pageable copy holds the host thread, not the
+    // device), so its upload hides behind the walks
     I.saFull.reserve(n);
     DevBuf<uint64_t> dC;
     dC.reserve(8);
@@ -592,20 +620,43 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     DevBuf<unsigned int> err;
     err.reserve(1);
     SH_HIP(hipMemsetAsync(err.ptr, 0, 4, st));
-    SH_HIP(hipMemsetAsync(bwt.ptr, 0, n + 64, st));  // reused as the unpacked text
-    hipLaunchKernelGGL(kDensify, dim3(gridFor(n)), dim3(kTB), 0, st, I.occF.ptr, n, I.samples.ptr, dC.ptr, rate,
-                       I.saFull.ptr, bwt.ptr, err.ptr);
+    SH_HIP(hipMemsetAsync(bwt.ptr, 0, n + 64, st));
+    hipLaunchKernelGGL(kDensify, dim3(gridFor((n + kDensifyRows - 1) / kDensifyRows * 64)), dim3(kTB), 0, st,
+                       I.occF.ptr, n, I.samples.ptr, dC.ptr, rate, I.saFull.ptr, bwt.ptr, err.ptr);
     SH_HIP(hipGetLastError());
     phase("densify");
     I.text3.reserve(text3Blocks(n));
     SH_HIP(hipMemsetAsync(I.text3.ptr, 0, text3Blocks(n) * sizeof(uint4), st));
     hipLaunchKernelGGL(kPackText, dim3(gridFor((n + 31) / 32)), dim3(kTB), 0, st, bwt.ptr, n, I.text3.ptr);
     SH_HIP(hipGetLastError());
+    phase("text");
+    {
+        struct Side {  // the reverse BWT's upload stream and the event st waits on
+            hipStream_t s = nullptr;
+            hipEvent_t e = nullptr;
+            ~Side() {
+                if (e) (void)hipEventDestroy(e);
+                if (s) (void)hipStreamDestroy(s);
+            }
+        } side;
+        SH_HIP(hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking));
+        SH_HIP(hipEventCreateWithFlags(&side.e, hipEventDisableTiming));
+        bwtRev.reserve(n + 64);
+        SH_HIP(hipMemcpyAsync(bwtRev.ptr, bwtR, n, hipMemcpyHostToDevice, side.s));
+        SH_HIP(hipEventRecord(side.e, side.s));
+        SH_HIP(hipStreamWaitEvent(st, side.e, 0));
+        phase("bwtR up (beside the walks)");
+        buildLines(bwtRev.ptr, n, nullptr, I.occR, totalsR, st);
+        phase("occR");
+    }
+    for (int c = 0; c < 5; ++c)
+        if (totalsR[c] != totals[c]) throw Error("forward/reverse BWT symbol counts differ");
     unsigned int herr = 0;
     SH_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, st));
     SH_HIP(hipStreamSynchronize(st));
-    phase("text");
     if (herr) throw Error("SA densification walk exceeded its bound (inconsistent .idx samples)");
+    bwtRev.release();
+    bwt.release();
     if (withKmer) buildKmerTable(I, kmerDepth(n), st);
     phase("kmer");
     phase.report();
