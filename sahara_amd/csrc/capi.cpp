@@ -236,11 +236,18 @@ Ctx* openImage(int device, const uint8_t* buf, size_t bytes) {
         std::fprintf(stderr, "[sahara] open: parse %.1f ms, context %.1f ms\n", tParse, tCtx - tParse);
     uint64_t rec0 = 0, nmax = 0;
     c->partRec0.clear();
+    // the image's arrays through the pinned ring (SAHARA_LOAD_RING=0: pageable copies)
+    Ctx* raw = c.get();
+    const HostUpload viaRing = [raw](void* dst, const void* src, size_t n, hipStream_t s) {
+        uploadViaRing(raw, dst, src, n, s);
+    };
+    const char* lr = std::getenv("SAHARA_LOAD_RING");
+    const HostUpload* up = lr && std::atoi(lr) == 0 ? nullptr : &viaRing;
     for (size_t p = 0; p < parts.size(); ++p) {
         const IdxParts& P = parts[p];
         if (p) c->more.emplace_back();
         buildFromParts(partOf(c.get(), (uint32_t)p), P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF,
-                       P.bwtR, P.sampled, P.samples, P.nsamples, c->st, parts.size() == 1);
+                       P.bwtR, P.sampled, P.samples, P.nsamples, c->st, parts.size() == 1, up);
         c->partRec0.push_back(rec0);
         rec0 += P.recLens.size();
         nmax = std::max(nmax, P.n);

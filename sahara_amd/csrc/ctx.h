@@ -459,6 +459,7 @@ struct Ctx {
         TaskGroup group;
     } packJobs[kRingSlots];
     std::thread ringInit;                 // pins the ring (started by newCtx)
+    uint64_t ringLoadNext = 0;            // uploadViaRing's next slot
     bool ringFailed = false;
     DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
     DevBuf<uint8_t> readRaw;              // streamed reads before the reverse-complement interleave
@@ -569,6 +570,9 @@ unsigned hostThreads(const Ctx* c, unsigned cap);
 Ctx* ctxOf(void* p);
 TaskPool& hostPool(Ctx* c);
 Placement placementOfNode(int node);
+// host bytes -> device through the pinned upload ring, copied into it by the
+// pool's threads (an index image's arrays: staging.cpp)
+void uploadViaRing(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st);
 // every pack job posted by the streamed upload is finished (the caller's
 // source buffer is no longer read): before a new call stages, after a failed one
 void drainPacking(Ctx* c);

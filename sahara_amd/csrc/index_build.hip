@@ -555,7 +555,11 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
 
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec, uint32_t rate,
                     const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits, const uint32_t* samples,
-                    uint64_t nsamples, hipStream_t st, bool withKmer) {
+                    uint64_t nsamples, hipStream_t st, bool withKmer, const HostUpload* up) {
+    auto upload = [up](void* dst, const void* src, size_t bytes, hipStream_t s) {
+        if (up) (*up)(dst, src, bytes, s);
+        else SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    };
     if (sigma != 5 && sigma != 6) throw Error("sigma must be 5 (dna4) or 6 (dna5)");
     if (n >= 0xFFFFFFFEull) throw Error("text too long for 32-bit rows");
     setCommon(I, sigma, n, recLens, nrec, rate, st);
@@ -598,8 +602,8 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     bwt.reserve(n + 64);
     sampled.reserve(nb);
     uint64_t totals[6], totalsR[6];
-    SH_HIP(hipMemcpyAsync(sampled.ptr, sampledBits, nb * 8, hipMemcpyHostToDevice, st));
-    SH_HIP(hipMemcpyAsync(bwt.ptr, bwtF, n, hipMemcpyHostToDevice, st));
+    upload(sampled.ptr, sampledBits, nb * 8, st);
+    upload(bwt.ptr, bwtF, n, st);
     phase("bwtF up");
     buildLines(bwt.ptr, n, sampled.ptr, I.occF, totals, st);
     phase("occF");
@@ -607,7 +611,7 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     setC(I, totals, nrec);
     I.nsamples = nsamples;
     I.samples.reserve(std::max<uint64_t>(nsamples, 1));
-    SH_HIP(hipMemcpyAsync(I.samples.ptr, samples, nsamples * 4, hipMemcpyHostToDevice, st));
+    upload(I.samples.ptr, samples, nsamples * 4, st);
     phase("samples up");
     // full SA + text from the sampled SA by bounded LF walks (the forward
     // BWT's buffer becomes the unpacked text); the reverse BWT goes up on a
@@ -642,7 +646,7 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
         SH_HIP(hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking));
         SH_HIP(hipEventCreateWithFlags(&side.e, hipEventDisableTiming));
         bwtRev.reserve(n + 64);
-        SH_HIP(hipMemcpyAsync(bwtRev.ptr, bwtR, n, hipMemcpyHostToDevice, side.s));
+        upload(bwtRev.ptr, bwtR, n, side.s);
         SH_HIP(hipEventRecord(side.e, side.s));
         SH_HIP(hipStreamWaitEvent(st, side.e, 0));
         phase("bwtR up (beside the walks)");

@@ -398,6 +398,33 @@ static void runPieces(TaskPool& P, uint64_t n, const std::function<void(uint64_t
     g.wait();
 }
 
+// An index image's arrays go up through the pinned ring: the pool's threads
+// copy one slot's worth of the source at a time (a mapped .idx faults its
+// pages in on all of them), and the copy engine moves each slot while the next
+// one fills. A pageable hipMemcpyAsync is staged by the runtime on the calling
+// thread alone.
+void uploadViaRing(Ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (c->ringInit.joinable()) c->ringInit.join();
+    if (!c->ring || bytes < Ctx::kRingSlot) {
+        SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+        return;
+    }
+    TaskPool& P = hostPool(c);
+    constexpr size_t kPiece = 1u << 20;  // bytes per pool task
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    for (size_t off = 0; off < bytes; off += Ctx::kRingSlot) {
+        const size_t slot = (size_t)(c->ringLoadNext++ % Ctx::kRingSlots);
+        const size_t len = std::min(Ctx::kRingSlot, bytes - off);
+        SH_HIP(hipEventSynchronize(c->ringEv[slot]));  // the slot's previous copy is done
+        uint8_t* stage = c->ring + slot * Ctx::kRingSlot;
+        runPieces(P, (len + kPiece - 1) / kPiece, [&](uint64_t i) {
+            std::memcpy(stage + i * kPiece, s + off + i * kPiece, std::min(kPiece, len - i * kPiece));
+        });
+        SH_HIP(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, stage, len, hipMemcpyHostToDevice, st));
+        SH_HIP(hipEventRecord(c->ringEv[slot], st));
+    }
+}
+
 static uint64_t chunkCount(const Ctx::Upload& U) { return U.chunk ? (U.rows + U.chunk - 1) / U.chunk : 0; }
 
 // Posts the 2-bit packing of chunk j (the next one not yet posted) to the

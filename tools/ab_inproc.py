@@ -80,7 +80,7 @@ def main():
                          f" refills {c['text_refills']} cy/iter refill {c['text_cycles_refill'] / it:.0f}"
                          f" step {c['text_cycles_step'] / it:.0f} emit {c['text_cycles_emit'] / it:.0f}"
                          f" count-mode text {c['text_ms']:.2f} ms launches {c['text_launches']} grid {c['text_grid']}"
-                         f" stolen/read {c['text_stolen'] / nreads:.3f} carried/read {c['text_carried'] / nreads:.4f}")
+                         f" stolen/read {c['text_stolen'] / nreads:.3f}")
             print(f"round {r} {name:10s} {nreads * a.steps / el / 1e6:8.1f}M reads/s {el * 1e3 / a.steps:7.2f} ms/step "
                   f"text {tm / a.steps:6.2f} ms hits {nh}{extra}", flush=True)
     base = None
