@@ -311,8 +311,6 @@ private:
 // C5, C2 within noise (profiles/r05_text_steps_ab.txt).
 constexpr uint32_t kTextStepsDefault = 2;
 constexpr uint32_t kRefillAtDefault = 8;
-// micro-steps per iteration once a wave's task queue is dry (0: kTextSteps)
-constexpr uint32_t kTextStepsDryDefault = 0;
 struct Ctx {
     int device = 0;
     Placement place;                      // NUMA node of the device; the context's threads run there
@@ -344,7 +342,6 @@ struct Ctx {
     bool locateSA = true;
     uint32_t split = 1;                   // text-phase threshold (rows per interval)
     uint32_t textSteps = kTextStepsDefault;  // text-phase micro-steps per lane per wave iteration
-    uint32_t textStepsDry = kTextStepsDryDefault;  // the same once a wave's task queue is dry (0: textSteps)
     uint32_t refillAt = kRefillAtDefault;    // text-phase batch refill threshold (idle lanes)
 
     // work buffers. Batches rotate over kSlots slots so that seeds and the FM

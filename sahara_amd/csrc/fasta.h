@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -142,6 +143,8 @@ enum class FastaForm { kRanks = 1, kCodes2 = 2 };
 struct FastaData {
     std::vector<uint64_t> offs;     // record i = symbols [offs[i], offs[i+1])
     std::vector<uint8_t> ranks;     // kRanks: one per symbol; kCodes2: (symbols + 3) / 4 bytes
+    uint8_t* codes = nullptr;       // kCodes2 with a CodesAlloc: the codes there instead (the caller's to free)
+    uint64_t codesBytes = 0;        // kCodes2: (symbols + 3) / 4
     std::vector<uint64_t> nPos;     // kCodes2: symbols that are N (dna5), ascending
     uint64_t symbols = 0;
     // the first byte that is no rank of the alphabet, if any
@@ -174,8 +177,19 @@ inline unsigned hostThreads() {
     return std::max(1u, std::min(n, 32u));
 }
 
+// kCodes2 may go straight into a caller's buffer (the page-locked memory the
+// search calls DMA): alloc(bytes) returns it, uninitialised, on a thread of
+// its own while pass 1 runs (bytes >= the codes' size); the result is then in
+// D.codes (the caller's to free) instead of D.ranks. release(p) frees it when
+// the parse fails.
+struct CodesAlloc {
+    std::function<uint8_t*(size_t)> alloc;
+    std::function<void(uint8_t*)> release;
+};
+
 inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, unsigned nt,
-                                    size_t kPiece = 8u << 20, FastaForm form = FastaForm::kRanks) {
+                                    size_t kPiece = 8u << 20, FastaForm form = FastaForm::kRanks,
+                                    const CodesAlloc* codesAlloc = nullptr) {
     const int fd = ::open(path.c_str(), O_RDONLY);
     if (fd < 0) throw std::runtime_error("can not open file " + path);
     struct stat sb {};
@@ -199,6 +213,27 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
         size_t n;
         ~Unmap() { ::munmap(p, n); }
     } unmap{mp, n};
+    const bool codes = form == FastaForm::kCodes2;
+    // the caller's output buffer, allocated beside pass 1 (symbols <= n)
+    struct Alloc {
+        std::thread t;
+        uint8_t* p = nullptr;
+        const CodesAlloc* a = nullptr;
+        uint8_t* take() {  // joined; the buffer is the caller's from here on
+            if (t.joinable()) t.join();
+            uint8_t* q = p;
+            p = nullptr;
+            return q;
+        }
+        ~Alloc() {
+            if (t.joinable()) t.join();
+            if (p && a && a->release) a->release(p);  // (the parse failed)
+        }
+    } ext;
+    if (codes && codesAlloc && codesAlloc->alloc) {
+        ext.a = codesAlloc;
+        ext.t = std::thread([&ext, codesAlloc, n] { ext.p = codesAlloc->alloc(n / 4 + 16); });
+    }
     // pieces of ~kPiece bytes starting at line starts
     std::vector<size_t> bound{0};
     for (size_t p = kPiece; p < n;) {
@@ -242,38 +277,49 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
         c.seq = k;
         if (c.heads.empty()) c.lead = k;
     });
-    // records and offsets
-    std::vector<uint64_t> base(P + 1, 0);
-    for (size_t i = 0; i < P; ++i) base[i + 1] = base[i] + pc[i].seq;
+    // records and offsets: each piece writes its records' offsets at the
+    // prefix-summed record and symbol counts (in parallel: 10M records)
+    std::vector<uint64_t> base(P + 1, 0), rbase(P + 1, 0);
+    for (size_t i = 0; i < P; ++i) {
+        base[i + 1] = base[i] + pc[i].seq;
+        rbase[i + 1] = rbase[i] + pc[i].heads.size();
+    }
     uint64_t lead = 0;  // sequence characters before the first header
     for (size_t i = 0; i < P; ++i) {
         lead += pc[i].lead;
         if (!pc[i].heads.empty()) break;
     }
     if (lead > 0) throw std::runtime_error("malformed FASTA (sequence before header) in " + path);
-    std::vector<uint64_t> heads;
-    for (size_t i = 0; i < P; ++i)
-        for (auto& h : pc[i].heads) {
-            heads.push_back(h.first);
-            D.offs.push_back(base[i] + h.second);
-        }
-    if (heads.empty()) return D;
-    D.offs.push_back(base[P]);
+    if (rbase[P] == 0) {
+        D.codes = ext.take();
+        return D;
+    }
+    D.offs.resize(rbase[P] + 1);
+    parallelFor(nt, P, [&](size_t i) {
+        uint64_t* o = D.offs.data() + rbase[i];
+        for (const auto& h : pc[i].heads) *o++ = base[i] + h.second;
+    });
+    D.offs[rbase[P]] = base[P];
     D.symbols = base[P];
     // pass 2: convert
     uint8_t table[256];
     for (int c = 0; c < 256; ++c) table[c] = charToRank((char)c, sigma);
-    const bool codes = form == FastaForm::kCodes2;
+    uint8_t* out = nullptr;
     if (!codes) {
         D.ranks.resize(base[P]);
     } else {
-        D.ranks.assign((base[P] + 3) / 4, 0);
+        D.codes = ext.take();
+        if (!D.codes) D.ranks.resize((base[P] + 3) / 4);
+        out = D.codes ? D.codes : D.ranks.data();
+        D.codesBytes = (base[P] + 3) / 4;
     }
-    // rank -> 2-bit code (A C G T = 0 1 2 3; N = 0, listed)
-    uint8_t code2[256];
-    for (int r = 0; r < 256; ++r) code2[r] = 0;
-    code2[1] = 0; code2[2] = 1; code2[3] = 2; code2[sigma == 6 ? 5 : 4] = 3;
-    const uint8_t rankN = sigma == 6 ? 4 : 0;  // (the table never gives 0)
+    // per character: bits 0-1 its 2-bit code (A C G T = 0 1 2 3, N and
+    // invalid characters 0), bit 2 N (dna5: listed), bit 3 no rank of the alphabet
+    uint8_t cls[256];
+    for (int c = 0; c < 256; ++c) {
+        const uint8_t r = table[c];
+        cls[c] = r >= sigma ? 8 : (sigma == 6 && r == 4) ? 4 : r == 1 ? 0 : r == 2 ? 1 : r == 3 ? 2 : 3;
+    }
     parallelFor(nt, P, [&](size_t i) {
         Piece& c = pc[i];
         if (!codes) {
@@ -300,32 +346,46 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
         // two bits per symbol: whole bytes inside the piece are stored, the
         // partial first and last bytes (shared with the neighbours) kept in
         // head / tail and or-ed in afterwards
-        uint8_t* const out = D.ranks.data();
         const uint64_t g0 = base[i];
         uint64_t g = g0;
         uint32_t acc = 0;
-        auto flush = [&](uint64_t byteIdx, uint8_t v) {
-            if (byteIdx == g0 / 4 && (g0 & 3u)) c.head = v;
-            else out[byteIdx] = v;
+        auto one = [&](unsigned char ch) {
+            const uint8_t v = cls[ch];
+            if (v & 12u) {
+                if ((v & 8u) && c.badAt == UINT64_MAX) {
+                    c.badAt = g - g0;
+                    c.badChar = ch;
+                }
+                if (v & 4u) c.nPos.push_back(g);
+            }
+            acc |= (uint32_t)(v & 3u) << (2u * (uint32_t)(g & 3u));
+            if ((g & 3u) == 3u) {
+                if (g / 4 == g0 / 4 && (g0 & 3u)) c.head = (uint8_t)acc;
+                else out[g / 4] = (uint8_t)acc;
+                acc = 0;
+            }
+            ++g;
         };
         for (size_t p = bound[i], e = bound[i + 1]; p < e;) {
             const void* nl = std::memchr(b + p, '\n', e - p);
             const size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : e;
             if (b[p] != '>') {
-                for (size_t q = p, qe = lineEnd(p, eol, nl != nullptr); q < qe; ++q, ++g) {
-                    const unsigned char ch = (unsigned char)b[q];
-                    const uint8_t v = table[ch];
-                    if (v >= sigma && c.badAt == UINT64_MAX) {
-                        c.badAt = g - g0;
-                        c.badChar = ch;
+                size_t q = p;
+                const size_t qe = lineEnd(p, eol, nl != nullptr);
+                while (q < qe && (g & 3u)) one((unsigned char)b[q++]);
+                // whole bytes, four characters at a time (g % 4 == 0 here, so
+                // the byte is the piece's own)
+                for (; q + 4 <= qe; q += 4) {
+                    const uint8_t v0 = cls[(unsigned char)b[q]], v1 = cls[(unsigned char)b[q + 1]];
+                    const uint8_t v2 = cls[(unsigned char)b[q + 2]], v3 = cls[(unsigned char)b[q + 3]];
+                    if ((v0 | v1 | v2 | v3) & 12u) {  // N or an invalid character: one at a time
+                        for (size_t j = 0; j < 4; ++j) one((unsigned char)b[q + j]);
+                        continue;
                     }
-                    if (v == rankN) c.nPos.push_back(g);
-                    acc |= (uint32_t)code2[v] << (2u * (uint32_t)(g & 3u));
-                    if ((g & 3u) == 3u) {
-                        flush(g / 4, (uint8_t)acc);
-                        acc = 0;
-                    }
+                    out[g / 4] = (uint8_t)(v0 | (v1 << 2) | (v2 << 4) | (v3 << 6));
+                    g += 4;
                 }
+                while (q < qe) one((unsigned char)b[q++]);
             }
             p = eol + 1;
         }
@@ -335,12 +395,19 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
         }
     });
     if (codes) {
+        // the bytes pieces share were written by none of them: zero, then or in
         uint64_t nN = 0;
         for (size_t i = 0; i < P; ++i) {
             const uint64_t g0 = base[i], g1 = base[i + 1];
             if (g1 == g0) continue;
-            if (g0 & 3u) D.ranks[g0 / 4] |= pc[i].head;
-            if ((g1 & 3u) && !(g1 / 4 == g0 / 4 && (g0 & 3u))) D.ranks[g1 / 4] |= pc[i].tail;
+            if (g0 & 3u) out[g0 / 4] = 0;
+            if (g1 & 3u) out[g1 / 4] = 0;
+        }
+        for (size_t i = 0; i < P; ++i) {
+            const uint64_t g0 = base[i], g1 = base[i + 1];
+            if (g1 == g0) continue;
+            if (g0 & 3u) out[g0 / 4] |= pc[i].head;
+            if ((g1 & 3u) && !(g1 / 4 == g0 / 4 && (g0 & 3u))) out[g1 / 4] |= pc[i].tail;
             nN += pc[i].nPos.size();
         }
         D.nPos.reserve(nN);
@@ -353,7 +420,9 @@ inline FastaData parseFastaParallel(const std::string& path, uint32_t sigma, uns
             D.badRecord = (size_t)(std::upper_bound(D.offs.begin(), D.offs.end(), at) - D.offs.begin()) - 1;
             D.badPos = at - D.offs[D.badRecord];
             D.badChar = pc[i].badChar;
-            const size_t h = heads[D.badRecord] + 1;
+            // the record's header: piece j holds records [rbase[j], rbase[j + 1])
+            const size_t j = (size_t)(std::upper_bound(rbase.begin(), rbase.end(), (uint64_t)D.badRecord) - rbase.begin()) - 1;
+            const size_t h = pc[j].heads[D.badRecord - rbase[j]].first + 1;
             const void* nl = std::memchr(b + h, '\n', n - h);
             size_t eol = nl ? (size_t)(static_cast<const char*>(nl) - b) : n;
             if (eol > h && b[eol - 1] == '\r') --eol;

@@ -294,18 +294,29 @@ int sahara_read_fasta(const char* path, uint32_t sigma, int form, uint32_t threa
         if (sigma != 5 && sigma != 6) throw sahara::Error("sigma must be 5 or 6");
         if (form != 1 && form != 2) throw sahara::Error("form must be 1 (ranks) or 2 (two bits per symbol)");
         const unsigned nt = threads ? threads : sahara_io::hostThreads();
-        sahara_io::FastaData D = sahara_io::parseFastaParallel(
-            path, sigma, nt, 8u << 20, form == 2 ? sahara_io::FastaForm::kCodes2 : sahara_io::FastaForm::kRanks);
-        if (form == 2) {  // page-locked: the packed search calls DMA it as it is
+        // the two-bit form is written straight into page-locked memory (the
+        // packed search calls DMA it as it is), pinned beside the parse's
+        // first pass; pageable if pinning fails (the calls then copy it
+        // through their staging ring)
+        sahara_io::CodesAlloc pinnedCodes;
+        pinnedCodes.alloc = [](size_t bytes) -> uint8_t* {
             void* p = nullptr;
-            if (hipHostMalloc(&p, std::max<size_t>(D.ranks.size(), 1), hipHostMallocPortable) != hipSuccess || !p) {
+            if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocPortable) != hipSuccess || !p) {
                 (void)hipGetLastError();
-                out->data = copyOut(D.ranks);  // pageable: the calls copy it through their staging ring
-            } else {
-                out->data = static_cast<uint8_t*>(p);
-                rememberPinnedFasta(p);
-                if (!D.ranks.empty()) std::memcpy(p, D.ranks.data(), D.ranks.size());
+                return static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes, 1)));
             }
+            rememberPinnedFasta(p);
+            return static_cast<uint8_t*>(p);
+        };
+        pinnedCodes.release = [](uint8_t* p) {
+            if (forgetPinnedFasta(p)) (void)hipHostFree(p);
+            else std::free(p);
+        };
+        sahara_io::FastaData D = sahara_io::parseFastaParallel(
+            path, sigma, nt, 8u << 20, form == 2 ? sahara_io::FastaForm::kCodes2 : sahara_io::FastaForm::kRanks,
+            form == 2 ? &pinnedCodes : nullptr);
+        if (form == 2) {
+            out->data = D.codes ? D.codes : copyOut(D.ranks);
         } else {
             out->data = copyOut(D.ranks);
         }

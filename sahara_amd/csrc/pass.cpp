@@ -232,8 +232,6 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
     const char* eSteps = std::getenv("SAHARA_TEXT_STEPS");
     const char* eRefill = std::getenv("SAHARA_REFILL_AT");
     c->textSteps = eSteps ? (uint32_t)std::max(1L, std::atol(eSteps)) : kTextStepsDefault;
-    const char* eDry = std::getenv("SAHARA_TEXT_STEPS_DRY");
-    c->textStepsDry = eDry ? (uint32_t)std::max(0L, std::min(64L, std::atol(eDry))) : kTextStepsDryDefault;
     c->refillAt = eRefill ? (uint32_t)std::min(64L, std::max(1L, std::atol(eRefill))) : kRefillAtDefault;
     int tbpc = 0;
     // the text phase addresses text and a batch's patterns with 32-bit buffer offsets
@@ -529,7 +527,7 @@ void runPass(Ctx* c, bool count, bool serial, sahara_stats& S, bool& overflow) {
             t.exactWindow = exactWindow ? 1u : 0u;
             t.stackCap = textStack;
             t.tableWords = tableWords;
-            t.steps = c->textSteps | (c->textStepsDry << 16);
+            t.steps = c->textSteps;
             t.refillAt = c->refillAt;
             t.stealAt = stealAt;
             t.qcnt = sl.qcnt.ptr;

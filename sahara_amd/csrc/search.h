@@ -112,8 +112,7 @@ struct TextBatchArgs {
     uint32_t exactWindow;    // 1: the window starts at its first symbol (funnel-shifted copy), else block-aligned
     uint32_t stackCap;       // text DFS stack entries per lane
     uint32_t tableWords;     // LDS words before the lane slots: max(2 * nsearch * m, kTextTableMin)
-    uint32_t steps;          // node expansions per lane between wave-level bookkeeping (low 16 bits; high 16:
-                             // once the wave's task queue is dry, 0 = the same)
+    uint32_t steps;          // node expansions per lane between wave-level bookkeeping
     uint32_t refillAt;       // refill idle lanes once this many are idle
     uint32_t stealAt;        // once the task queue is dry: idle lanes take the bottom stack entry of a busy
                              // lane of their wave (with its window and pattern) once this many are idle (0: off)

@@ -1030,12 +1030,7 @@ __global__ __launch_bounds__(256) void kSearchTextBatch(TextBatchArgs a) {
         // holds it (stalls) until the emission below
         bool leaf = false;
         uint32_t leafStart = 0, leafE = 0;
-        // (a.steps: the count while tasks remain in the low half, once the
-        // wave's queue is dry in the high half, 0 = the same: no refills
-        // come, so more steps per iteration spread its fixed costs)
-        const bool dry = qDone && !haveNext && qNext >= qEnd;
-        const uint32_t nsteps = dry && (a.steps >> 16) ? a.steps >> 16 : a.steps & 0xFFFFu;
-        for (uint32_t step = 0; step < nsteps; ++step) {
+        for (uint32_t step = 0; step < a.steps; ++step) {
             const bool pop = !have && !leaf && sp > 0;
             const uint2 top = stackGet(pop ? sp - 1u : 0u);
             if (pop) { cur = top; --sp; have = true; }

@@ -4,6 +4,8 @@
 // files (CRLF, blank lines, '>' inside lines, empty records, invalid bytes),
 // any piece size and thread count. Built and run by tests/test_fasta_parallel.py.
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <random>
 #include <string>
 
@@ -87,6 +89,20 @@ int main(int argc, char** argv) {
                         if (sigma == 6 && r == 4) wantN.push_back(q);
                     }
                     ok = ok && E.nPos == wantN && E.symbols == D.ranks.size();
+                    // the same into a caller's buffer (uninitialised: filled
+                    // with a pattern first), byte for byte
+                    CodesAlloc A;
+                    A.alloc = [](size_t b) {
+                        uint8_t* p = static_cast<uint8_t*>(std::malloc(b));
+                        std::memset(p, 0xA5, b);
+                        return p;
+                    };
+                    A.release = [](uint8_t* p) { std::free(p); };
+                    FastaData X = parseFastaParallel(path, sigma, nt, piece, FastaForm::kCodes2, &A);
+                    ok = ok && X.ranks.empty() && X.codesBytes == E.ranks.size() && X.offs == E.offs &&
+                         X.nPos == E.nPos && X.bad == E.bad && X.badRecord == E.badRecord && X.badPos == E.badPos &&
+                         (E.ranks.empty() || std::equal(E.ranks.begin(), E.ranks.end(), X.codes));
+                    std::free(X.codes);
                 }
                 if (!ok) {
                     std::printf("mismatch: iteration %d piece %zu threads %u (%s | %s)\n", it, piece, nt, werr.c_str(),
