@@ -11,6 +11,12 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: larger CPU cases")
+    # A test that hangs fails after this long with every thread's stack
+    # (pytest-timeout's thread method: it can interrupt a test stuck in a GPU
+    # call) instead of holding the run; --timeout on the command line wins.
+    if hasattr(config.option, "timeout") and not config.option.timeout:
+        config.option.timeout = 150
+        config.option.timeout_method = "thread"
 
 
 @pytest.fixture(scope="session")

@@ -83,9 +83,14 @@ def _ordered(h):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch,chunk", [(None, None), ("997", "64"), ("211", "100")])
-def test_packed_calls_equal_rank_calls(gpu_device, monkeypatch, batch, chunk):
-    for var, val in (("SAHARA_BATCH", batch), ("SAHARA_UPLOAD_CHUNK", chunk)):
+@pytest.mark.parametrize("batch,chunk,ramp,ramp_end", [(None, None, None, None), ("997", "64", None, None),
+                                                       ("211", "100", None, None), ("997", "64", None, "0"),
+                                                       ("997", "150", "300:7", "500:1:3")])
+def test_packed_calls_equal_rank_calls(gpu_device, monkeypatch, batch, chunk, ramp, ramp_end):
+    """(streamed calls end on smaller batches by default, pass.cpp; SAHARA_RAMP /
+    SAHARA_RAMP_END set the first and last batches, "0": none)"""
+    for var, val in (("SAHARA_BATCH", batch), ("SAHARA_UPLOAD_CHUNK", chunk), ("SAHARA_RAMP", ramp),
+                     ("SAHARA_RAMP_END", ramp_end)):
         if val:
             monkeypatch.setenv(var, val)
     flat, lens, reads, sch = _setup()
