@@ -163,18 +163,8 @@ unsigned hostThreads(const Ctx* c, unsigned cap) {
 }
 
 Ctx* newCtx(int device) {
-    // (SAHARA_TIMING: where a context's creation goes; the first HIP call of
-    // a process starts the runtime)
-    const bool timing = std::getenv("SAHARA_TIMING") != nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    auto ms = [&t0] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
-    std::vector<std::pair<const char*, double>> marks;
-    auto mark = [&](const char* w) {
-        if (timing) marks.emplace_back(w, ms());
-    };
     int n = 0;
     SH_HIP(hipGetDeviceCount(&n));
-    mark("runtime");
     const int hipDev = mapDevice(device);
     if (hipDev < 0 || hipDev >= n)
         throw Error("no HIP device " + std::to_string(hipDev) + " (found " + std::to_string(n) + ")");
@@ -187,43 +177,14 @@ Ctx* newCtx(int device) {
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
         throw Error(std::string("libsahara_hip is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
     c->numCU = prop.multiProcessorCount;
-    mark("device");
     SH_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    mark("stream");
-    // The other five streams are created on a thread of their own, beside
-    // the index load (each took ~70 ms in a fresh process: 0.4 s of the CLI's
-    // load); stE first, for the load's reverse-BWT upload. (No stream gets a
-    // CU mask: with a CU-masked stream in the process the memory-bound
-    // kernels on the other streams ran 1.4-1.8x longer, r5.)
-    {
-        Ctx* raw = c.get();
-        auto side = std::make_shared<std::promise<void>>();
-        raw->sideReady = side->get_future().share();
-        raw->streamsInit = std::thread([raw, side, timing, t0] {
-            try {
-                SH_HIP(hipSetDevice(raw->device));
-                SH_HIP(hipStreamCreateWithFlags(&raw->stE, hipStreamNonBlocking));
-                side->set_value();
-                SH_HIP(hipStreamCreateWithFlags(&raw->stB, hipStreamNonBlocking));
-                SH_HIP(hipStreamCreateWithFlags(&raw->stC, hipStreamNonBlocking));
-                SH_HIP(hipStreamCreateWithFlags(&raw->stD, hipStreamNonBlocking));
-                SH_HIP(hipStreamCreateWithFlags(&raw->stF, hipStreamNonBlocking));
-                // (also first uses of the runtime: 0.1-0.3 s in a fresh process)
-                for (void*& p : raw->outStage) SH_HIP(hipHostMalloc(&p, Ctx::kOutChunk));
-                raw->counters.reserve(kCounters);
-                SH_HIP(hipMemset(raw->counters.ptr, 0, kCounters * sizeof(unsigned long long)));
-                if (timing)
-                    std::fprintf(stderr, "[sahara] context streams ready at %.1f ms\n",
-                                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-            } catch (const std::exception& e) {
-                raw->streamsErr = e.what();
-                try {
-                    side->set_value();
-                } catch (...) {
-                }
-            }
-        });
-    }
+    // (No stream gets a CU mask: with a CU-masked stream in the process the
+    // memory-bound kernels on the other streams ran 1.4-1.8x longer, r5.)
+    SH_HIP(hipStreamCreateWithFlags(&c->stB, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stC, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stD, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stE, hipStreamNonBlocking));
+    SH_HIP(hipStreamCreateWithFlags(&c->stF, hipStreamNonBlocking));
     for (auto& e : c->ev) SH_HIP(hipEventCreate(&e));
     for (auto& e : c->evSleep) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     for (auto& e : c->ringEv) SH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -249,13 +210,10 @@ Ctx* newCtx(int device) {
         sl.small.reserve(8);
         sl.queues.reserve(768);
     }
+    for (void*& p : c->outStage) SH_HIP(hipHostMalloc(&p, Ctx::kOutChunk));
     c->small.reserve(8);
-    mark("events");
-    if (timing) {
-        std::fprintf(stderr, "[sahara] context (ms since its start):");
-        for (auto& m : marks) std::fprintf(stderr, " %s %.1f", m.first, m.second);
-        std::fprintf(stderr, "\n");
-    }
+    c->counters.reserve(kCounters);
+    SH_HIP(hipMemset(c->counters.ptr, 0, kCounters * sizeof(unsigned long long)));
     return c.release();
 }
 
@@ -263,7 +221,6 @@ Ctx* ctxOf(void* p) {
     if (!p) throw Error("null context");
     Ctx* c = static_cast<Ctx*>(p);
     SH_HIP(hipSetDevice(c->device));
-    c->ready();
     return c;
 }
 
@@ -284,19 +241,13 @@ Ctx* openImage(int device, const uint8_t* buf, size_t bytes) {
     const HostUpload viaRing = [raw](void* dst, const void* src, size_t n, hipStream_t s) {
         uploadViaRing(raw, dst, src, n, s);
     };
-    // the load's second stream: the context's stE once it exists
-    const std::function<hipStream_t()> side = [raw] {
-        raw->sideReady.wait();
-        if (!raw->stE) raw->ready();  // (its creation failed: throws)
-        return raw->stE;
-    };
     const char* lr = std::getenv("SAHARA_LOAD_RING");
     const HostUpload* up = lr && std::atoi(lr) == 0 ? nullptr : &viaRing;
     for (size_t p = 0; p < parts.size(); ++p) {
         const IdxParts& P = parts[p];
         if (p) c->more.emplace_back();
         buildFromParts(partOf(c.get(), (uint32_t)p), P.sigma, P.n, P.recLens.data(), P.recLens.size(), P.rate, P.bwtF,
-                       P.bwtR, P.sampled, P.samples, P.nsamples, c->st, parts.size() == 1, up, &side);
+                       P.bwtR, P.sampled, P.samples, P.nsamples, c->st, parts.size() == 1, up);
         c->partRec0.push_back(rec0);
         rec0 += P.recLens.size();
         nmax = std::max(nmax, P.n);
@@ -305,7 +256,6 @@ Ctx* openImage(int device, const uint8_t* buf, size_t bytes) {
         const uint32_t K = kmerDepth(nmax, (uint32_t)parts.size());
         for (uint32_t p = 0; p < parts.size(); ++p) buildKmerTable(partOf(c.get(), p), K, c->st);
     }
-    c->ready();
     return c.release();
 }
 
@@ -346,7 +296,6 @@ int sahara_gpu_build(int device, const uint8_t* ranks, const uint64_t* rec_lens,
             const uint32_t K = kmerDepth(nmax, (uint32_t)first.size() - 1);
             for (uint32_t p = 0; p + 1 < first.size(); ++p) buildKmerTable(partOf(c.get(), p), K, c->st);
         }
-        c->ready();
         *ctx = c.release();
     });
 }

@@ -12,7 +12,6 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
-#include <future>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -457,16 +456,6 @@ struct Ctx {
         TaskGroup group;
     } packJobs[kRingSlots];
     std::thread ringInit;                 // pins the ring (started by newCtx)
-    // stB..stF are created beside the index load (a fresh process's stream
-    // creation takes ~70 ms each, one hardware queue apiece); stE first, which
-    // the load's reverse-BWT upload uses (sideReady). ready() joins.
-    std::thread streamsInit;
-    std::shared_future<void> sideReady;
-    std::string streamsErr;
-    void ready() {
-        if (streamsInit.joinable()) streamsInit.join();
-        if (!streamsErr.empty()) throw Error("creating streams: " + streamsErr);
-    }
     uint64_t ringLoadNext = 0;            // uploadViaRing's next slot
     bool ringFailed = false;
     DevBuf<uint32_t> badFlag;             // device rank check of streamed chunks
@@ -525,7 +514,6 @@ struct Ctx {
         // the pinning thread assigns ring and downRing: it must be done before
         // either is read (a context closed or failed right after newCtx)
         if (ringInit.joinable()) ringInit.join();
-        if (streamsInit.joinable()) streamsInit.join();
         expander.reset();
         for (hipEvent_t e : downEv) (void)hipEventDestroy(e);
         for (hipEvent_t e : partEv) (void)hipEventDestroy(e);

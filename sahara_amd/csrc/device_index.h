@@ -126,7 +126,7 @@ using HostUpload = std::function<void(void* dst, const void* src, size_t bytes, 
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec,
                     uint32_t rate, const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits,
                     const uint32_t* samples, uint64_t nsamples, hipStream_t st, bool withKmer = true,
-                    const HostUpload* up = nullptr, const std::function<hipStream_t()>* sideStream = nullptr);
+                    const HostUpload* up = nullptr);
 // depth of the k-mer table for a text of n symbols: floor(log4 n) + 1, at
 // most 16 (a 68.7 GB table at 3 Gbp, where the mean 16-mer occurs 0.7 times:
 // most exact first parts of a search then start as a text task), and at most

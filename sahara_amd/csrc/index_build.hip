@@ -555,8 +555,7 @@ void buildFromText(DeviceIndex& I, const uint8_t* hostRanks, const uint64_t* rec
 
 void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* recLens, uint64_t nrec, uint32_t rate,
                     const uint8_t* bwtF, const uint8_t* bwtR, const uint64_t* sampledBits, const uint32_t* samples,
-                    uint64_t nsamples, hipStream_t st, bool withKmer, const HostUpload* up,
-                    const std::function<hipStream_t()>* sideStream) {
+                    uint64_t nsamples, hipStream_t st, bool withKmer, const HostUpload* up) {
     auto upload = [up](void* dst, const void* src, size_t bytes, hipStream_t s) {
         if (up) (*up)(dst, src, bytes, s);
         else SH_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
@@ -636,21 +635,15 @@ void buildFromParts(DeviceIndex& I, uint32_t sigma, uint64_t n, const uint64_t* 
     SH_HIP(hipGetLastError());
     phase("text");
     {
-        struct Side {  // the reverse BWT's upload stream (the caller's, or its own) and the event st waits on
+        struct Side {  // the reverse BWT's upload stream and the event st waits on
             hipStream_t s = nullptr;
             hipEvent_t e = nullptr;
-            bool own = false;
             ~Side() {
                 if (e) (void)hipEventDestroy(e);
-                if (s && own) (void)hipStreamDestroy(s);
+                if (s) (void)hipStreamDestroy(s);
             }
         } side;
-        if (sideStream) {
-            side.s = (*sideStream)();
-        } else {
-            SH_HIP(hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking));
-            side.own = true;
-        }
+        SH_HIP(hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking));
         SH_HIP(hipEventCreateWithFlags(&side.e, hipEventDisableTiming));
         bwtRev.reserve(n + 64);
         upload(bwtRev.ptr, bwtR, n, side.s);
