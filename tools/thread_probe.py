@@ -2,7 +2,7 @@
 call (sahara_gpu_search_packed_compact) timed on a context built on the main
 thread and on one built on a helper thread that has exited since, alternating.
 
-usage: python tools/thread_probe.py [--config c3] [--rounds 2] [--steps 5]
+usage: python tools/thread_probe.py [--config c3] [--rounds 2] [--steps 5] [--exited] [--alive]
 """
 import argparse
 import os
@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--exited", action="store_true", help="also a context built on a helper thread that has exited")
+    ap.add_argument("--alive", action="store_true", help="also a helper thread that builds, searches and closes")
     a = ap.parse_args()
     import bench
     import sahara_amd as sa
@@ -29,21 +31,36 @@ def main():
     scheme = sa.search_scheme(gen, 0, k, rlen, hamming=not edit)
     packed = sa.pack_reads(reads, 6, pinned=True)
     idx = {"main": sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=0)}
-    holder = {}
-    t = threading.Thread(target=lambda: holder.update(i=sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=0)))
-    t.start()
-    t.join()
-    idx["helper"] = holder["i"]
-    del flat
+    if a.exited:  # (two resident indexes: ~180 GB of HBM at C3)
+        holder = {}
+        t = threading.Thread(target=lambda: holder.update(i=sa.BiFMIndex.build_flat(flat, lens, sigma=6, device=0)))
+        t.start()
+        t.join()
+        idx["helper"] = holder["i"]
+    flat0 = flat
+    def timed(ix):
+        for _ in range(2):
+            sa.search_packed_compact(ix, packed, scheme, edit=edit).close()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            sa.search_packed_compact(ix, packed, scheme, edit=edit).close()
+        return nreads * a.steps / (time.perf_counter() - t0)
     for r in range(a.rounds):
         for name, ix in idx.items():
-            for _ in range(2):
-                sa.search_packed_compact(ix, packed, scheme, edit=edit).close()
-            t0 = time.perf_counter()
-            for _ in range(a.steps):
-                sa.search_packed_compact(ix, packed, scheme, edit=edit).close()
-            el = time.perf_counter() - t0
-            print(f"round {r} context built on {name:6s} thread: {nreads * a.steps / el / 1e6:8.1f}M reads/s", flush=True)
+            print(f"round {r} context built on {name:6s} thread: {timed(ix) / 1e6:8.1f}M reads/s", flush=True)
+        if not a.alive:
+            continue
+        # a helper thread that builds a context and searches on it while alive
+        out = {}
+
+        def alive():
+            ix = sa.BiFMIndex.build_flat(flat0, lens, sigma=6, device=0)
+            out["v"] = timed(ix)
+            ix.close()
+        t = threading.Thread(target=alive)
+        t.start()
+        t.join()
+        print(f"round {r} context built and searched on a live helper thread: {out['v'] / 1e6:8.1f}M reads/s", flush=True)
 
 
 if __name__ == "__main__":
