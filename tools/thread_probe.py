@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--exited", action="store_true", help="also a context built on a helper thread that has exited")
     ap.add_argument("--alive", action="store_true", help="also a helper thread that builds, searches and closes")
+    ap.add_argument("--env", default="", help="VAR=VAL,... set for a second pass of every case")
     a = ap.parse_args()
     import bench
     import sahara_amd as sa
@@ -44,7 +45,12 @@ def main():
         t0 = time.perf_counter()
         for _ in range(a.steps):
             sa.search_packed_compact(ix, packed, scheme, edit=edit).close()
-        return nreads * a.steps / (time.perf_counter() - t0)
+        v = nreads * a.steps / (time.perf_counter() - t0)
+        st = ix.stats()
+        print(f"    ({threading.current_thread().name}: stage {st['stage_ms']:.2f} ms, text {st['text_ms']:.2f} ms, "
+              f"search {st['search_ms']:.2f} ms, locate {st['locate_ms']:.2f} ms, chunks {list(st['upload_chunks'])}, "
+              f"total {st['total_ms']:.2f} ms)", flush=True)
+        return v
     for r in range(a.rounds):
         for name, ix in idx.items():
             print(f"round {r} context built on {name:6s} thread: {timed(ix) / 1e6:8.1f}M reads/s", flush=True)
