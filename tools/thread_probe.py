@@ -48,7 +48,7 @@ def main():
         v = nreads * a.steps / (time.perf_counter() - t0)
         st = ix.stats()
         print(f"    ({threading.current_thread().name}: stage {st['stage_ms']:.2f} ms, text {st['text_ms']:.2f} ms, "
-              f"search {st['search_ms']:.2f} ms, locate {st['locate_ms']:.2f} ms, chunks {list(st['upload_chunks'])}, "
+              f"search {st['search_ms']:.2f} ms (grid {st['search_grid']}, launches {st['search_launches']}), text grid {st['text_grid']}, locate {st['locate_ms']:.2f} ms, chunks {list(st['upload_chunks'])}, "
               f"total {st['total_ms']:.2f} ms)", flush=True)
         return v
     for r in range(a.rounds):
