@@ -1,4 +1,4 @@
-"""Python model of kSearchText's chain micro-step (sahara_amd/csrc/search.hip).
+"""Python model of kSearchTextBatch's chain micro-step (sahara_amd/csrc/search.hip).
 
 Test infrastructure: `chain()` restates, one node at a time and with Python
 sets instead of nibble masks, what a lane of the text kernel does per
