@@ -2,6 +2,8 @@
 # SAHARA_COPY_STREAMS=shared (4 streams per context) against own copy
 # streams (6): the thread probe (a second context in the process) and the
 # bench line, alternating, one process each.
+# (SAHARA_COPY_STREAMS lived in capi.cpp newCtx for the r6 experiment and was removed
+# again; profiles/r06_copy_streams_ab.txt holds the results)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" || exit 1
